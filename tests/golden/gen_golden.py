@@ -1,0 +1,200 @@
+"""Generate golden fixtures by running the REFERENCE VAESNe package on CPU.
+
+Run (this container only; /root/reference does not exist on the GPU box):
+    cd /tmp && PYTHONPATH=/root/reference/package PYTHONDONTWRITEBYTECODE=1 \
+        python /root/repo/tests/golden/gen_golden.py /root/repo/tests/golden
+
+The reference is imported from its read-only tree and never copied; only the
+numbers it produces are written (small .npz fixtures, inputs + outputs).
+``/root/repo`` must NOT be on sys.path (the build is also called VAESNe).
+
+Determinism recipe: every module is built with dropout=0,
+so one loss evaluation consumes exactly one uniform draw per VAE
+(Laplace.rsample, torch/distributions/laplace.py:83), photometry first.  We
+record those draws by re-seeding and replaying them, so the oracle and the
+HIP build can inject the identical noise.
+"""
+import importlib.util
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+assert not any(os.path.abspath(p) == "/root/repo" for p in sys.path if p), "repo on sys.path"
+
+spec = importlib.util.spec_from_file_location("fill_rule", os.path.join(HERE, "fill_rule.py"))
+fill_rule = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(fill_rule)
+
+from VAESNe.PhotometricVAE import PhotometricVAE  # noqa: E402  (reference package)
+from VAESNe.SpectraVAE import SpectraVAE          # noqa: E402
+from VAESNe.mmVAE import photospecMMVAE           # noqa: E402
+from VAESNe.losses import m_iwae, _m_iwae, elbo   # noqa: E402
+
+torch.set_num_threads(8)
+
+CASES = {
+    # name: kind, sizes, model kwargs
+    "mmvae_tiny": dict(kind="mmvae", B=2, K=2, Lp=16, Ls=128, nb=6, layers=1, Lz=4, Dz=4,
+                       beta=1.0, selfattn=False, concat=True, steps=3),
+    "mmvae_tiny_noconcat": dict(kind="mmvae", B=2, K=3, Lp=12, Ls=64, nb=3, layers=2, Lz=4, Dz=2,
+                                beta=0.7, selfattn=True, concat=False, steps=2),
+    "mmvae_cfg4": dict(kind="mmvae", B=4, K=2, Lp=60, Ls=982, nb=6, layers=4, Lz=4, Dz=4,
+                       beta=1.0, selfattn=False, concat=True, steps=3),
+    "mmvae_cfg5": dict(kind="mmvae", B=2, K=8, Lp=60, Ls=982, nb=2, layers=4, Lz=4, Dz=4,
+                       beta=0.5, selfattn=True, concat=True, steps=2),
+    "elbo_spec_cfg2": dict(kind="spec", B=4, K=1, Ls=982, layers=4, Lz=4, Dz=4, beta=1.0,
+                           selfattn=False, concat=True, steps=3),
+    "elbo_photo_cfg3": dict(kind="photo", B=4, K=1, Lp=60, nb=2, layers=4, Lz=4, Dz=2, beta=0.5,
+                            selfattn=False, concat=True, steps=3),
+    "elbo_spec_tiny_K3": dict(kind="spec", B=3, K=3, Ls=50, layers=2, Lz=4, Dz=3, beta=2.0,
+                              selfattn=True, concat=True, steps=2),
+}
+
+FULL_GRAD_SUFFIXES = [
+    "dec.generativetransformer.transformerblocks.0.self_attn.in_proj_weight",
+    "dec.generativetransformer.transformerblocks.0.layernorm1.weight",
+    "dec.generativetransformer.get_flux.fc2.weight",
+    "dec.generativetransformer.get_photo.fc2.weight",
+    "enc.inference_transformer.initbottleneck",
+    "enc.inference_transformer.transformerblocks.0.cross_attn.out_proj.weight",
+    "enc.inference_transformer.bandembd.weight",
+    "dec.generativetransformer.bandembd.weight",
+]
+
+
+def build(c):
+    common = dict(latent_len=c["Lz"], latent_dim=c["Dz"], model_dim=32, num_heads=4, ff_dim=32,
+                  num_layers=c["layers"], dropout=0.0, concat=c["concat"])
+    if c["kind"] == "mmvae":
+        photo = PhotometricVAE(num_bands=c["nb"], selfattn=False, **common)
+        specv = SpectraVAE(selfattn=c["selfattn"], **common)
+        model = photospecMMVAE(vaes=[photo, specv], beta=c["beta"])
+    elif c["kind"] == "spec":
+        model = SpectraVAE(selfattn=c["selfattn"], beta=c["beta"], **common)
+    else:
+        model = PhotometricVAE(num_bands=c["nb"], selfattn=c["selfattn"], beta=c["beta"], **common)
+    sd = model.state_dict()
+    new = {}
+    for k, v in sd.items():
+        f = fill_rule.fill(k, tuple(v.shape))
+        new[k] = v.clone() if f is None else torch.from_numpy(f)
+    model.load_state_dict(new)
+    model.train()
+    return model
+
+
+def inputs(c, seed=1234):
+    rng = np.random.default_rng(seed)
+    out = {}
+    if c["kind"] in ("mmvae", "photo"):
+        f, t, b, m = fill_rule.photo_inputs(rng, c["B"], c["Lp"], c["nb"])
+        out.update(pflux=f, ptime=t, pband=b, pmask=m)
+    if c["kind"] in ("mmvae", "spec"):
+        f, w, ph, m = fill_rule.spec_inputs(rng, c["B"], c["Ls"])
+        out.update(sflux=f, swave=w, sphase=ph, smask=m)
+    return out
+
+
+def to_x(c, arr):
+    P = lambda: (torch.from_numpy(arr["pflux"]), torch.from_numpy(arr["ptime"]),
+                 torch.from_numpy(arr["pband"]), torch.from_numpy(arr["pmask"]))
+    S = lambda: (torch.from_numpy(arr["sflux"]), torch.from_numpy(arr["swave"]),
+                 torch.from_numpy(arr["sphase"]), torch.from_numpy(arr["smask"]))
+    if c["kind"] == "mmvae":
+        return [P(), S()]
+    return S() if c["kind"] == "spec" else P()
+
+
+def draws(c, seed):
+    """Replay the uniform draws a loss evaluation consumes after manual_seed(seed)."""
+    torch.manual_seed(seed)
+    eps = torch.finfo(torch.float32).eps
+    shape = (c["K"], c["B"], c["Lz"], c["Dz"])
+    n = 2 if c["kind"] == "mmvae" else 1
+    return [torch.empty(shape).uniform_(eps - 1, 1) for _ in range(n)]
+
+
+def loss_fn(c, model, x):
+    if c["kind"] == "mmvae":
+        return m_iwae(model, x, K=c["K"])
+    return elbo(model, x, K=c["K"])
+
+
+def run_case(name, c, outdir):
+    model = build(c)
+    arr = inputs(c)
+    x = to_x(c, arr)
+    out = dict(arr)
+    out["config"] = np.array(json.dumps(c))
+    seed0 = 7
+    us = draws(c, seed0)
+    for i, u in enumerate(us):
+        out[f"u{i}"] = u.numpy()
+
+    # forward pieces
+    torch.manual_seed(seed0)
+    with torch.no_grad():
+        if c["kind"] == "mmvae":
+            qz, px, zss = model(x, K=c["K"])
+            for m in range(2):
+                out[f"mu{m}"] = qz[m].loc.numpy()
+                out[f"scale{m}"] = qz[m].scale.numpy()
+                out[f"zs{m}"] = zss[m].numpy()
+                for d in range(2):
+                    out[f"loc{m}{d}"] = px[m][d].loc.numpy()
+                    out[f"pxscale{m}{d}"] = px[m][d].scale.numpy()
+            torch.manual_seed(seed0)
+            out["lw"] = _m_iwae(model, x, K=c["K"]).numpy()
+        else:
+            q, pxz, zs = model(x, K=c["K"])
+            out["mu0"], out["scale0"], out["zs0"] = q.loc.numpy(), q.scale.numpy(), zs.numpy()
+            out["loc00"], out["pxscale00"] = pxz.loc.numpy(), pxz.scale.numpy()
+    # value + gradient
+    torch.manual_seed(seed0)
+    loss = -loss_fn(c, model, x)
+    loss.backward()
+    out["loss"] = np.array(loss.item(), dtype=np.float64)
+    names, norms = [], []
+    for k, prm in model.named_parameters():
+        if prm.grad is None:
+            continue
+        names.append(k)
+        norms.append(prm.grad.norm().item())
+        if any(k.endswith(s) for s in FULL_GRAD_SUFFIXES) or name == "mmvae_tiny":
+            out["grad:" + k] = prm.grad.numpy().copy()
+    out["grad_names"] = np.array(json.dumps(names))
+    out["grad_norms"] = np.array(norms, dtype=np.float64)
+
+    # AdamW trajectory from the filled params (fresh model)
+    model = build(c)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+    losses = []
+    for s in range(c["steps"]):
+        seed = 100 + s
+        for i, u in enumerate(draws(c, seed)):
+            out[f"traj_u{s}_{i}"] = u.numpy()
+        torch.manual_seed(seed)
+        opt.zero_grad()
+        loss = -loss_fn(c, model, x)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    out["traj_losses"] = np.array(losses, dtype=np.float64)
+    pn = {k: v.norm().item() for k, v in model.state_dict().items()}
+    out["traj_param_norms"] = np.array(json.dumps(pn))
+    path = os.path.join(outdir, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: loss={out['loss']:.6f} traj={losses} -> {path}")
+
+
+if __name__ == "__main__":
+    outdir = sys.argv[1] if len(sys.argv) > 1 else HERE
+    only = sys.argv[2:]
+    for name, c in CASES.items():
+        if only and name not in only:
+            continue
+        run_case(name, c, outdir)
