@@ -1,0 +1,359 @@
+"""Benchmark: the ZTF photometry+spectra MMVAE training step (BASELINE.json
+configs[4], cannon/ZTF_photospect.py) on N MI355X GPUs, one process per GPU.
+
+One step = m_iwae forward (K=8 importance samples, both encoders, the 2x2
+cross-modal decoder matrix, dropout 0.1 in train mode) + backward + one RCCL
+all-reduce of the flat gradient (N>1) + FusedAdamW update, on a fixed
+per-GPU batch of 16 synthetic (light curve, spectrum) pairs already resident
+in HBM (weak scaling).  The step is captured once as a hipGraph and replayed.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-graph]
+                    [--no-cpu-baseline]
+
+Rank 0 prints ONE JSON line (value = whole-job SN pairs/s).  Beside it:
+  roofline     : the dominant kernel (spectra-decoder masked self-attention
+                 backward) timed with HIP events on its own stream, its
+                 algorithmic FLOPs / average launch time vs the FP32 peak;
+  cpu_baseline : the CPU oracle (pure-PyTorch restatement of the reference,
+                 oracle/vaesne_oracle.py) timed on the host cores on a bounded
+                 sample (rank 0, N=1 only);
+  elbo_rel_err : |loss_build - loss_ref| / |loss_ref| on the reference's own
+                 cfg-5 golden fixture (dropout off, injected noise).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "vaesne-dev_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 matrix peak (spec)
+HBM_PEAK_GBS = 8000.0
+
+CFG = dict(workload="ZTF_photospect MMVAE training step (cfg 5)", num_bands=2, latent_len=4,
+           latent_dim=4, model_dim=32, num_heads=4, ff_dim=32, num_layers=4, dropout=0.1,
+           beta=0.5, K=8, Lp=60, Ls=982, spectra_selfattn=True, lr=1e-3)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_model(device, dropout):
+    from VAESNe.PhotometricVAE import PhotometricVAE
+    from VAESNe.SpectraVAE import SpectraVAE
+    from VAESNe.mmVAE import photospecMMVAE
+    c = CFG
+    common = dict(latent_len=c["latent_len"], latent_dim=c["latent_dim"], model_dim=c["model_dim"],
+                  num_heads=c["num_heads"], ff_dim=c["ff_dim"], num_layers=c["num_layers"],
+                  dropout=dropout)
+    spec = SpectraVAE(selfattn=c["spectra_selfattn"], spectra_length=c["Ls"], **common)
+    photo = PhotometricVAE(num_bands=c["num_bands"], selfattn=False, photometric_length=c["Lp"],
+                           **common)
+    return photospecMMVAE(vaes=[photo, spec], beta=c["beta"]).to(device)
+
+
+def synthetic_batch(B, seed, device):
+    """SURVEY.md §8(d) synthetic inputs (tests/golden/fill_rule.py recipe)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("fill_rule", os.path.join(ROOT, "tests", "golden", "fill_rule.py"))
+    fr = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(fr)
+    rng = np.random.default_rng(seed)
+    pf, pt, pb, pm = fr.photo_inputs(rng, B, CFG["Lp"], CFG["num_bands"])
+    sf, sw, sp, sm = fr.spec_inputs(rng, B, CFG["Ls"])
+    T = lambda a: torch.from_numpy(a).to(device)
+    return [(T(pf), T(pt), T(pb), T(pm)), (T(sf), T(sw), T(sp), T(sm))]
+
+
+class Step:
+    """fwd + bwd + pack (graph 1) | all-reduce (N>1) | AdamW update + RNG advance (graph 2)."""
+
+    def __init__(self, model, x, device, world, use_graph):
+        from VAESNe import rng
+        from VAESNe.distributed import GradAllReduce
+        from VAESNe.losses import m_iwae
+        from VAESNe.optim import FusedAdamW
+        self.model, self.x, self.device, self.world = model, x, device, world
+        self.m_iwae, self.rng = m_iwae, rng
+        self.opt = FusedAdamW([p for p in model.parameters() if p.requires_grad], lr=CFG["lr"],
+                              grad_hook=GradAllReduce("sum") if world > 1 else None)
+        self.loss = torch.zeros((), device=device)
+        self.graphs = None
+        self.use_graph = use_graph
+        model.train()
+
+    def fwd_bwd(self):
+        self.opt.zero_grad(set_to_none=True)
+        loss = -self.m_iwae(self.model, self.x, K=CFG["K"])
+        loss.backward()
+        self.opt.pack_grads()
+        self.loss.copy_(loss.detach())
+
+    def update(self):
+        self.opt.apply_update()
+        self.rng.advance(self.device)   # fresh sampler / dropout draws next step
+
+    def eager(self):
+        self.fwd_bwd()
+        self.opt.reduce_grads()
+        self.update()
+
+    def capture(self):
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                self.eager()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        if self.world == 1:
+            with torch.cuda.graph(g1):
+                self.fwd_bwd()
+                self.update()
+            self.graphs = (g1, None)
+        else:
+            with torch.cuda.graph(g1):
+                self.fwd_bwd()
+            with torch.cuda.graph(g2):
+                self.update()
+            self.graphs = (g1, g2)
+
+    def __call__(self):
+        if self.graphs is None:
+            self.eager()
+            return
+        g1, g2 = self.graphs
+        g1.replay()
+        if g2 is not None:
+            self.opt.reduce_grads()
+            g2.replay()
+
+
+def time_kernel(fn, iters, device):
+    """Average duration of fn's launches, HIP events on the stream they run on."""
+    s = torch.cuda.Stream(device)
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(iters):
+            fn()
+        e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def roofline(device, B):
+    """Spectra-decoder masked self-attention (N = K*B sequences x 982 tokens,
+    4 heads x dh 8, dropout 0.1), the dominant op of the step.
+    Algorithmic FLOPs: forward 4*dh per score (QK^T + PV), backward 8*dh per
+    score (S, dP, dV, dK, dQ products: recompute of S included as the
+    flash-backward's algorithmic work is usually quoted without it -> 4 products
+    = 8*dh counted here)."""
+    from VAESNe import _lib, rng
+    N, L, E, H, dh = CFG["K"] * B, CFG["Ls"], CFG["model_dim"], CFG["num_heads"], 8
+    qkv = torch.randn(N, L, 3 * E, device=device)
+    mask = (torch.rand(N, L, device=device) < 0.05)
+    mask[:, 0] = False
+    mask = mask.view(torch.uint8)
+    o = torch.empty(N, L, E, device=device)
+    lse = torch.empty(N, H, L, device=device)
+    do = torch.randn(N, L, E, device=device)
+    dqkv = torch.empty_like(qkv)
+    ws = torch.empty(N * H * L, device=device)
+    st = rng.state(device)
+    b, d = qkv.data_ptr(), dqkv.data_ptr()
+    lib, s3 = _lib.lib, L * 3 * E
+
+    def fwd():
+        lib.attn_fwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E, mask.data_ptr(), L,
+                     o.data_ptr(), L * E, E, lse.data_ptr(), N, H, L, L, dh, 0.1, st.data_ptr(), 7,
+                     _lib.stream())
+
+    def bwd():
+        lib.attn_bwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E, mask.data_ptr(), L,
+                     o.data_ptr(), L * E, E, lse.data_ptr(), do.data_ptr(), L * E, E,
+                     d, s3, 3 * E, d + 4 * E, s3, 3 * E, d + 8 * E, s3, 3 * E,
+                     N, H, L, L, dh, 0.1, st.data_ptr(), 7, ws.data_ptr(), _lib.stream())
+
+    t_f = time_kernel(fwd, 20, device)
+    t_b = time_kernel(bwd, 20, device)
+    scores = N * H * L * L
+    f_fwd = scores * 4 * dh
+    f_bwd = scores * 8 * dh
+    res = dict(
+        fwd=dict(kernel="attn_fwd_kernel", ms=t_f * 1e3, tflops=f_fwd / t_f / 1e12),
+        bwd=dict(kernel="attn_bwd (pre+kv+q)", ms=t_b * 1e3, tflops=f_bwd / t_b / 1e12))
+    dom = "bwd" if t_b >= t_f else "fwd"
+    a = res[dom]["tflops"]
+    return dict(bound="mfma", kernel=res[dom]["kernel"], achieved=round(a, 3),
+                peak=FP32_PEAK_TFLOPS, unit="TFLOP/s", frac=round(a / FP32_PEAK_TFLOPS, 4),
+                traffic=None, launch_ms=round(res[dom]["ms"], 4),
+                flops_per_launch=f_bwd if dom == "bwd" else f_fwd,
+                detail={k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
+                            for kk, vv in v.items()} for k, v in res.items()},
+                note="fp32 VALU kernel; peak = FP32 157.3 TF (vector = matrix rate on gfx950); "
+                     "scores per launch = K*B*H*982^2")
+
+
+def cpu_baseline(sample_B=2, steps=2):
+    """The oracle (CPU restatement of the reference) on the same workload:
+    cfg-5 shapes, K=8, dropout 0.1 train mode, AdamW; bounded sample."""
+    from oracle import vaesne_oracle as O
+    torch.set_num_threads(max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))))
+    c = CFG
+    common = dict(latent_len=c["latent_len"], latent_dim=c["latent_dim"], model_dim=c["model_dim"],
+                  num_heads=c["num_heads"], ff_dim=c["ff_dim"], num_layers=c["num_layers"])
+    cfg = O.MMVAECfg(photo=O.VaeCfg("photo", num_bands=c["num_bands"], **common),
+                     spec=O.VaeCfg("spec", selfattn=True, **common), beta=c["beta"])
+    g = torch.Generator().manual_seed(0)
+    p = O.make_params(cfg, lambda k, shp: (torch.randn(shp, generator=g) / math.sqrt(shp[-1])).numpy()
+                      if "_pz" not in k else None, requires_grad=True)
+    x = synthetic_batch(sample_B, 99, "cpu")
+    st = O.AdamWState(lr=c["lr"])
+    eps = torch.finfo(torch.float32).eps
+
+    def one():
+        us = [torch.empty(c["K"], sample_B, c["latent_len"], c["latent_dim"]).uniform_(eps - 1, 1)
+              for _ in range(2)]
+        for v in p.values():
+            v.grad = None
+        loss, _, _ = O.m_iwae(p, cfg, x, c["K"], us, p_drop=c["dropout"], training=True)
+        (-loss).backward()
+        O.adamw_step(p, {k: v.grad for k, v in p.items() if v.requires_grad}, st)
+
+    one()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    dt = time.perf_counter() - t0
+    return dict(value=round(sample_B * steps / dt, 4), unit="SN pairs/s", cores=torch.get_num_threads(),
+                kind="port", sample=f"{steps} oracle training steps of {sample_B} pairs (cfg-5 shapes, "
+                                    f"K=8, dropout 0.1, AdamW) after 1 warm-up step; {dt:.1f}s",
+                cpu=_cpu_model())
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def elbo_rel_err(device):
+    """Loss on the reference's cfg-5 golden fixture (identical params/inputs/u)."""
+    from VAESNe import rng
+    from VAESNe.losses import m_iwae
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from conftest import build_model, golden_us, golden_x, load_golden
+    g = load_golden("mmvae_cfg5")
+    c = g["config"]
+    model = build_model(c, device=device)
+    model.train()
+    with torch.no_grad(), rng.inject_uniform(golden_us(g)):
+        loss = -m_iwae(model, golden_x(g, device), K=c["K"])
+    ref = float(g["loss"])
+    return abs(loss.item() - ref) / abs(ref)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=16, help="per-GPU batch (SN pairs)")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    from VAESNe import _lib, rng
+    from VAESNe.distributed import broadcast_parameters
+    _lib.load()
+    torch.manual_seed(0)
+    rng.manual_seed(1234 + rank)
+    model = make_model(device, CFG["dropout"])
+    broadcast_parameters(model)
+    x = synthetic_batch(args.batch, 1234 + rank, device)
+    step = Step(model, x, device, world, use_graph=not args.no_graph)
+    graph = False
+    if not args.no_graph:
+        try:
+            step.capture()
+            graph = True
+        except Exception as e:  # reported in the JSON line, never silent
+            log(f"[bench] hipGraph capture failed ({e!r}); timing eager steps")
+            step.graphs = None
+            torch.cuda.synchronize(device)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    loss = step.loss.item()
+    if not math.isfinite(loss):
+        raise RuntimeError(f"non-finite training loss {loss}")
+    ms = dt / args.steps * 1e3
+    value = world * args.batch * args.steps / dt
+    out = {
+        "metric": "SN pairs/sec/GPU on ZTF photo+spec MMVAE step; ELBO rel-err vs CPU ref",
+        "value": round(value, 2), "unit": "SN pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": CFG["workload"], "per_gpu_batch": args.batch,
+                   "global_batch": args.batch * world, "K": CFG["K"], "seq_len": CFG["Ls"],
+                   "photometry_len": CFG["Lp"], "num_bands": CFG["num_bands"], "beta": CFG["beta"],
+                   "dropout": CFG["dropout"], "spectra_selfattn": True, "parallelism": f"dp{world}",
+                   "hipgraph": graph},
+        "value_per_gpu": round(value / world, 2),
+        "final_loss": loss,
+    }
+    if rank == 0:
+        try:
+            out["elbo_rel_err"] = elbo_rel_err(device)
+        except Exception as e:
+            out["elbo_rel_err"] = None
+            log(f"[bench] elbo_rel_err failed: {e!r}")
+        if not args.no_roofline:
+            out["roofline"] = roofline(device, args.batch)
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

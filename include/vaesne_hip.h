@@ -1,0 +1,185 @@
+/*
+ * vaesne_hip.h — C ABI of libvaesne_hip.so, the gfx950 (MI355X) kernels of the
+ * VAESNe multimodal-VAE training step.
+ *
+ * The reference (YunyiShen/VAESNe-dev) is pure PyTorch and has no FFI: its
+ * "operator API" is nn.Module.forward(x, K) plus loss functions taking
+ * (model, x, K).  Each entry point below replaces the implicit PyTorch eager
+ * op(s) the reference invokes at the cited site; the Python package
+ * vaesne-dev_amd/VAESNe binds them with ctypes behind the
+ * reference's module/loss API.  Paths are relative to
+ * /root/reference/package/VAESNe; torch/ paths are torch 2.10 sources.
+ *
+ * Conventions:
+ *   - every function returns a hipError_t as int (0 = success) and launches
+ *     asynchronously on `stream` (a hipStream_t; pass torch's current stream);
+ *   - tensors are fp32 device pointers with explicit element strides
+ *     (ld* = row stride, *_bs = batch stride); masks are uint8 (1 = ignore);
+ *     band indices are int64;
+ *   - no function allocates: workspaces are caller-provided, sized by the
+ *     matching *_workspace() query;
+ *   - `rng_state` is a device int64[2] {seed, counter}; `call_id` names the
+ *     call site, so (seed, counter, call_id, coordinates) fixes every draw and
+ *     forward/backward regenerate identical dropout masks;
+ *   - all reductions are fixed-order (bitwise reproducible).
+ */
+#ifndef VAESNE_HIP_H
+#define VAESNE_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- token-wise linear layers ------------------------------------------
+ * nn.Linear(K->N) (+ ReLU / exact GELU) on rows of a token matrix:
+ * util_layers.py:9-18 (singlelayerMLP), :20-34 (MLP), :142-149 (sinusoidal
+ * MLP), :275-279 (FFN Linear-GELU-Linear), torch/nn/functional.py:6206
+ * (packed in-projection) and the MHA out_proj.
+ *   y = act((x [+ x2]) W^T + b)   act: 0 none, 1 relu, 2 gelu(erf)
+ *   z (optional) receives the pre-activation; accum: y += ... */
+int vaesne_linear_fwd(const float* x, int64_t ldx, const float* x2, int64_t ldx2, int64_t M,
+                      int K, const float* W, const float* b, int N, float* y, int64_t ldy,
+                      float* z, int64_t ldz, int act, int accum, void* stream);
+/* dx (+)= (dy * act'(z)) W      (autograd of the above) */
+int vaesne_linear_bwd_data(const float* dy, int64_t lddy, const float* z, int64_t ldz, int act,
+                           int64_t M, int N, const float* W, int K, float* dx, int64_t lddx,
+                           int accum, void* stream);
+/* dW (+)= (dy*act'(z))^T (x [+ x2]),  db (+)= colsum(dy*act'(z)) */
+int64_t vaesne_linear_bwd_weight_workspace(int64_t M, int O, int I);
+int vaesne_linear_bwd_weight(const float* dy, int64_t lddy, const float* z, int64_t ldz, int act,
+                             const float* x, int64_t ldx, const float* x2, int64_t ldx2,
+                             int64_t M, int O, int I, float* dW, float* db, int accum,
+                             float* workspace, void* stream);
+
+/* ---- post-LN residual join ------------------------------------------------
+ * TransformerBlock: x = LayerNorm(x + Dropout(res))  util_layers.py:291,298,303,307
+ * (nn.LayerNorm eps 1e-5; nn.Dropout p).  mean/rstd [M] saved for backward. */
+int vaesne_add_ln_fwd(const float* x, int64_t ldx, const float* res, int64_t ldres, int64_t M,
+                      int E, const float* gamma, const float* beta, float p_drop,
+                      const int64_t* rng_state, uint32_t call_id, float* y, int64_t ldy,
+                      float* mean, float* rstd, void* stream);
+int64_t vaesne_add_ln_bwd_workspace(int64_t M, int E);
+int vaesne_add_ln_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx,
+                      const float* res, int64_t ldres, int64_t M, int E, const float* gamma,
+                      const float* mean, const float* rstd, float p_drop,
+                      const int64_t* rng_state, uint32_t call_id, float* dx, int64_t lddx,
+                      int accum_dx, float* dres, int64_t lddres, int accum_dres, float* dgamma,
+                      float* dbeta, int accum_param, float* workspace, void* stream);
+/* out0[f] (+)= sum_g partial[g*F+f] (f < split), out1 likewise (f >= split) */
+int vaesne_reduce_partials(const float* partial, int G, int F, float* out0, float* out1,
+                           int split, int accum, void* stream);
+
+/* ---- masked multi-head attention core ------------------------------------
+ * nn.MultiheadAttention(batch_first=True) as called at util_layers.py:289
+ * (self, key_padding_mask), :297 (context self), :301 (cross); arithmetic of
+ * torch/nn/functional.py:6559-6594: q/sqrt(dh), -inf key mask, softmax,
+ * dropout(p) on the probabilities, P v.  Flash-style: scores never stored.
+ * lse [B,H,Lq] (log2 domain) is saved for the backward.  dh in {8, 16}. */
+int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
+                    int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls,
+                    const uint8_t* kpm, int64_t m_bs, float* o, int64_t o_bs, int64_t o_ls,
+                    float* lse, int B, int H, int Lq, int Lk, int dh, float p_drop,
+                    const int64_t* rng_state, uint32_t call_id, void* stream);
+int64_t vaesne_attn_bwd_workspace(int B, int H, int Lq);
+int vaesne_attn_bwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
+                    int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls,
+                    const uint8_t* kpm, int64_t m_bs, const float* o, int64_t o_bs,
+                    int64_t o_ls, const float* lse, const float* dout, int64_t do_bs,
+                    int64_t do_ls, float* dq, int64_t dq_bs, int64_t dq_ls, float* dk,
+                    int64_t dk_bs, int64_t dk_ls, float* dv, int64_t dv_bs, int64_t dv_ls, int B,
+                    int H, int Lq, int Lk, int dh, float p_drop, const int64_t* rng_state,
+                    uint32_t call_id, float* workspace, void* stream);
+
+/* ---- embeddings ------------------------------------------------------------
+ * [sin(x*div) | cos(x*div)]: util_layers.py:125-129 (plain, 16 freqs) and
+ * :142-146 (MLP form, 32 freqs).  x is read at index r % period, so the
+ * K-fold expand of the decoders (PhotometricVAE.py:190-193,
+ * SpectraVAE.py:189-192) is never materialised. */
+int vaesne_sincos(const float* x, int64_t period, int64_t rows, const float* div, int nf,
+                  float* out, int64_t ldo, void* stream);
+/* nn.Embedding(num_bands, E) lookup (PhotometricLayers.py:63,129) and its
+ * deterministic scatter-add backward (nb <= 16).  out = (base ? base : 0) + table[idx]
+ * (the `time_embd + band_embd` sum of PhotometricLayers.py:64-65 in one pass). */
+int vaesne_embed_fwd(const int64_t* idx, int64_t period, int64_t rows, const float* table, int E,
+                     const float* base, int64_t ldb, float* out, int64_t ldo, void* stream);
+int64_t vaesne_embed_bwd_workspace(int64_t rows, int E, int nb);
+int vaesne_embed_bwd(const int64_t* idx, int64_t period, int64_t rows, const float* dout,
+                     int64_t lddo, int E, int nb, float* dtable, int accum, float* workspace,
+                     void* stream);
+/* out[f] (+)= sum_g in[g*F+f]: backward of x.repeat(B,1,1) (initbottleneck,
+ * PhotometricLayers.py:137-138, SpectraLayers.py:134-135) */
+int vaesne_sum_leading(const float* in, int G, int F, float* out, int accum, void* stream);
+
+/* ---- posterior, sampler, likelihood scale --------------------------------- */
+/* mu = b[:, :Lz], scale = softplus(b[:, Lz:])  PhotometricVAE.py:53-54, SpectraVAE.py:48-49 */
+int vaesne_latent_head_fwd(const float* bott, int B, int n, float* mu, float* scale,
+                           void* stream);
+int vaesne_latent_head_bwd(const float* bott, int B, int n, const float* dmu,
+                           const float* dscale, float* dbott, void* stream);
+/* u ~ U(eps-1, 1) (laplace.py:83) from the counter RNG */
+int vaesne_uniform(float* u, int64_t n, const int64_t* rng_state, uint32_t call_id,
+                   void* stream);
+/* Laplace.rsample: z = loc - scale*sign(u)*log1p(-|u|)  laplace.py:74-86
+ * (PhotometricVAE.py:162-163, SpectraVAE.py:151-152), z [K, n] */
+int vaesne_rsample_fwd(const float* loc, const float* scale, const float* u, int K, int64_t n,
+                       float* z, void* stream);
+int vaesne_rsample_bwd(const float* dz, const float* u, int K, int64_t n, float* dloc,
+                       float* dscale, void* stream);
+/* px scale = 1 + big*mask, repeated K times: PhotometricVAE.py:91-93 (1e8),
+ * SpectraVAE.py:84-86 (1e10) */
+int vaesne_mask_scale(const uint8_t* mask, int64_t n, int K, float big, float* out,
+                      void* stream);
+
+/* ---- objectives -------------------------------------------------------------
+ * _m_iwae: losses.py:47-62 -> lw [2K, B]; the per-cell likelihood is
+ * Laplace.log_prob (laplace.py:88-91) of the reference's px_zs[r][d] objects.
+ * Array arguments are HOST arrays of device pointers: x[2] ([B,L_d] flux),
+ * llik[2], L[2], loc[4]/scale[4] (index 2r+d, [K,B,L_d]), zs[2] ([K,B,n]),
+ * mu[2]/sc[2] ([B,n], the two posteriors), n = latent_len*latent_dim.
+ * _bwd takes dL/dlw [2K,B] and writes dloc[4], dzs[2], dmu[2], dsc[2]
+ * (null entries are skipped). */
+int vaesne_iwae_lw_fwd(const float* const* x, const float* llik, const int* L,
+                       const float* const* loc, const float* const* scale,
+                       const float* const* zs, const float* const* mu, const float* const* sc,
+                       const float* pz_loc, const float* pz_scale, int K, int B, int n,
+                       float* lw, void* stream);
+int vaesne_iwae_lw_bwd(const float* const* x, const float* llik, const int* L,
+                       const float* const* loc, const float* const* scale,
+                       const float* const* zs, const float* const* mu, const float* const* sc,
+                       const float* pz_loc, const float* pz_scale, int K, int B, int n,
+                       const float* dlw, float* const* dloc, float* const* dzs,
+                       float* const* dmu, float* const* dsc, void* stream);
+/* m_iwae's reduction: loss = sum_b log_mean_exp_j lw[j, b]  (losses.py:92-93,
+ * util_layers.py:326-327); bwd: dlw = g * softmax_j lw[:, b], g read on device. */
+int vaesne_lme_sum_fwd(const float* lw, int J, int B, float* loss, void* stream);
+int vaesne_lme_sum_bwd(const float* lw, int J, int B, const float* gout, float* dlw,
+                       void* stream);
+/* elbo: losses.py:16-24 with the closed-form Laplace KL of
+ * util_layers.py:330-336 -> torch/distributions/kl.py:331-338; lpx [K,B]
+ * workspace, loss = mean(lpx) - mean_b sum_j KL. */
+int vaesne_elbo_fwd(const float* x, int L, float llik, const float* loc, const float* scale,
+                    const float* mu, const float* sc, const float* pz_loc,
+                    const float* pz_scale, int K, int B, int n, float* lpx, float* loss,
+                    void* stream);
+int vaesne_elbo_bwd(const float* x, int L, float llik, const float* loc, const float* scale,
+                    const float* mu, const float* sc, const float* pz_loc,
+                    const float* pz_scale, int K, int B, int n, const float* gout,
+                    float* dloc, float* dmu, float* dsc, void* stream);
+
+/* ---- optimizer / step plumbing ----------------------------------------------
+ * torch.optim.AdamW (the scripts' optimizer, e.g. cannon/test_photospectra.py:133)
+ * over one flat fp32 parameter buffer; `step` is a device float incremented by
+ * vaesne_step_advance (which also advances rng_state[1]), so the whole step can
+ * be captured in a hipGraph. */
+int vaesne_adamw(float* p, const float* g, float* m, float* v, int64_t n, const float* step,
+                 float lr, float b1, float b2, float eps, float wd, void* stream);
+int vaesne_step_advance(float* step, int64_t* rng_state, void* stream);
+/* gather (unpack=0) / scatter (unpack=1) `count` tensors to/from a flat buffer */
+int vaesne_pack(const float* const* srcs, const int64_t* offs, const int64_t* ns, int count,
+                float* dst, int unpack, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VAESNE_HIP_H */

@@ -1,0 +1,250 @@
+"""Per-kernel parity of libvaesne_hip.so against the CPU oracle (fp64 torch
+restatement of the reference arithmetic), on random shapes and the edge cases
+the reference's data produce: ragged key padding masks, a single unmasked key,
+L not a multiple of any tile, the 983-token encoder context, Lk = 4/5 context
+tokens, and dropout (mask statistics and forward/backward mask agreement)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import vaesne_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def _mha_params(E, seed):
+    g = torch.Generator().manual_seed(seed)
+    return {"a.in_proj_weight": torch.randn(3 * E, E, generator=g) / math.sqrt(E),
+            "a.in_proj_bias": 0.1 * torch.randn(3 * E, generator=g),
+            "a.out_proj.weight": torch.randn(E, E, generator=g) / math.sqrt(E),
+            "a.out_proj.bias": 0.1 * torch.randn(E, generator=g)}
+
+
+def _rand_mask(B, L, p, g, keep_first=True):
+    m = torch.rand(B, L, generator=g) < p
+    if keep_first:
+        m[:, 0] = False
+    return m
+
+
+@pytest.mark.parametrize("B,Lq,Lk,self_attn,pm", [
+    (3, 982, 982, True, 0.05),     # spectra decoder self-attention
+    (2, 983, 983, True, 0.05),     # spectra encoder context self-attention (cfg 5)
+    (4, 60, 60, True, 0.1),        # photometry decoder self-attention
+    (3, 8, 983, False, 0.05),      # encoder cross-attention (queries = latent tokens)
+    (5, 982, 5, False, 0.0),       # spectra decoder cross-attention (4 latent + phase)
+    (2, 37, 1, False, 0.0),        # a single key
+    (2, 300, 257, False, 0.9),     # heavy ragged masking
+])
+def test_mha_forward_backward_vs_oracle(B, Lq, Lk, self_attn, pm):
+    from VAESNe.util_layers import MultiheadAttention
+    E, H = 32, 4
+    g = torch.Generator().manual_seed(B * 1000 + Lq + Lk)
+    p64 = {k: v.double() for k, v in _mha_params(E, Lq + Lk).items()}
+    xq = torch.randn(B, Lq, E, generator=g, dtype=torch.float64)
+    xk = xq if self_attn else torch.randn(B, Lk, E, generator=g, dtype=torch.float64)
+    mask = _rand_mask(B, Lk, pm, g) if pm > 0 else None
+    # oracle (fp64, CPU)
+    pr = {k: v.clone().requires_grad_(True) for k, v in p64.items()}
+    xq_r = xq.clone().requires_grad_(True)
+    xk_r = xq_r if self_attn else xk.clone().requires_grad_(True)
+    ref = O.multihead_attention(pr, "a", xq_r, xk_r, mask, H)
+    go = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    (ref * go).sum().backward()
+    # HIP
+    mha = MultiheadAttention(E, H, dropout=0.0, batch_first=True).to(DEV)
+    with torch.no_grad():
+        mha.in_proj_weight.copy_(p64["a.in_proj_weight"].float())
+        mha.in_proj_bias.copy_(p64["a.in_proj_bias"].float())
+        mha.out_proj.weight.copy_(p64["a.out_proj.weight"].float())
+        mha.out_proj.bias.copy_(p64["a.out_proj.bias"].float())
+    xq_d = xq.float().to(DEV).requires_grad_(True)
+    xk_d = xq_d if self_attn else xk.float().to(DEV).requires_grad_(True)
+    out, _ = mha(xq_d, xk_d, xk_d, key_padding_mask=None if mask is None else mask.to(DEV))
+    (out * go.float().to(DEV)).sum().backward()
+    assert _rel(out, ref) < 2e-5
+    assert _rel(xq_d.grad, xq_r.grad) < 1e-4
+    if not self_attn:
+        assert _rel(xk_d.grad, xk_r.grad) < 1e-4
+    assert _rel(mha.in_proj_weight.grad, pr["a.in_proj_weight"].grad) < 1e-4
+    assert _rel(mha.out_proj.weight.grad, pr["a.out_proj.weight"].grad) < 1e-4
+    # q/v bias grads (the k-bias grad is analytically 0)
+    E_ = E
+    bref = pr["a.in_proj_bias"].grad
+    bgot = mha.in_proj_bias.grad
+    assert _rel(bgot[:E_], bref[:E_]) < 1e-4 and _rel(bgot[2 * E_:], bref[2 * E_:]) < 1e-4
+    assert bgot[E_:2 * E_].abs().max().item() < 1e-4 * bref.abs().max().item() + 1e-6
+
+
+def test_fully_masked_row_gives_nan_like_reference():
+    """A key padding mask with no observed key makes softmax NaN in the
+    reference (-inf everywhere); the kernel propagates the same NaN."""
+    from VAESNe import _ops
+    B, L, E = 2, 16, 32
+    qkv = torch.randn(B, L, 3 * E, device=DEV)
+    m = torch.zeros(B, L, dtype=torch.bool, device=DEV)
+    m[1] = True
+    o = _ops.self_attention(qkv, m, 4, 0.0)
+    assert torch.isfinite(o[0]).all() and torch.isnan(o[1]).all()
+
+
+def _probe_attention_mask(B, Lq, Lk, j0, p, seed_call):
+    """Read the attention-dropout keep mask of keys j0..j0+7 for every query:
+    q = 0 (uniform softmax over the 8 unmasked probe keys), v_j = e_(j-j0)."""
+    from VAESNe import _ops, rng
+    E, H, dh = 32, 4, 8
+    q = torch.zeros(B, Lq, E, device=DEV)
+    kv = torch.zeros(B, Lk, 2 * E, device=DEV)
+    for h in range(H):
+        for t in range(8):
+            kv[:, j0 + t, E + h * dh + t] = 1.0
+    mask = torch.ones(B, Lk, dtype=torch.bool, device=DEV)
+    mask[:, j0:j0 + 8] = False
+    rng._call = seed_call - 1
+    o = _ops.cross_attention(q, kv, mask, H, p)
+    keep = (o.view(B, Lq, H, dh) * 8 * (1 - p)).round()   # 1 kept / 0 dropped
+    return keep, q, kv, mask
+
+
+def test_attention_dropout_statistics_and_backward_mask():
+    from VAESNe import _ops, rng
+    B, Lq, Lk, p = 4, 512, 130, 0.1
+    keep, q, kv, mask = _probe_attention_mask(B, Lq, Lk, 100, p, 777)
+    assert set(torch.unique(keep).tolist()) <= {0.0, 1.0}
+    rate = 1 - keep.mean().item()
+    n = keep.numel()
+    assert abs(rate - p) < 4 * math.sqrt(p * (1 - p) / n), rate
+    # neighbouring keys / heads / queries are not correlated
+    k = keep.float() - keep.float().mean()
+    for a, b in [(k[..., :-1], k[..., 1:]), (k[:, :-1], k[:, 1:])]:
+        corr = (a * b).mean() / (k * k).mean()
+        assert abs(corr.item()) < 0.02
+    # backward regenerates the same mask: dV of probe key j for head h equals
+    # sum_q keep[q, h, j] / (8 (1 - p)) * dO[q, h, :]
+    qd = q.clone().requires_grad_(True)
+    kvd = kv.clone().requires_grad_(True)
+    rng._call = 777 - 1
+    o = _ops.cross_attention(qd, kvd, mask, 4, p)
+    go = torch.randn_like(o)
+    (o * go).sum().backward()
+    dv = kvd.grad[:, 100:108, 32:].view(B, 8, 4, 8)          # [B, j, h, d]
+    expect = torch.einsum("bqhj,bqhd->bjhd", keep, go.view(B, Lq, 4, 8)) / (8 * (1 - p))
+    assert _rel(dv, expect) < 1e-5
+
+
+def test_add_layernorm_vs_oracle_and_dropout():
+    from VAESNe import _ops, rng
+    M, E = 5000, 32
+    ln = torch.nn.LayerNorm(E).to(DEV)
+    with torch.no_grad():
+        ln.weight.copy_(1 + 0.1 * torch.randn(E))
+        ln.bias.copy_(0.1 * torch.randn(E))
+    x = torch.randn(M, E, device=DEV, requires_grad=True)
+    r = torch.randn(M, E, device=DEV, requires_grad=True)
+    y = _ops.add_layernorm(x, r, ln, 0.0)
+    gy = torch.randn_like(y)
+    (y * gy).sum().backward()
+    p = {"n.weight": ln.weight.detach().double().cpu().requires_grad_(True),
+         "n.bias": ln.bias.detach().double().cpu().requires_grad_(True)}
+    xr = x.detach().double().cpu().requires_grad_(True)
+    rr = r.detach().double().cpu().requires_grad_(True)
+    yr = O.layer_norm(p, "n", xr + rr)
+    (yr * gy.double().cpu()).sum().backward()
+    assert _rel(y, yr) < 1e-5
+    assert _rel(x.grad, xr.grad) < 1e-4 and _rel(r.grad, rr.grad) < 1e-4
+    assert _rel(ln.weight.grad, p["n.weight"].grad) < 1e-4
+    assert _rel(ln.bias.grad, p["n.bias"].grad) < 1e-4
+    # dropout: x = 0, res = 1 -> kept entries sit above the row mean
+    ln2 = torch.nn.LayerNorm(E).to(DEV)
+    xz = torch.zeros(M, E, device=DEV)
+    ones = torch.ones(M, E, device=DEV, requires_grad=True)
+    rng._call = 41
+    y2 = _ops.add_layernorm(xz, ones, ln2, 0.1)
+    kept = (y2 > 0) | (y2.abs() < 1e-6)
+    rate = 1 - kept.float().mean().item()
+    assert abs(rate - 0.1) < 4 * math.sqrt(0.09 / kept.numel())
+    # backward uses the same mask: d res = dLN * keep / (1-p)
+    gy2 = torch.randn_like(y2)
+    (y2 * gy2).sum().backward()
+    assert (ones.grad[~kept] == 0).all()
+
+
+@pytest.mark.parametrize("K,N,act", [(32, 96, None), (32, 32, "gelu"), (64, 32, "relu"),
+                                     (96, 32, "relu"), (1, 32, None), (4, 32, "relu"),
+                                     (3, 32, "relu"), (32, 1, None), (32, 2, None)])
+def test_linear_vs_oracle(K, N, act):
+    from VAESNe import _ops
+    g = torch.Generator().manual_seed(K * 100 + N)
+    M = 3001
+    W = (torch.randn(N, K, generator=g) / math.sqrt(K)).double()
+    b = (0.1 * torch.randn(N, generator=g)).double()
+    x = torch.randn(M, K, generator=g, dtype=torch.float64)
+    x2 = torch.randn(M, K, generator=g, dtype=torch.float64)
+    Wd, bd = W.float().to(DEV).requires_grad_(True), b.float().to(DEV).requires_grad_(True)
+    xd, x2d = x.float().to(DEV).requires_grad_(True), x2.float().to(DEV).requires_grad_(True)
+    y = _ops.linear(xd, Wd, bd, act=act, x2=x2d)
+    Wr, br = W.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    xr, x2r = x.clone().requires_grad_(True), x2.clone().requires_grad_(True)
+    yr = torch.nn.functional.linear(xr + x2r, Wr, br)
+    yr = {None: yr, "relu": torch.relu(yr), "gelu": torch.nn.functional.gelu(yr)}[act]
+    gy = torch.randn(M, N, generator=g, dtype=torch.float64)
+    (y * gy.float().to(DEV)).sum().backward()
+    (yr * gy).sum().backward()
+    assert _rel(y, yr) < 1e-5
+    assert _rel(xd.grad, xr.grad) < 1e-4 and _rel(x2d.grad, x2r.grad) < 1e-4
+    assert _rel(Wd.grad, Wr.grad) < 1e-4 and _rel(bd.grad, br.grad) < 1e-4
+
+
+def test_embedding_sincos_rsample_latent_head():
+    from VAESNe import _ops
+    g = torch.Generator().manual_seed(5)
+    # embedding gather + deterministic scatter-add, with fused base add
+    idx = torch.randint(0, 6, (37, 60), generator=g)
+    table = torch.randn(6, 32, generator=g)
+    base = torch.randn(37, 60, 32, generator=g)
+    td = table.to(DEV).requires_grad_(True)
+    bd = base.to(DEV).requires_grad_(True)
+    out = _ops.embedding(idx.to(DEV), td, base=bd)
+    go = torch.randn(37, 60, 32, generator=g)
+    (out * go.to(DEV)).sum().backward()
+    assert _rel(out, table[idx] + base) < 1e-6
+    ref = torch.zeros(6, 32, dtype=torch.float64).index_add_(0, idx.reshape(-1), go.reshape(-1, 32).double())
+    assert _rel(td.grad, ref) < 1e-5 and _rel(bd.grad, go) == 0.0
+    # sinusoidal features vs the reference recipe
+    x = torch.randn(7, 982, generator=g)
+    div = torch.exp(torch.arange(0, 32).float() * (-torch.log(torch.tensor(10000.0)) / 32))
+    f = _ops.sincos(x.to(DEV), div.to(DEV))
+    assert _rel(f, O.sinus_features(x.double(), div.double())) < 1e-5
+    # latent head + rsample (+ grads)
+    bott = torch.randn(5, 8, 4, generator=g, dtype=torch.float64)
+    bott[0, 4, 0] = 25.0   # softplus threshold branch
+    u = O.draw_u((3, 5, 4, 4), generator=g).double()
+    b_d = bott.float().to(DEV).requires_grad_(True)
+    mu, sc = _ops.latent_head(b_d, 4)
+    z = _ops.RsampleFn.apply(mu, sc, u.float().to(DEV))
+    gz = torch.randn(z.shape, generator=g, dtype=torch.float64)
+    (z * gz.float().to(DEV)).sum().backward()
+    b_r = bott.clone().requires_grad_(True)
+    mu_r, sc_r = b_r[:, :4], torch.nn.functional.softplus(b_r[:, 4:])
+    z_r = O.laplace_rsample(mu_r, sc_r, u)
+    (z_r * gz).sum().backward()
+    assert _rel(z, z_r) < 1e-5 and _rel(b_d.grad, b_r.grad) < 1e-5
+
+
+def test_device_uniform_range_and_moments():
+    from VAESNe import rng
+    u = rng.draw_uniform((4096, 256), DEV)
+    eps = torch.finfo(torch.float32).eps
+    assert u.min().item() >= eps - 1 and u.max().item() < 1
+    assert abs(u.mean().item()) < 5e-3 and abs(u.var().item() - 1 / 3) < 5e-3
+    u2 = rng.draw_uniform((4096, 256), DEV)
+    assert not torch.equal(u, u2)

@@ -1,0 +1,81 @@
+"""Photometry (light-curve) transformer encoder / decoder, MI355X build.
+
+Same constructors, attributes and state_dict keys as the reference's
+PhotometricLayers.py; forward passes run on the HIP kernels.
+"""
+import torch
+from torch import nn
+
+from . import _ops
+from .util_layers import (MLP, Linear, SinusoidalMLPPositionalEmbedding,
+                          SinusoidalPositionalEmbedding, TransformerBlock, singlelayerMLP)
+
+
+class photometricTransformerDecoder(nn.Module):
+    """PhotometricLayers.py:10-69.  Queries are sinMLP(time) + band embedding;
+    4 blocks of masked self-attention over the light-curve points and
+    cross-attention to the decoded latent tokens; head 32->32->1."""
+
+    def __init__(self, bottleneck_dim, num_bands, model_dim=32, num_heads=4, ff_dim=32,
+                 num_layers=4, dropout=0.1, donotmask=False, selfattn=False):
+        super().__init__()
+        self.transformerblocks = nn.ModuleList(
+            [TransformerBlock(model_dim, num_heads, ff_dim, dropout, selfattn)
+             for _ in range(num_layers)])
+        self.model_dim = model_dim
+        self.sinusoidal_time_embd = SinusoidalMLPPositionalEmbedding(model_dim)
+        self.bandembd = nn.Embedding(num_bands, model_dim)
+        self.contextfc = MLP(bottleneck_dim, model_dim, [model_dim])
+        self.get_photo = singlelayerMLP(model_dim, 1)
+        self.donotmask = donotmask
+
+    def forward(self, time, band, bottleneck, mask=None):
+        if self.donotmask:
+            mask = None
+        # x = time_embd + band_embd (PhotometricLayers.py:62-64), the add fused in the gather
+        x = _ops.embedding(band, self.bandembd.weight, base=self.sinusoidal_time_embd(time))
+        h = x
+        bottleneck = self.contextfc(bottleneck)
+        for transformerblock in self.transformerblocks:
+            h = transformerblock(h, bottleneck, mask=mask)
+        return self.get_photo(x, h).squeeze(-1)   # get_photo(x + h)
+
+
+class photometricTransformerEncoder(nn.Module):
+    """PhotometricLayers.py:72-143.  Light-curve tokens (flux, time, band),
+    2*latent_len learned query tokens cross-attending to them (key padding
+    mask), bottleneck MLP."""
+
+    def __init__(self, num_bands, bottleneck_length, bottleneck_dim, model_dim=32, num_heads=4,
+                 ff_dim=32, num_layers=4, dropout=0.1, selfattn=False, concat=True):
+        super().__init__()
+        self.model_dim = model_dim
+        self.initbottleneck = nn.Parameter(torch.randn(bottleneck_length, model_dim))
+        self.bottleneckfc = singlelayerMLP(model_dim, bottleneck_dim)
+        self.transformerblocks = nn.ModuleList(
+            [TransformerBlock(model_dim, num_heads, ff_dim, dropout, selfattn)
+             for _ in range(num_layers)])
+        self.concat = concat
+        self.bandembd = nn.Embedding(num_bands, model_dim)
+        self.fluxfc = Linear(1, model_dim)
+        if concat:
+            self.time_embd = SinusoidalMLPPositionalEmbedding(model_dim)
+            self.LCfc = MLP(3 * model_dim, model_dim, [model_dim])
+        else:
+            self.time_embd = SinusoidalPositionalEmbedding(model_dim)
+            self.LCfc = None
+
+    def forward(self, flux, time, band, mask=None):
+        if self.concat:
+            tok = self.LCfc(torch.cat([self.fluxfc(flux[:, :, None]),
+                                       self.time_embd(time),
+                                       _ops.embedding(band, self.bandembd.weight)], dim=-1))
+        else:
+            # fluxfc(flux) + sin(time) + bandembd(band): both adds fused into the kernels
+            tok = _ops.embedding(band, self.bandembd.weight,
+                                 base=self.fluxfc(flux[:, :, None], base=self.time_embd(time)))
+        x = _ops.repeat_batch(self.initbottleneck, flux.shape[0])
+        h = x
+        for transformerblock in self.transformerblocks:
+            h = transformerblock(h, tok, mask=None, context_mask=mask)
+        return self.bottleneckfc(x, h)   # bottleneckfc(x + h)

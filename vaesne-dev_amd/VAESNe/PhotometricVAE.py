@@ -1,0 +1,122 @@
+"""Photometry VAE, MI355X build (reference: PhotometricVAE.py:10-222).
+
+Encoder -> (mu, softplus scale) -> Laplace.rsample([K]) -> decoder, each step
+a HIP kernel.  Constructors accept and ignore `photometric_length` (the
+cannon scripts pass it).
+"""
+import torch
+import torch.distributions as dist
+from torch import nn
+
+from . import _ops
+from .PhotometricLayers import photometricTransformerDecoder, photometricTransformerEncoder
+from .base_vae import VAE, check_laplace
+
+
+class PhotometricEnc(nn.Module):
+    """PhotometricVAE.py:10-56: bottleneck [B, 2*latent_len, latent_dim] ->
+    mu = b[:, :latent_len], scale = softplus(b[:, latent_len:])."""
+
+    def __init__(self, num_bands, latent_len, latent_dim, model_dim, num_heads, ff_dim,
+                 num_layers, dropout=0.1, selfattn=False, concat=True):
+        super().__init__()
+        self.inference_transformer = photometricTransformerEncoder(
+            num_bands, 2 * latent_len, latent_dim, model_dim, num_heads, ff_dim, num_layers,
+            dropout, selfattn, concat)
+        self.latent_dim = latent_dim
+        self.latent_len = latent_len
+
+    def forward(self, flux, time, band, mask=None):
+        bottleneck = self.inference_transformer(flux, time, band, mask)
+        return _ops.latent_head(bottleneck, self.latent_len)
+
+
+class PhotometricDec(nn.Module):
+    """PhotometricVAE.py:58-94: returns (loc, 1 + 1e8*mask)."""
+
+    def __init__(self, latent_dim, num_bands, model_dim, num_heads, ff_dim, num_layers,
+                 dropout=0.1, selfattn=False):
+        super().__init__()
+        self.generativetransformer = photometricTransformerDecoder(
+            latent_dim, num_bands, model_dim, num_heads, ff_dim, num_layers, dropout, selfattn)
+
+    def pxz(self, time, band, z, mask=None):
+        return self.generativetransformer(time, band, z, mask)
+
+    def forward(self, time, band, z, mask=None):
+        x_rec = self.pxz(time, band, z, mask)
+        if mask is None:
+            var = torch.ones_like(x_rec)
+        else:
+            var = _ops.mask_scale(mask, 1, 1e8, x_rec).view_as(x_rec)
+        return x_rec, var
+
+
+class PhotometricVAE(VAE):
+    def __init__(self, num_bands=6, latent_len=8, latent_dim=4, model_dim=64, num_heads=4,
+                 ff_dim=64, num_layers=4, dropout=0.1, selfattn=False, concat=True, beta=1.,
+                 prior=dist.Laplace, likelihood=dist.Laplace, posterior=dist.Laplace,
+                 photometric_length=None):
+        check_laplace(prior, likelihood, posterior)
+        super().__init__(
+            prior, likelihood, posterior,
+            PhotometricEnc(num_bands, latent_len, latent_dim, model_dim, num_heads, ff_dim,
+                           num_layers, dropout, selfattn, concat),
+            PhotometricDec(latent_dim, num_bands, model_dim, num_heads, ff_dim, num_layers,
+                           dropout),
+            params=[num_bands, latent_len, latent_dim, model_dim, num_heads, ff_dim, num_layers,
+                    dropout, selfattn])
+        self._pz_params = nn.ParameterList([
+            nn.Parameter(torch.zeros(latent_len, latent_dim), requires_grad=False),  # loc
+            nn.Parameter(torch.ones(latent_len, latent_dim), requires_grad=False),   # scale
+        ])
+        self.llik_scaling = 1. / beta
+        self.modelName = 'light_curve'
+        self.latent_len = latent_len
+        self.latent_dim = latent_dim
+
+    def forward(self, x, K=1):
+        """PhotometricVAE.py:157-176 -> (qz_x, px_z, zs)."""
+        flux, time, band, mask = x
+        self._qz_x_params = self.enc(flux, time, band, mask)
+        qz_x = self._dist(self.qz_x, *self._qz_x_params)
+        zs = _ops.laplace_rsample(*self._qz_x_params, K)
+        px_z = self.decode(zs, x)
+        return qz_x, px_z, zs
+
+    def encode(self, x, mean=True):
+        flux, time, band, mask = x
+        self.eval()
+        with torch.no_grad():
+            qz_x = self._dist(self.qz_x, *self.enc(flux, time, band, mask))
+        if mean:
+            return qz_x.mean
+        return qz_x
+
+    def decode(self, zs, x):
+        """PhotometricVAE.py:188-199: expand time/band/mask K times, decode,
+        wrap in the likelihood distribution [K, B, L]."""
+        _, time, band, mask = x
+        K = zs.shape[0]
+        L = time.shape[-1]
+        rep = lambda t: t.unsqueeze(0).expand(K, -1, -1).reshape(-1, L)
+        loc, scale = self.dec(rep(time), rep(band), zs.reshape(-1, zs.shape[-2], zs.shape[-1]),
+                              None if mask is None else rep(mask))
+        return self._dist(self.px_z, loc.reshape(K, -1, L), scale.reshape(K, -1, L))
+
+    def reconstruct(self, x, K=1):
+        self.eval()
+        with torch.no_grad():
+            mu, scale = self.enc(*x)
+            zs = _ops.laplace_rsample(mu, scale, K)
+            return self.decode(zs, x).mean
+
+    def generate(self, N, time, band, mask=None):
+        """Decode N prior draws at the given (time, band[, mask]) grid
+        (the reference's version references an undefined K, PhotometricVAE.py:216)."""
+        self.eval()
+        with torch.no_grad():
+            loc, scale = self.pz_params[0], self.pz_params[1]
+            zs = _ops.laplace_rsample(loc.expand(time.shape[0], *loc.shape).contiguous(),
+                                      scale.expand(time.shape[0], *scale.shape).contiguous(), N)
+            return self.decode(zs, (None, time, band, mask)).mean

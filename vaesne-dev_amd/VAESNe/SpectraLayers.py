@@ -1,0 +1,83 @@
+"""Spectra transformer encoder / decoder, MI355X build.
+
+Same constructors, attributes and state_dict keys as the reference's
+SpectraLayers.py; forward passes run on the HIP kernels.  The decoder's
+982-token masked self-attention is the dominant cost of the whole step
+(SURVEY.md §8(a) a7).
+"""
+import torch
+from torch import nn
+
+from . import _ops
+from .util_layers import (MLP, Linear, SinusoidalMLPPositionalEmbedding,
+                          SinusoidalPositionalEmbedding, TransformerBlock, singlelayerMLP)
+
+
+class spectraTransformerDecoder(nn.Module):
+    """SpectraLayers.py:11-63.  Queries sinMLP(wavelength); context =
+    [contextfc(z) | sinMLP(phase)] (latent_len + 1 tokens); 4 blocks of masked
+    self-attention + cross-attention; head 32->32->1."""
+
+    def __init__(self, bottleneck_dim, model_dim=32, num_heads=4, ff_dim=32, num_layers=4,
+                 dropout=0.1, selfattn=False):
+        super().__init__()
+        self.transformerblocks = nn.ModuleList(
+            [TransformerBlock(model_dim, num_heads, ff_dim, dropout, selfattn)
+             for _ in range(num_layers)])
+        self.wavelength_embd_layer = SinusoidalMLPPositionalEmbedding(model_dim)
+        self.phase_embd_layer = SinusoidalMLPPositionalEmbedding(model_dim)
+        self.contextfc = MLP(bottleneck_dim, model_dim, [model_dim])
+        self.get_flux = singlelayerMLP(model_dim, 1)
+
+    def forward(self, wavelength, phase, bottleneck, mask=None):
+        x = self.wavelength_embd_layer(wavelength)
+        phase_embd = self.phase_embd_layer(phase[:, None])
+        h = x
+        bottleneck = torch.cat([self.contextfc(bottleneck), phase_embd], dim=1)
+        for transformerblock in self.transformerblocks:
+            h = transformerblock(h, bottleneck, mask=mask)
+        return self.get_flux(x, h).squeeze(-1)   # get_flux(x + h)
+
+
+class spectraTransformerEncoder(nn.Module):
+    """SpectraLayers.py:66-138.  NB the argument order (wavelength, flux, ...):
+    SpectraEnc passes (flux, wavelength, ...) into it (SpectraVAE.py:41-44), so
+    flux_embd sees the wavelength grid and the sinusoidal embedding sees the
+    flux.  That is the reference's behaviour and is kept."""
+
+    def __init__(self, bottleneck_length, bottleneck_dim, model_dim, num_heads, num_layers,
+                 ff_dim, dropout=0.1, selfattn=False, concat=True):
+        super().__init__()
+        self.initbottleneck = nn.Parameter(torch.randn(bottleneck_length, model_dim))
+        self.flux_embd = Linear(1, model_dim)
+        self.transformerblocks = nn.ModuleList(
+            [TransformerBlock(model_dim, num_heads, ff_dim, dropout, selfattn)
+             for _ in range(num_layers)])
+        self.bottleneckfc = singlelayerMLP(model_dim, bottleneck_dim)
+        self.concat = concat
+        if concat:
+            self.spectrafc = MLP(2 * model_dim, model_dim, [model_dim])
+            self.wavelength_embd_layer = SinusoidalPositionalEmbedding(model_dim)
+        else:
+            self.spectrafc = None
+            self.wavelength_embd_layer = SinusoidalMLPPositionalEmbedding(model_dim)
+        self.phase_embd_layer = SinusoidalMLPPositionalEmbedding(model_dim)
+
+    def forward(self, wavelength, flux, phase, mask=None):
+        if self.concat:
+            flux_embd = self.spectrafc(torch.cat([self.flux_embd(flux[:, :, None]),
+                                                  self.wavelength_embd_layer(wavelength)], dim=-1))
+        else:
+            flux_embd = self.flux_embd(flux[:, :, None],
+                                       base=self.wavelength_embd_layer(wavelength))
+        phase_embd = self.phase_embd_layer(phase[:, None])
+        context = torch.cat([flux_embd, phase_embd], dim=1)
+        if mask is not None:
+            # the phase token is never masked (SpectraLayers.py:129-131)
+            mask = torch.cat([mask, torch.zeros(mask.shape[0], 1, dtype=mask.dtype,
+                                                device=mask.device)], dim=1)
+        x = _ops.repeat_batch(self.initbottleneck, context.shape[0])
+        h = x
+        for transformerblock in self.transformerblocks:
+            h = transformerblock(h, context, context_mask=mask)
+        return self.bottleneckfc(x, h)   # bottleneckfc(x + h)

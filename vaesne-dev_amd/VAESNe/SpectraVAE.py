@@ -1,0 +1,118 @@
+"""Spectra VAE, MI355X build (reference: SpectraVAE.py:11-206).
+
+Constructors accept and ignore `spectra_length` (the cannon scripts pass it,
+SURVEY.md F9).
+"""
+import torch
+import torch.distributions as dist
+from torch import nn
+
+from . import _ops
+from .SpectraLayers import spectraTransformerDecoder, spectraTransformerEncoder
+from .base_vae import VAE, check_laplace
+
+
+class SpectraEnc(nn.Module):
+    """SpectraVAE.py:11-51."""
+
+    def __init__(self, latent_len, latent_dim, model_dim, num_heads, num_layers, ff_dim,
+                 dropout=0.1, selfattn=False, concat=True):
+        super().__init__()
+        self.inference_transformer = spectraTransformerEncoder(
+            2 * latent_len, latent_dim, model_dim, num_heads, num_layers, ff_dim, dropout,
+            selfattn, concat)
+        self.latent_dim = latent_dim
+        self.latent_len = latent_len
+
+    def forward(self, flux, wavelength, phase, mask=None):
+        # NB argument order into the encoder is the reference's (see SpectraLayers)
+        bottleneck = self.inference_transformer(flux, wavelength, phase, mask)
+        return _ops.latent_head(bottleneck, self.latent_len)
+
+
+class SpectraDec(nn.Module):
+    """SpectraVAE.py:53-87: returns (loc, 1 + 1e10*mask)."""
+
+    def __init__(self, latent_dim, model_dim, num_heads, ff_dim, num_layers, dropout=0.1,
+                 selfattn=False):
+        super().__init__()
+        self.generativetransformer = spectraTransformerDecoder(
+            latent_dim, model_dim, num_heads, ff_dim, num_layers, dropout, selfattn)
+
+    def pxz(self, wavelength, phase, z, mask=None):
+        return self.generativetransformer(wavelength, phase, z, mask)
+
+    def forward(self, wavelength, phase, z, mask=None):
+        x_rec = self.pxz(wavelength, phase, z, mask)
+        if mask is None:
+            var = torch.ones_like(x_rec)
+        else:
+            var = _ops.mask_scale(mask, 1, 1e10, x_rec).view_as(x_rec)
+        return x_rec, var
+
+
+class SpectraVAE(VAE):
+    def __init__(self, latent_len=4, latent_dim=2, model_dim=32, num_heads=4, ff_dim=32,
+                 num_layers=4, dropout=0.1, selfattn=False, concat=True, beta=1.,
+                 prior=dist.Laplace, likelihood=dist.Laplace, posterior=dist.Laplace,
+                 spectra_length=None):
+        check_laplace(prior, likelihood, posterior)
+        super().__init__(
+            prior, likelihood, posterior,
+            SpectraEnc(latent_len, latent_dim, model_dim, num_heads, num_layers, ff_dim,
+                       dropout, selfattn, concat),
+            SpectraDec(latent_dim, model_dim, num_heads, ff_dim, num_layers, dropout),
+            params=[latent_len, latent_dim, model_dim, num_heads, num_layers, ff_dim, dropout,
+                    selfattn])
+        self._pz_params = nn.ParameterList([
+            nn.Parameter(torch.zeros(latent_len, latent_dim), requires_grad=False),
+            nn.Parameter(torch.ones(latent_len, latent_dim), requires_grad=False),
+        ])
+        self.llik_scaling = 1. / beta
+        self.modelName = 'spectrum'
+        self.latent_len = latent_len
+        self.latent_dim = latent_dim
+
+    def forward(self, x, K=1):
+        """SpectraVAE.py:148-165 -> (qz_x, px_z, zs)."""
+        flux, wavelength, phase, mask = x
+        self._qz_x_params = self.enc(flux, wavelength, phase, mask)
+        qz_x = self._dist(self.qz_x, *self._qz_x_params)
+        zs = _ops.laplace_rsample(*self._qz_x_params, K)
+        px_z = self.decode(zs, x)
+        return qz_x, px_z, zs
+
+    def reconstruct(self, x, K=1):
+        self.eval()
+        with torch.no_grad():
+            mu, scale = self.enc(*x)
+            zs = _ops.laplace_rsample(mu, scale, K)
+            return self.decode(zs, x).mean
+
+    def encode(self, x, mean=True):
+        flux, wavelength, phase, mask = x
+        self.eval()
+        with torch.no_grad():
+            qz_x = self._dist(self.qz_x, *self.enc(flux, wavelength, phase, mask))
+        if mean:
+            return qz_x.mean
+        return qz_x
+
+    def decode(self, zs, x):
+        """SpectraVAE.py:186-196."""
+        _, wavelength, phase, mask = x
+        K = zs.shape[0]
+        L = wavelength.shape[-1]
+        rep = lambda t: t.unsqueeze(0).expand(K, -1, -1).reshape(-1, L)
+        loc, scale = self.dec(rep(wavelength), phase.unsqueeze(0).expand(K, -1).reshape(-1),
+                              zs.reshape(-1, zs.shape[-2], zs.shape[-1]),
+                              None if mask is None else rep(mask))
+        return self._dist(self.px_z, loc.reshape(K, -1, L), scale.reshape(K, -1, L))
+
+    def generate(self, N, x):
+        """SpectraVAE.py:198-206: N prior draws decoded at x's grids."""
+        self.eval()
+        with torch.no_grad():
+            loc, scale = self.pz_params[0], self.pz_params[1]
+            zs = _ops.laplace_rsample(loc.unsqueeze(0).contiguous(), scale.unsqueeze(0).contiguous(), N)
+            return self.decode(zs, x).mean.unsqueeze(0)

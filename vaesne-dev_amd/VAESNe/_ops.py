@@ -1,0 +1,505 @@
+"""Autograd operators of the VAESNe step, each backed by libvaesne_hip.so.
+
+Every forward and backward here is a launch of a hand-written gfx950 kernel
+(include/vaesne_hip.h); torch supplies device memory, the current stream and
+autograd bookkeeping only (allocation, views, reshapes, cat of tiny tensors).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import torch
+
+from . import _lib, rng
+from ._lib import lib, ptr, stream
+
+ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise TypeError(f"VAESNe HIP ops compute in fp32 (as the reference); got {t.dtype}")
+    return t
+
+
+def _rows(t: torch.Tensor):
+    """View t [..., K] as M rows of K with a uniform row stride; copies only if
+    the leading dims cannot be collapsed.  Returns (t, M, ld)."""
+    K = t.shape[-1]
+    if t.dim() == 2 and t.stride(-1) == 1 and t.stride(0) >= K:
+        return t, t.shape[0], t.stride(0)
+    t = t.contiguous()
+    return t, (t.numel() // K if K > 0 else 0), K
+
+
+def _ws(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(1, (int(nbytes) + 3) // 4), dtype=torch.float32, device=device)
+
+
+def _mask_u8(mask):
+    if mask is None:
+        return None
+    if mask.dtype == torch.bool:
+        mask = mask.contiguous().view(torch.uint8)
+    elif mask.dtype != torch.uint8:
+        mask = (mask != 0).to(torch.uint8)
+    return mask.contiguous()
+
+
+# ---------------------------------------------------------------------------
+# Linear (+ activation, + fused input add)
+# ---------------------------------------------------------------------------
+class LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, b, act, x2, base):
+        _lib.require_device(x, W, b, x2, base)
+        _f32(x)
+        lead = x.shape[:-1]
+        K = x.shape[-1]
+        N = W.shape[0]
+        W = W.contiguous()
+        xr, M, ldx = _rows(x)
+        x2r, ldx2 = None, 0
+        if x2 is not None:
+            if x2.shape != x.shape:
+                raise RuntimeError("LinearFn: x2 must match x")
+            x2r, _, ldx2 = _rows(x2)
+        if base is not None:
+            if act or base.shape != (*lead, N):
+                raise RuntimeError("LinearFn: base must be [*, N] and act None")
+            y = base.reshape(M, N).clone()   # y = base + x W^T + b (kernel accumulates)
+        else:
+            y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        z = torch.empty((M, N), dtype=torch.float32, device=x.device) if act else None
+        lib.linear_fwd(xr.data_ptr(), ldx, ptr(x2r), ldx2, M, K, W.data_ptr(), ptr(b), N,
+                       y.data_ptr(), N, ptr(z), N, act, int(base is not None), stream())
+        ctx.act, ctx.M, ctx.K, ctx.N, ctx.ldx, ctx.ldx2 = act, M, K, N, ldx, ldx2
+        ctx.xshape = x.shape
+        ctx.has_b = b is not None
+        ctx.save_for_backward(xr, x2r, W, z)
+        return y.view(*lead, N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xr, x2r, W, z = ctx.saved_tensors
+        act, M, K, N = ctx.act, ctx.M, ctx.K, ctx.N
+        dy = dy.contiguous()
+        dx = dW = db = None
+        s = stream()
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[4]:
+            dx = torch.empty((M, K), dtype=torch.float32, device=dy.device)
+            lib.linear_bwd_data(dy.data_ptr(), N, ptr(z), N, act, M, N, W.data_ptr(), K,
+                                dx.data_ptr(), K, 0, s)
+            dx = dx.view(ctx.xshape)
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dW = torch.empty((N, K), dtype=torch.float32, device=dy.device)
+            db = torch.empty((N,), dtype=torch.float32, device=dy.device) if ctx.has_b else None
+            ws = _ws(lib.linear_bwd_weight_workspace(M, N, K), dy.device)
+            lib.linear_bwd_weight(dy.data_ptr(), N, ptr(z), N, act, xr.data_ptr(), ctx.ldx,
+                                  ptr(x2r), ctx.ldx2, M, N, K, dW.data_ptr(), ptr(db), 0,
+                                  ws.data_ptr(), s)
+        return (dx if ctx.needs_input_grad[0] else None, dW, db, None,
+                dx if ctx.needs_input_grad[4] else None,
+                dy.view(*ctx.xshape[:-1], N) if ctx.needs_input_grad[5] else None)
+
+
+def linear(x, weight, bias=None, act=None, x2=None, base=None):
+    """[base +] act((x [+ x2]) @ weight.T + bias) on the HIP linear kernel."""
+    return LinearFn.apply(x, weight, bias, ACT[act], x2, base)
+
+
+# ---------------------------------------------------------------------------
+# residual + dropout + LayerNorm
+# ---------------------------------------------------------------------------
+class AddLNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, gamma, beta, p, eps):
+        _lib.require_device(x, res, gamma, beta)
+        if abs(eps - 1e-5) > 1e-12:
+            raise RuntimeError("VAESNe LayerNorm kernel is built for eps=1e-5 (nn.LayerNorm default)")
+        E = x.shape[-1]
+        x = x.contiguous()
+        res = res.contiguous()
+        M = x.numel() // E
+        y = torch.empty_like(x)
+        mean = torch.empty(M, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(M, dtype=torch.float32, device=x.device)
+        st = rng.state(x.device) if p > 0 else None
+        cid = rng.next_call_id() if p > 0 else 0
+        lib.add_ln_fwd(x.data_ptr(), E, res.data_ptr(), E, M, E, gamma.data_ptr(),
+                       beta.data_ptr(), float(p), ptr(st), cid, y.data_ptr(), E,
+                       mean.data_ptr(), rstd.data_ptr(), stream())
+        ctx.p, ctx.cid, ctx.M, ctx.E = p, cid, M, E
+        ctx.save_for_backward(x, res, gamma, mean, rstd, st)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, res, gamma, mean, rstd, st = ctx.saved_tensors
+        dy = dy.contiguous()
+        M, E = ctx.M, ctx.E
+        dx = torch.empty_like(x)
+        dres = torch.empty_like(res)
+        dg = torch.empty_like(gamma)
+        dbt = torch.empty_like(gamma)
+        ws = _ws(lib.add_ln_bwd_workspace(M, E), dy.device)
+        lib.add_ln_bwd(dy.data_ptr(), E, x.data_ptr(), E, res.data_ptr(), E, M, E,
+                       gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), float(ctx.p), ptr(st),
+                       ctx.cid, dx.data_ptr(), E, 0, dres.data_ptr(), E, 0, dg.data_ptr(),
+                       dbt.data_ptr(), 0, ws.data_ptr(), stream())
+        return dx, dres, dg, dbt, None, None
+
+
+def add_layernorm(x, res, ln, p):
+    """LayerNorm `ln` of x + Dropout_p(res)."""
+    if tuple(ln.normalized_shape) != (x.shape[-1],) or ln.weight is None:
+        raise RuntimeError("VAESNe add_layernorm expects an affine LayerNorm over the last dim")
+    return AddLNFn.apply(x, res, ln.weight, ln.bias, float(p), float(ln.eps))
+
+
+# ---------------------------------------------------------------------------
+# attention core
+# ---------------------------------------------------------------------------
+def _attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, mask, B, H, Lq, Lk, dh, p, dev):
+    E = H * dh
+    o = torch.empty((B, Lq, E), dtype=torch.float32, device=dev)
+    lse = torch.empty((B, H, Lq), dtype=torch.float32, device=dev)
+    st = rng.state(dev) if p > 0 else None
+    cid = rng.next_call_id() if p > 0 else 0
+    lib.attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, ptr(mask), Lk, o.data_ptr(), Lq * E, E,
+                 lse.data_ptr(), B, H, Lq, Lk, dh, float(p), ptr(st), cid, stream())
+    return o, lse, st, cid
+
+
+class SelfAttnFn(torch.autograd.Function):
+    """Packed qkv [B, L, 3E] -> o [B, L, E] (self-attention, key padding mask)."""
+
+    @staticmethod
+    def forward(ctx, qkv, mask, H, p):
+        _lib.require_device(qkv)
+        qkv = qkv.contiguous()
+        B, L, E3 = qkv.shape
+        E = E3 // 3
+        dh = E // H
+        m = _mask_u8(mask)
+        base = qkv.data_ptr()
+        o, lse, st, cid = _attn_fwd(base, L * E3, E3, base + 4 * E, L * E3, E3, base + 8 * E,
+                                    L * E3, E3, m, B, H, L, L, dh, p, qkv.device)
+        ctx.dims = (B, L, E, H, dh, float(p), cid)
+        ctx.save_for_backward(qkv, m, o, lse, st)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, m, o, lse, st = ctx.saved_tensors
+        B, L, E, H, dh, p, cid = ctx.dims
+        do = do.contiguous()
+        E3 = 3 * E
+        dqkv = torch.empty_like(qkv)
+        ws = _ws(lib.attn_bwd_workspace(B, H, L), do.device)
+        b, d = qkv.data_ptr(), dqkv.data_ptr()
+        lib.attn_bwd(b, L * E3, E3, b + 4 * E, L * E3, E3, b + 8 * E, L * E3, E3, ptr(m), L,
+                     o.data_ptr(), L * E, E, lse.data_ptr(), do.data_ptr(), L * E, E,
+                     d, L * E3, E3, d + 4 * E, L * E3, E3, d + 8 * E, L * E3, E3,
+                     B, H, L, L, dh, p, ptr(st), cid, ws.data_ptr(), stream())
+        return dqkv, None, None, None
+
+
+class CrossAttnFn(torch.autograd.Function):
+    """q [B, Lq, E], packed kv [B, Lk, 2E] -> o [B, Lq, E]."""
+
+    @staticmethod
+    def forward(ctx, q, kv, mask, H, p):
+        _lib.require_device(q, kv)
+        q = q.contiguous()
+        kv = kv.contiguous()
+        B, Lq, E = q.shape
+        Lk = kv.shape[1]
+        dh = E // H
+        m = _mask_u8(mask)
+        kb = kv.data_ptr()
+        o, lse, st, cid = _attn_fwd(q.data_ptr(), Lq * E, E, kb, Lk * 2 * E, 2 * E, kb + 4 * E,
+                                    Lk * 2 * E, 2 * E, m, B, H, Lq, Lk, dh, p, q.device)
+        ctx.dims = (B, Lq, Lk, E, H, dh, float(p), cid)
+        ctx.save_for_backward(q, kv, m, o, lse, st)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, kv, m, o, lse, st = ctx.saved_tensors
+        B, Lq, Lk, E, H, dh, p, cid = ctx.dims
+        do = do.contiguous()
+        dq = torch.empty_like(q)
+        dkv = torch.empty_like(kv)
+        ws = _ws(lib.attn_bwd_workspace(B, H, Lq), do.device)
+        kb, dkb = kv.data_ptr(), dkv.data_ptr()
+        lib.attn_bwd(q.data_ptr(), Lq * E, E, kb, Lk * 2 * E, 2 * E, kb + 4 * E, Lk * 2 * E,
+                     2 * E, ptr(m), Lk, o.data_ptr(), Lq * E, E, lse.data_ptr(), do.data_ptr(),
+                     Lq * E, E, dq.data_ptr(), Lq * E, E, dkb, Lk * 2 * E, 2 * E, dkb + 4 * E,
+                     Lk * 2 * E, 2 * E, B, H, Lq, Lk, dh, p, ptr(st), cid, ws.data_ptr(),
+                     stream())
+        return dq, dkv, None, None, None
+
+
+def self_attention(qkv, mask, num_heads, p):
+    return SelfAttnFn.apply(qkv, mask, num_heads, float(p))
+
+
+def cross_attention(q, kv, mask, num_heads, p):
+    return CrossAttnFn.apply(q, kv, mask, num_heads, float(p))
+
+
+# ---------------------------------------------------------------------------
+# embeddings
+# ---------------------------------------------------------------------------
+def sincos(x, div):
+    """[sin(x*div) | cos(x*div)] over a new last axis (no gradient: x is data)."""
+    _lib.require_device(x)
+    xs = x.detach().contiguous()
+    nf = div.numel()
+    out = torch.empty((*x.shape, 2 * nf), dtype=torch.float32, device=x.device)
+    n = xs.numel()
+    lib.sincos(xs.data_ptr(), max(n, 1), n, div.data_ptr(), nf, out.data_ptr(), 2 * nf, stream())
+    return out
+
+
+class EmbedFn(torch.autograd.Function):
+    """out = (base or 0) + table[idx]  (nn.Embedding lookup, optional fused add)."""
+
+    @staticmethod
+    def forward(ctx, idx, table, base):
+        _lib.require_device(idx, table, base)
+        idx = idx.contiguous()
+        if idx.dtype != torch.int64:
+            idx = idx.long()
+        nb, E = table.shape
+        table = table.contiguous()
+        if base is not None:
+            base = base.contiguous()
+            if base.shape != (*idx.shape, E):
+                raise RuntimeError("embedding base must be [*idx.shape, E]")
+        out = torch.empty((*idx.shape, E), dtype=torch.float32, device=table.device)
+        n = idx.numel()
+        lib.embed_fwd(idx.data_ptr(), max(n, 1), n, table.data_ptr(), E, ptr(base), E,
+                      out.data_ptr(), E, stream())
+        ctx.save_for_backward(idx)
+        ctx.nb, ctx.E = nb, E
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (idx,) = ctx.saved_tensors
+        dout = dout.contiguous()
+        n = idx.numel()
+        dt = None
+        if ctx.needs_input_grad[1]:
+            dt = torch.empty((ctx.nb, ctx.E), dtype=torch.float32, device=dout.device)
+            ws = _ws(lib.embed_bwd_workspace(n, ctx.E, ctx.nb), dout.device)
+            lib.embed_bwd(idx.data_ptr(), max(n, 1), n, dout.data_ptr(), ctx.E, ctx.E, ctx.nb,
+                          dt.data_ptr(), 0, ws.data_ptr(), stream())
+        return None, dt, (dout if ctx.needs_input_grad[2] else None)
+
+
+def embedding(idx, table, base=None):
+    return EmbedFn.apply(idx, table, base)
+
+
+class RepeatFn(torch.autograd.Function):
+    """p [*S] -> p[None].repeat(B, ...) ; backward sums over B (HIP reduction)."""
+
+    @staticmethod
+    def forward(ctx, p, B):
+        _lib.require_device(p)
+        ctx.shape = p.shape
+        return p.unsqueeze(0).expand(B, *p.shape).contiguous()
+
+    @staticmethod
+    def backward(ctx, d):
+        d = d.contiguous()
+        B = d.shape[0]
+        F = d[0].numel()
+        out = torch.empty(ctx.shape, dtype=torch.float32, device=d.device)
+        lib.sum_leading(d.data_ptr(), B, F, out.data_ptr(), 0, stream())
+        return out, None
+
+
+def repeat_batch(p, B):
+    return RepeatFn.apply(p, int(B))
+
+
+# ---------------------------------------------------------------------------
+# posterior head, sampler, likelihood scale
+# ---------------------------------------------------------------------------
+class LatentHeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, bott, Lz):
+        _lib.require_device(bott)
+        bott = bott.contiguous()
+        B, L2, Dz = bott.shape
+        if L2 != 2 * Lz:
+            raise RuntimeError("bottleneck length must be 2*latent_len")
+        mu = torch.empty((B, Lz, Dz), dtype=torch.float32, device=bott.device)
+        sc = torch.empty_like(mu)
+        lib.latent_head_fwd(bott.data_ptr(), B, Lz * Dz, mu.data_ptr(), sc.data_ptr(), stream())
+        ctx.save_for_backward(bott)
+        ctx.n = Lz * Dz
+        return mu, sc
+
+    @staticmethod
+    def backward(ctx, dmu, dsc):
+        (bott,) = ctx.saved_tensors
+        dmu = dmu.contiguous() if dmu is not None else None
+        dsc = dsc.contiguous() if dsc is not None else None
+        db = torch.empty_like(bott)
+        lib.latent_head_bwd(bott.data_ptr(), bott.shape[0], ctx.n, ptr(dmu), ptr(dsc),
+                            db.data_ptr(), stream())
+        return db, None
+
+
+def latent_head(bott, latent_len):
+    return LatentHeadFn.apply(bott, int(latent_len))
+
+
+class RsampleFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, loc, scale, u):
+        _lib.require_device(loc, scale, u)
+        loc = loc.contiguous()
+        scale = scale.contiguous()
+        K = u.shape[0]
+        n = loc.numel()
+        z = torch.empty((K, *loc.shape), dtype=torch.float32, device=loc.device)
+        lib.rsample_fwd(loc.data_ptr(), scale.data_ptr(), u.data_ptr(), K, n, z.data_ptr(),
+                        stream())
+        ctx.save_for_backward(u)
+        ctx.K, ctx.n, ctx.shape = K, n, loc.shape
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        (u,) = ctx.saved_tensors
+        dz = dz.contiguous()
+        dl = torch.empty(ctx.shape, dtype=torch.float32, device=dz.device)
+        ds = torch.empty_like(dl)
+        lib.rsample_bwd(dz.data_ptr(), u.data_ptr(), ctx.K, ctx.n, dl.data_ptr(), ds.data_ptr(),
+                        stream())
+        return dl, ds, None
+
+
+def laplace_rsample(loc, scale, K):
+    """Laplace(loc, scale).rsample([K]) with a device (or injected) uniform draw."""
+    u = rng.draw_uniform((K, *loc.shape), loc.device)
+    return RsampleFn.apply(loc, scale, u)
+
+
+def mask_scale(mask, K, big, shape_like):
+    """1 + big*mask repeated K times -> [K*B, L] (no gradient)."""
+    m = _mask_u8(mask)
+    out = torch.empty((K * m.shape[0], m.shape[1]), dtype=torch.float32, device=m.device)
+    lib.mask_scale(m.data_ptr(), m.numel(), K, float(big), out.data_ptr(), stream())
+    return out
+
+
+# ---------------------------------------------------------------------------
+# objectives
+# ---------------------------------------------------------------------------
+class IwaeLwFn(torch.autograd.Function):
+    """_m_iwae's lw [2K, B] from the 2x2 likelihood cells and the posteriors."""
+
+    @staticmethod
+    def forward(ctx, x0, x1, llik, l00, l01, l10, l11, s00, s01, s10, s11, z0, z1, mu0, sc0,
+                mu1, sc1, pzl, pzs):
+        ts = [x0, x1, l00, l01, l10, l11, s00, s01, s10, s11, z0, z1, mu0, sc0, mu1, sc1, pzl, pzs]
+        _lib.require_device(*ts)
+        ts = [t.contiguous() for t in ts]
+        x0, x1, l00, l01, l10, l11, s00, s01, s10, s11, z0, z1, mu0, sc0, mu1, sc1, pzl, pzs = ts
+        K, B = l00.shape[0], l00.shape[1]
+        n = mu0[0].numel()
+        lw = torch.empty((2 * K, B), dtype=torch.float32, device=x0.device)
+        ctx.meta = (K, B, n, [float(v) for v in llik], [x0.shape[-1], x1.shape[-1]])
+        a = IwaeLwFn._arrays(ctx.meta, ts)
+        lib.iwae_lw_fwd(*a, pzl.data_ptr(), pzs.data_ptr(), K, B, n, lw.data_ptr(), stream())
+        ctx.save_for_backward(*ts)
+        return lw
+
+    @staticmethod
+    def _arrays(meta, ts):
+        K, B, n, llik, L = meta
+        x0, x1, l00, l01, l10, l11, s00, s01, s10, s11, z0, z1, mu0, sc0, mu1, sc1 = ts[:16]
+        return (_lib.ptr_array([x0, x1]), (C.c_float * 2)(*llik), (C.c_int * 2)(*L),
+                _lib.ptr_array([l00, l01, l10, l11]), _lib.ptr_array([s00, s01, s10, s11]),
+                _lib.ptr_array([z0, z1]), _lib.ptr_array([mu0, mu1]), _lib.ptr_array([sc0, sc1]))
+
+    @staticmethod
+    def backward(ctx, dlw):
+        ts = ctx.saved_tensors
+        K, B, n, llik, L = ctx.meta
+        dlw = dlw.contiguous()
+        ng = ctx.needs_input_grad
+        # input index: 3..6 loc cells, 11..12 zs, 13..16 mu0 sc0 mu1 sc1
+        loc_in = ts[2:6]
+        dloc = [torch.empty_like(t) if ng[3 + i] else None for i, t in enumerate(loc_in)]
+        dz = [torch.empty_like(ts[10 + i]) if ng[11 + i] else None for i in range(2)]
+        dmu = [torch.empty_like(ts[12]) if ng[13] else None, torch.empty_like(ts[14]) if ng[15] else None]
+        dsc = [torch.empty_like(ts[13]) if ng[14] else None, torch.empty_like(ts[15]) if ng[16] else None]
+        a = IwaeLwFn._arrays(ctx.meta, ts)
+        lib.iwae_lw_bwd(*a, ts[16].data_ptr(), ts[17].data_ptr(), K, B, n, dlw.data_ptr(),
+                        _lib.ptr_array(dloc), _lib.ptr_array(dz), _lib.ptr_array(dmu),
+                        _lib.ptr_array(dsc), stream())
+        return (None, None, None, *dloc, None, None, None, None, dz[0], dz[1], dmu[0], dsc[0],
+                dmu[1], dsc[1], None, None)
+
+
+class LmeSumFn(torch.autograd.Function):
+    """sum_b log_mean_exp_j lw[j, b]."""
+
+    @staticmethod
+    def forward(ctx, lw):
+        _lib.require_device(lw)
+        lw = lw.contiguous()
+        J, B = lw.shape
+        loss = torch.empty((), dtype=torch.float32, device=lw.device)
+        lib.lme_sum_fwd(lw.data_ptr(), J, B, loss.data_ptr(), stream())
+        ctx.save_for_backward(lw)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (lw,) = ctx.saved_tensors
+        J, B = lw.shape
+        g = g.contiguous()
+        dlw = torch.empty_like(lw)
+        lib.lme_sum_bwd(lw.data_ptr(), J, B, g.data_ptr(), dlw.data_ptr(), stream())
+        return dlw
+
+
+class ElboFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, llik, loc, scale, mu, sc, pzl, pzs):
+        ts = [x, loc, scale, mu, sc, pzl, pzs]
+        _lib.require_device(*ts)
+        x, loc, scale, mu, sc, pzl, pzs = [t.contiguous() for t in ts]
+        K, B, L = loc.shape[0], loc.shape[1], loc[0, 0].numel()
+        n = mu[0].numel()
+        lpx = torch.empty((K, B), dtype=torch.float32, device=x.device)
+        loss = torch.empty((), dtype=torch.float32, device=x.device)
+        lib.elbo_fwd(x.data_ptr(), L, float(llik), loc.data_ptr(), scale.data_ptr(),
+                     mu.data_ptr(), sc.data_ptr(), pzl.data_ptr(), pzs.data_ptr(), K, B, n,
+                     lpx.data_ptr(), loss.data_ptr(), stream())
+        ctx.meta = (K, B, L, n, float(llik))
+        ctx.save_for_backward(x, loc, scale, mu, sc, pzl, pzs)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, loc, scale, mu, sc, pzl, pzs = ctx.saved_tensors
+        K, B, L, n, llik = ctx.meta
+        g = g.contiguous()
+        dloc = torch.empty_like(loc)
+        dmu = torch.empty_like(mu)
+        dsc = torch.empty_like(sc)
+        lib.elbo_bwd(x.data_ptr(), L, llik, loc.data_ptr(), scale.data_ptr(), mu.data_ptr(),
+                     sc.data_ptr(), pzl.data_ptr(), pzs.data_ptr(), K, B, n, g.data_ptr(),
+                     dloc.data_ptr(), dmu.data_ptr(), dsc.data_ptr(), stream())
+        return None, None, dloc, None, dmu, dsc, None, None

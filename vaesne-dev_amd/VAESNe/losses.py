@@ -1,0 +1,78 @@
+"""Objectives, MI355X build (reference: losses.py).
+
+Same functions and signatures as the reference; the log-probability / KL /
+log-mean-exp arithmetic runs in fused HIP kernels reading the tensors of the
+Laplace objects the models return:
+
+    elbo(model, x, K=1, debug=False)   losses.py:16-24   (mean over K*B)
+    _m_iwae(model, x, K=1) -> lw       losses.py:47-62   ([2K, B])
+    m_iwae(model, x, K=1)              losses.py:78-93   (sum over B)
+    compute_microbatch_split           losses.py:68-76
+"""
+import numpy as np
+import torch
+
+from . import _ops
+
+
+def expand_first_dim(t, K):
+    shape = t.shape
+    return t.unsqueeze(0).expand((K,) + shape)
+
+
+def _pz(model):
+    p = model.pz_params
+    return p[0], p[1]
+
+
+def elbo(model, x, K=1, debug=False):
+    """E_{p(x)}[ELBO]: mean_{k,b}(llik * sum_L log p(x|z)) - mean_b sum KL(q(z|x) || p(z))."""
+    qz_x, px_z, _ = model(x, K)
+    pz_loc, pz_scale = _pz(model)
+    loss = _ops.ElboFn.apply(x[0], float(model.llik_scaling), px_z.loc, px_z.scale, qz_x.loc,
+                             qz_x.scale, pz_loc, pz_scale)
+    if debug:
+        print(f"elbo: {loss.item()}")
+    return loss
+
+
+def _m_iwae(model, x, K=1):
+    """IWAE log-weights for the 2-modality MoE VAE -> lw [2*K, B]."""
+    if len(model.vaes) != 2:
+        raise NotImplementedError("fused m_iwae covers the reference's two-modality photospecMMVAE")
+    qz_xs, px_zs, zss = model(x, K)
+    pz_loc, pz_scale = _pz(model)
+    llik = [float(model.vaes[0].llik_scaling), float(model.vaes[1].llik_scaling)]
+    return _ops.IwaeLwFn.apply(
+        x[0][0], x[1][0], llik,
+        px_zs[0][0].loc, px_zs[0][1].loc, px_zs[1][0].loc, px_zs[1][1].loc,
+        px_zs[0][0].scale, px_zs[0][1].scale, px_zs[1][0].scale, px_zs[1][1].scale,
+        zss[0], zss[1], qz_xs[0].loc, qz_xs[0].scale, qz_xs[1].loc, qz_xs[1].scale,
+        pz_loc, pz_scale)
+
+
+def is_multidata(dataB):
+    return isinstance(dataB, list)
+
+
+def compute_microbatch_split(x, K):
+    """losses.py:68-76 (a memory heuristic of the reference; never splits at
+    realistic batch sizes)."""
+    B = x[0][0].size(0) if is_multidata(x) else x[0].size(0)
+    S = sum([1.0 / (K * np.prod(_x[0].size()[1:])) for _x in x]) if is_multidata(x) \
+        else 1.0 / (K * np.prod(x[0].size()[1:]))
+    S = int(1e8 * S)
+    assert (S > 0), "Cannot fit individual data in memory, consider smaller K"
+    return min(B, S)
+
+
+def m_iwae(model, x, K=1):
+    """IWAE estimate of log p(x) for the multimodal VAE: sum_b LME_{2K} lw."""
+    S = compute_microbatch_split(x, K)
+    n_chunk = len(x[0][0].split(S))
+    lw = []
+    for i in range(n_chunk):
+        split_i = tuple(tuple(tensor.split(S)[i] for tensor in tensor_tuple) for tensor_tuple in x)
+        lw.append(_m_iwae(model, split_i, K))
+    lw = lw[0] if len(lw) == 1 else torch.cat(lw, 1)
+    return _ops.LmeSumFn.apply(lw)

@@ -1,0 +1,61 @@
+"""Mixture-of-experts multimodal VAE over (light curve, spectrum) pairs,
+MI355X build (reference: mmVAE.py:71-132, photospecMMVAE)."""
+import torch
+import torch.distributions as dist
+import torch.nn as nn
+
+from . import _ops
+
+
+class photospecMMVAE(nn.Module):
+    def __init__(self, vaes, prior_dist=dist.Laplace, beta=1., length_ratio=982 / 60):
+        super().__init__()
+        self.pz = prior_dist
+        self.vaes = nn.ModuleList(vaes)
+        self.modelName = "photospectra"
+        self._pz_params = nn.ParameterList([
+            nn.Parameter(torch.zeros(vaes[0].latent_len, vaes[0].latent_dim), requires_grad=False),
+            nn.Parameter(torch.ones(vaes[0].latent_len, vaes[0].latent_dim), requires_grad=False),
+        ])
+        # mmVAE.py:82-84
+        self.vaes[0].llik_scaling = 1. / beta
+        self.vaes[1].llik_scaling = 1. / beta
+        self.vaes[0].llik_scaling *= length_ratio
+
+    @property
+    def pz_params(self):
+        return self._pz_params
+
+    def forward(self, x, K=1):
+        """mmVAE.py:91-106: diagonal cells from each VAE's forward, off-diagonal
+        px_zs[e][d] = vaes[d].decode(zs_e, x[d])."""
+        qz_xs, zss = [], []
+        px_zs = [[None for _ in range(len(self.vaes))] for _ in range(len(self.vaes))]
+        for m, vae in enumerate(self.vaes):
+            qz_x, px_z, zs = vae(x[m], K=K)
+            qz_xs.append(qz_x)
+            zss.append(zs)
+            px_zs[m][m] = px_z
+        for e, zs in enumerate(zss):
+            for d, vae in enumerate(self.vaes):
+                if e != d:
+                    px_zs[e][d] = vae.decode(zs, x[d])
+        return qz_xs, px_zs, zss
+
+    def generate(self, N, x):
+        """mmVAE.py:108-118: N prior draws per conditioning example, decoded by
+        every modality."""
+        self.eval()
+        with torch.no_grad():
+            B = x[0][0].shape[0]
+            loc = self._pz_params[0].expand(B, *self._pz_params[0].shape).contiguous()
+            scale = self._pz_params[1].expand(B, *self._pz_params[1].shape).contiguous()
+            latents = _ops.laplace_rsample(loc, scale, N)
+            return [vae.decode(latents, x[d]).mean for d, vae in enumerate(self.vaes)]
+
+    def reconstruct(self, data, K=1):
+        """mmVAE.py:120-126: cross-modal matrix of reconstruction means."""
+        self.eval()
+        with torch.no_grad():
+            _, px_zs, _ = self.forward(data, K=K)
+            return [[px_z.mean for px_z in r] for r in px_zs]

@@ -1,0 +1,212 @@
+"""Building blocks of the VAESNe transformer stacks, MI355X build.
+
+Mirrors the hot-path symbols of the reference's util_layers.py (same class
+names, constructor signatures, attribute and state_dict names) so checkpoints'
+state_dicts and the cannon scripts keep working:
+
+    singlelayerMLP            util_layers.py:9-18
+    MLP                       util_layers.py:20-34
+    SinusoidalPositionalEmbedding     :113-129
+    SinusoidalMLPPositionalEmbedding  :131-149
+    TransformerBlock          util_layers.py:257-309
+    get_mean / log_mean_exp / kl_divergence   :313-336
+
+Forward passes run on the HIP kernels (VAESNe._ops); there is no CPU path.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+from . import _ops
+
+
+class Linear(nn.Linear):
+    """nn.Linear whose forward runs on the HIP linear kernel."""
+
+    def forward(self, x, act=None, x2=None, base=None):
+        return _ops.linear(x, self.weight, self.bias, act=act, x2=x2, base=base)
+
+
+########### simple MLPs ###############
+class singlelayerMLP(nn.Module):
+    """fc2(relu(fc1(x))) — util_layers.py:9-18.  `x2` (optional) is added to x
+    inside the first kernel (the reference's `f(x + h)` residual calls)."""
+
+    def __init__(self, in_dim, out_dim):
+        super().__init__()
+        self.fc1 = Linear(in_dim, in_dim)
+        self.fc2 = Linear(in_dim, out_dim)
+
+    def forward(self, x, x2=None):
+        return self.fc2(self.fc1(x, act="relu", x2=x2))
+
+
+class MLP(nn.Module):
+    """Linear -> ReLU -> ... -> Linear — util_layers.py:20-34 (keys mlp.0, mlp.2, ...)."""
+
+    def __init__(self, in_dim, out_dim, hidden_dim=[64, 64]):
+        super().__init__()
+        layers = []
+        for i in range(len(hidden_dim)):
+            layers.append(Linear(in_dim if i == 0 else hidden_dim[i - 1], hidden_dim[i]))
+            layers.append(nn.ReLU())
+        layers.append(Linear(hidden_dim[-1], out_dim))
+        self.mlp = nn.Sequential(*layers)
+
+    def forward(self, x):
+        mods = list(self.mlp)
+        for i in range(0, len(mods) - 1, 2):
+            x = mods[i](x, act="relu")
+        return mods[-1](x)
+
+
+################# positional encoding ###################
+class _DivTerm:
+    """The reference's div_term, computed on the host exactly as the reference
+    (fp32 torch ops), cached per device (the reference re-copies it H2D on every
+    call, util_layers.py:127,144)."""
+
+    def __init__(self, t: torch.Tensor):
+        self.cpu = t
+        self._dev = {}
+
+    def on(self, device):
+        key = str(device)
+        d = self._dev.get(key)
+        if d is None:
+            d = self.cpu.to(device)
+            self._dev[key] = d
+        return d
+
+
+class SinusoidalPositionalEmbedding(nn.Module):
+    """[sin(x*d), cos(x*d)] with d = exp(arange(0,dim,2) * -ln(1e4)/dim) — util_layers.py:113-129."""
+
+    def __init__(self, dim=64):
+        super().__init__()
+        self.dim = dim
+        self._div = _DivTerm(torch.exp(torch.arange(0, dim, 2).float() *
+                                       (-torch.log(torch.tensor(10000.0)) / dim)))
+
+    @property
+    def div_term(self):
+        return self._div.cpu
+
+    def forward(self, x):
+        return _ops.sincos(x, self._div.on(x.device))
+
+
+class SinusoidalMLPPositionalEmbedding(nn.Module):
+    """sin/cos over d = exp(arange(dim) * -ln(1e4)/dim), then fc2(relu(fc1(.)))
+    — util_layers.py:131-149."""
+
+    def __init__(self, dim=64):
+        super().__init__()
+        self.dim = dim
+        self._div = _DivTerm(torch.exp(torch.arange(0, dim).float() *
+                                       (-torch.log(torch.tensor(10000.0)) / dim)))
+        self.fc1 = Linear(2 * dim, dim)
+        self.fc2 = Linear(dim, dim)
+
+    @property
+    def div_term(self):
+        return self._div.cpu
+
+    def forward(self, x):
+        enc = _ops.sincos(x, self._div.on(x.device))
+        return self.fc2(self.fc1(enc, act="relu"))
+
+
+################# attention ###################
+class MultiheadAttention(nn.MultiheadAttention):
+    """nn.MultiheadAttention (same parameters, init and state_dict keys) whose
+    forward runs the fused HIP path: packed in-projection kernel, flash-style
+    masked attention kernel (dropout on the probabilities in train mode), then
+    the out-projection kernel.  Returns (output, None): the reference discards
+    the head-averaged weights at every call site (util_layers.py:289,297,301)."""
+
+    def forward(self, query, key, value, key_padding_mask=None, need_weights=True,
+                attn_mask=None, average_attn_weights=True, is_causal=False):
+        if attn_mask is not None or is_causal:
+            raise NotImplementedError("VAESNe attention: attn_mask / is_causal are not used by the reference")
+        if not self.batch_first:
+            raise NotImplementedError("VAESNe attention is batch_first (as the reference)")
+        if key is not value:
+            raise NotImplementedError("VAESNe attention expects key is value")
+        E, H = self.embed_dim, self.num_heads
+        p = self.dropout if self.training else 0.0
+        W, b = self.in_proj_weight, self.in_proj_bias
+        if query is key:
+            qkv = _ops.linear(query, W, b)
+            o = _ops.self_attention(qkv, key_padding_mask, H, p)
+        else:
+            q = _ops.linear(query, W[:E], b[:E])
+            kv = _ops.linear(key, W[E:], b[E:])
+            o = _ops.cross_attention(q, kv, key_padding_mask, H, p)
+        return _ops.linear(o, self.out_proj.weight, self.out_proj.bias), None
+
+
+class TransformerBlock(nn.Module):
+    """Post-LN block with optional context self-attention and cross-attention
+    — util_layers.py:257-309.  Each residual join is one fused
+    residual+dropout+LayerNorm kernel; the FFN is Linear+GELU fused, Linear."""
+
+    def __init__(self, embed_dim, num_heads, ff_dim, dropout=0.1, context_self_attn=False):
+        super().__init__()
+        self.self_attn = MultiheadAttention(embed_dim, num_heads, dropout=dropout, batch_first=True)
+        self.cross_attn = MultiheadAttention(embed_dim, num_heads, dropout=dropout, batch_first=True)
+        if context_self_attn:
+            self.context_self_attn = MultiheadAttention(embed_dim, num_heads, dropout=dropout,
+                                                        batch_first=True)
+            self.layernorm_context = nn.LayerNorm(embed_dim)
+        else:
+            self.context_self_attn = None
+        self.ffn = nn.Sequential(
+            Linear(embed_dim, ff_dim),
+            nn.GELU(),
+            Linear(ff_dim, embed_dim),
+        )
+        self.layernorm1 = nn.LayerNorm(embed_dim)
+        self.layernorm2 = nn.LayerNorm(embed_dim)
+        self.layernorm3 = nn.LayerNorm(embed_dim)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x, context=None, mask=None, context_mask=None):
+        p = self.dropout.p if self.training else 0.0
+        a, _ = self.self_attn(x, x, x, key_padding_mask=mask)
+        x = _ops.add_layernorm(x, a, self.layernorm1, p)
+        if context is not None:
+            if self.context_self_attn is not None:
+                c, _ = self.context_self_attn(context, context, context, key_padding_mask=context_mask)
+                context = _ops.add_layernorm(context, c, self.layernorm_context, p)
+            a, _ = self.cross_attn(x, context, context, key_padding_mask=context_mask)
+            x = _ops.add_layernorm(x, a, self.layernorm2, p)
+        f = self.ffn[2](self.ffn[0](x, act="gelu"))
+        return _ops.add_layernorm(x, f, self.layernorm3, p)
+
+
+############## vae use ###################
+def get_mean(d, K=100):
+    """util_layers.py:313-323."""
+    try:
+        mean = d.mean
+    except NotImplementedError:
+        samples = d.rsample(torch.Size([K]))
+        mean = samples.mean(0)
+    return mean
+
+
+def log_mean_exp(value, dim=0, keepdim=False):
+    """util_layers.py:326-327 (API utility; the fused objectives do not call it)."""
+    return torch.logsumexp(value, dim, keepdim=keepdim) - math.log(value.size(dim))
+
+
+def kl_divergence(d1, d2, K=100):
+    """util_layers.py:330-336 (API utility; `losses.elbo` uses the fused kernel)."""
+    if (type(d1), type(d2)) in torch.distributions.kl._KL_REGISTRY:
+        return torch.distributions.kl_divergence(d1, d2)
+    samples = d1.rsample(torch.Size([K]))
+    return (d1.log_prob(samples) - d2.log_prob(samples)).mean(0)

@@ -1,0 +1,69 @@
+"""Build libvaesne_hip.so for gfx950 (MI355X) in-tree.
+
+    python vaesne-dev_amd/build_lib.py          # -> vaesne-dev_amd/lib/libvaesne_hip.so
+
+Each csrc/*.hip is compiled with hipcc --offload-arch=gfx950 in parallel and
+linked into one shared library with a plain C ABI (include/vaesne_hip.h).
+The library links libamdhip64.so.7 by soname only; in a process that has
+imported torch first, that resolves to the HIP runtime torch already loaded
+(one HIP runtime per process).
+"""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+OBJDIR = os.path.join(HERE, "build")
+LIB = os.path.join(LIBDIR, "libvaesne_hip.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fvisibility=hidden",
+          "-I" + os.path.join(ROOT, "include"), "-Wall", "-Wno-unused-function"]
+
+
+def sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+
+
+def _deps_mtime():
+    paths = sources() + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    paths.append(os.path.join(ROOT, "include", "vaesne_hip.h"))
+    return max(os.path.getmtime(p) for p in paths)
+
+
+def _compile(src):
+    obj = os.path.join(OBJDIR, os.path.basename(src)[:-4] + ".o")
+    cmd = [HIPCC, "-c", *CFLAGS, "-o", obj, src]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+    return obj
+
+
+def build(force=False, verbose=True):
+    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(OBJDIR, exist_ok=True)
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime():
+        if verbose:
+            print(f"[vaesne] {LIB} up to date")
+        return LIB
+    srcs = sources()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(_compile, srcs))
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", tmp, *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    os.replace(tmp, LIB)
+    if verbose:
+        print(f"[vaesne] built {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,108 @@
+// Shared device helpers for the VAESNe gfx950 kernels.
+//
+// Conventions (see include/vaesne_hip.h):
+//   * every entry point is extern "C", takes raw device pointers, element
+//     strides and a hipStream_t, and returns a hipError_t as int;
+//   * all arithmetic is fp32 (the reference computes in fp32);
+//   * reductions are two-stage (per-workgroup partials -> fixed-order sum),
+//     so every result is bitwise reproducible run to run;
+//   * random numbers are counter-based: a value depends only on
+//     (seed, counter, call id, element coordinates), so the forward and the
+//     backward kernels regenerate the same dropout mask, and a captured
+//     hipGraph gets fresh draws by advancing the device-side counter.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "vaesne_hip.h"  // the C ABI: definitions below must match it
+
+#define VAESNE_API extern "C" __attribute__((visibility("default")))
+
+#define VAESNE_CHECK_LAUNCH() \
+  do {                        \
+    hipError_t e__ = hipGetLastError(); \
+    if (e__ != hipSuccess) return (int)e__; \
+  } while (0)
+
+namespace vaesne {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Counter-based RNG.
+//
+// rng_state points at a device int64[2] = {seed, counter}.  A call site passes
+// a host-side call id; the triple (seed, counter, call id) keys a stream and
+// the element coordinates select the value.  `mix32` is a 2-multiply
+// avalanche finaliser (lowbias32); `key_of` folds the 64-bit seed, the
+// counter and the call id into one 32-bit stream key.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t key_of(const int64_t* rng_state, uint32_t call_id) {
+  uint64_t seed = (uint64_t)rng_state[0];
+  uint64_t ctr = (uint64_t)rng_state[1];
+  uint32_t k = mix32((uint32_t)seed ^ 0x243f6a88u);
+  k = mix32(k ^ (uint32_t)(seed >> 32) ^ 0x85a308d3u);
+  k = mix32(k ^ (uint32_t)ctr);
+  k = mix32(k ^ (uint32_t)(ctr >> 32) ^ 0x13198a2eu);
+  k = mix32(k ^ (call_id * 0x9e3779b9u));
+  return k;
+}
+
+// 32 random bits for element `idx` of stream `key`.
+__device__ __forceinline__ uint32_t rand_u32(uint32_t key, uint64_t idx) {
+  uint32_t h = mix32(key ^ (uint32_t)idx * 0x9e3779b1u);
+  return mix32(h ^ (uint32_t)(idx >> 32) ^ 0x6a09e667u);
+}
+
+// Attention-probability dropout: one 32-bit hash covers a PAIR of keys
+// (low 16 bits -> key 2*kp, high 16 bits -> key 2*kp+1).  `row_key` is the
+// per-(batch,head,query) key.
+__device__ __forceinline__ uint32_t attn_row_key(uint32_t key, uint32_t row) {
+  return mix32(key ^ (row * 0x9e3779b1u));
+}
+__device__ __forceinline__ uint32_t attn_pair_bits(uint32_t row_key, uint32_t kp) {
+  return mix32(row_key ^ (kp * 0x85ebca6bu + 0xc2b2ae35u));
+}
+
+// keep threshold: an element is DROPPED when its 16-bit value < thr16,
+// thr16 = round(p * 65536)  (p_eff = thr16 / 65536; 0.1 -> 6554 -> 0.100006).
+__host__ __device__ __forceinline__ uint32_t drop_thr16(float p) {
+  float t = p * 65536.0f + 0.5f;
+  if (t <= 0.f) return 0u;
+  if (t >= 65536.f) return 65536u;
+  return (uint32_t)t;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  // d/dx [0.5 x (1 + erf(x/sqrt2))] = 0.5(1+erf(x/sqrt2)) + x * exp(-x^2/2)/sqrt(2pi)
+  return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) +
+         x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
+
+__host__ __device__ __forceinline__ int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+}  // namespace vaesne

@@ -1,0 +1,383 @@
+// Small fused elementwise kernels of the VAESNe step:
+//   * sinusoidal features  (SinusoidalPositionalEmbedding / the front half of
+//     SinusoidalMLPPositionalEmbedding, util_layers.py:125-129,142-146)
+//   * nn.Embedding gather / deterministic scatter-add (band embeddings,
+//     PhotometricLayers.py:63,129)
+//   * latent head: mu = b[:, :Lz], scale = softplus(b[:, Lz:])
+//     (PhotometricVAE.py:53-54, SpectraVAE.py:48-49; torch softplus, threshold 20)
+//   * Laplace.rsample with a counter-based uniform draw
+//     (torch/distributions/laplace.py:74-86)
+//   * likelihood scale 1 + big*mask (PhotometricVAE.py:89-94, SpectraVAE.py:82-87)
+//   * fused AdamW over one flat parameter buffer (torch.optim.AdamW semantics),
+//     gradient packing, RNG counter advance.
+#include "common.h"
+
+using namespace vaesne;
+
+namespace {
+constexpr int NT = 256;
+
+inline unsigned blocks_for(int64_t n, int per = NT, int64_t cap = 1 << 20) {
+  int64_t b = (n + per - 1) / per;
+  if (b > cap) b = cap;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+__global__ void sincos_kernel(const float* __restrict__ x, int64_t period, int64_t rows,
+                              const float* __restrict__ div, int nf, float* __restrict__ out,
+                              int64_t ldo) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = rows * nf;
+  for (; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = t / nf;
+    int f = (int)(t - r * nf);
+    float a = x[r % period] * div[f];
+    float sv, cv;
+    sincosf(a, &sv, &cv);
+    out[r * ldo + f] = sv;
+    out[r * ldo + nf + f] = cv;
+  }
+}
+
+__global__ void embed_fwd_kernel(const int64_t* __restrict__ idx, int64_t period, int64_t rows,
+                                 const float* __restrict__ table, int E,
+                                 const float* __restrict__ base, int64_t ldb,
+                                 float* __restrict__ out, int64_t ldo) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = rows * E;
+  for (; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = t / E;
+    int e = (int)(t - r * E);
+    float v = table[idx[r % period] * E + e];
+    if (base) v += base[r * ldb + e];
+    out[r * ldo + e] = v;
+  }
+}
+
+// dtable partials: thread (e = tid % E, g = tid / E) walks rows g, g+G, ...;
+// per-class accumulators in registers (nb <= 16), fixed-order block reduce.
+template <int NB>
+__global__ __launch_bounds__(NT) void embed_bwd_kernel(const int64_t* __restrict__ idx,
+                                                       int64_t period, int64_t rows,
+                                                       const float* __restrict__ dout,
+                                                       int64_t lddo, int E, int nb,
+                                                       float* __restrict__ partial) {
+  __shared__ float red[NT * NB];
+  const int groups = NT / E;
+  const int e = threadIdx.x % E;
+  const int g = threadIdx.x / E;
+  float acc[NB];
+#pragma unroll
+  for (int c = 0; c < NB; ++c) acc[c] = 0.f;
+  if (g < groups) {
+    for (int64_t r = (int64_t)blockIdx.x * groups + g; r < rows; r += (int64_t)gridDim.x * groups) {
+      int c = (int)idx[r % period];
+      float v = dout[r * lddo + e];
+#pragma unroll
+      for (int cc = 0; cc < NB; ++cc) acc[cc] += (cc == c) ? v : 0.f;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NB; ++c) red[c * NT + threadIdx.x] = (g < groups) ? acc[c] : 0.f;
+  __syncthreads();
+  for (int f = threadIdx.x; f < nb * E; f += NT) {
+    int c = f / E, ee = f - c * E;
+    float s = 0.f;
+    for (int gg = 0; gg < groups; ++gg) s += red[c * NT + gg * E + ee];
+    partial[(int64_t)blockIdx.x * nb * E + f] = s;
+  }
+}
+
+__global__ void reduce_rows_kernel(const float* __restrict__ partial, int G, int F,
+                                   float* __restrict__ out, int accum) {
+  int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += partial[(int64_t)g * F + f];
+  out[f] = accum ? out[f] + s : s;
+}
+
+// bottleneck [B, 2*Lz, Dz] -> mu [B, Lz*Dz], scale [B, Lz*Dz]
+__global__ void latent_head_fwd_kernel(const float* __restrict__ bott, int B, int n,
+                                       float* __restrict__ mu, float* __restrict__ scale) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)B * n) return;
+  int64_t b = t / n;
+  int j = (int)(t - b * n);
+  mu[t] = bott[b * 2 * n + j];
+  float x = bott[b * 2 * n + n + j];
+  scale[t] = x > 20.f ? x : log1pf(expf(x));
+}
+
+__global__ void latent_head_bwd_kernel(const float* __restrict__ bott, int B, int n,
+                                       const float* __restrict__ dmu,
+                                       const float* __restrict__ dscale,
+                                       float* __restrict__ dbott) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)B * n) return;
+  int64_t b = t / n;
+  int j = (int)(t - b * n);
+  dbott[b * 2 * n + j] = dmu ? dmu[t] : 0.f;
+  float x = bott[b * 2 * n + n + j];
+  float g = dscale ? dscale[t] : 0.f;
+  float z = expf(x);
+  dbott[b * 2 * n + n + j] = x > 20.f ? g : g * z / (z + 1.f);
+}
+
+// u ~ U(eps - 1, 1) as torch's uniform_(a, b): 24-bit mantissa draw in [0,1)
+__device__ __forceinline__ float uniform_sym(uint32_t bits) {
+  const float eps = 1.1920928955078125e-07f;
+  float x = (float)(bits >> 8) * 5.9604644775390625e-08f;
+  return x * (1.f - (eps - 1.f)) + (eps - 1.f);
+}
+
+__global__ void uniform_kernel(float* __restrict__ u, int64_t n, const int64_t* rng_state,
+                               uint32_t call_id) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  u[t] = uniform_sym(rand_u32(key_of(rng_state, call_id), (uint64_t)t));
+}
+
+// z[k, b, j] = loc[b, j] - scale[b, j] * sign(u) * log1p(-|u|)
+__global__ void rsample_fwd_kernel(const float* __restrict__ loc, const float* __restrict__ scale,
+                                   const float* __restrict__ u, int K, int64_t n,
+                                   float* __restrict__ z) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  float l = loc[t], s = scale[t];
+  for (int k = 0; k < K; ++k) {
+    float uu = u[(int64_t)k * n + t];
+    float sg = uu > 0.f ? 1.f : (uu < 0.f ? -1.f : 0.f);
+    z[(int64_t)k * n + t] = l - s * sg * log1pf(-fabsf(uu));
+  }
+}
+
+__global__ void rsample_bwd_kernel(const float* __restrict__ dz, const float* __restrict__ u, int K,
+                                   int64_t n, float* __restrict__ dloc, float* __restrict__ dscale) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  float gl = 0.f, gs = 0.f;
+  for (int k = 0; k < K; ++k) {
+    float g = dz[(int64_t)k * n + t];
+    float uu = u[(int64_t)k * n + t];
+    float sg = uu > 0.f ? 1.f : (uu < 0.f ? -1.f : 0.f);
+    gl += g;
+    gs += g * (-sg * log1pf(-fabsf(uu)));
+  }
+  dloc[t] = gl;
+  dscale[t] = gs;
+}
+
+__global__ void mask_scale_kernel(const uint8_t* __restrict__ mask, int64_t n, int K, float big,
+                                  float* __restrict__ out) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  float s = 1.f + big * (float)mask[t];
+  for (int k = 0; k < K; ++k) out[(int64_t)k * n + t] = s;
+}
+
+// torch.optim.AdamW single-tensor arithmetic (torch/optim/adamw.py ->
+// adam.py _single_tensor_adam with decoupled decay): step counter on device.
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                             float* __restrict__ m, float* __restrict__ v, int64_t n,
+                             const float* __restrict__ step, float lr, float b1, float b2,
+                             float eps, float wd) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const float st = *step;
+  const float bc1 = 1.f - powf(b1, st);
+  const float bc2 = 1.f - powf(b2, st);
+  const float step_size = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  for (; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+    float w = p[t] * (1.f - lr * wd);
+    float gg = g[t];
+    float mm = m[t];
+    mm = mm + (1.f - b1) * (gg - mm);
+    float vv = v[t] * b2 + (1.f - b2) * gg * gg;
+    float denom = sqrtf(vv) / bc2s + eps;
+    p[t] = w - step_size * (mm / denom);
+    m[t] = mm;
+    v[t] = vv;
+  }
+}
+
+__global__ void incr_kernel(float* step, int64_t* rng_state) {
+  if (step) *step += 1.f;
+  if (rng_state) rng_state[1] += 1;
+}
+
+constexpr int PACK_MAX = 48;
+struct PackArgs {
+  const float* src[PACK_MAX];
+  int64_t off[PACK_MAX];
+  int64_t n[PACK_MAX];
+  int count;
+};
+
+// dst[off_i + j] = src_i[j] (or 0 when src_i is null); one block row per tensor
+__global__ void pack_kernel(PackArgs a, float* __restrict__ dst, int unpack) {
+  int i = blockIdx.y;
+  if (i >= a.count) return;
+  const int64_t n = a.n[i];
+  float* d = dst + a.off[i];
+  const float* s = a.src[i];
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    if (unpack) {
+      if (s) const_cast<float*>(s)[t] = d[t];
+    } else {
+      d[t] = s ? s[t] : 0.f;
+    }
+  }
+}
+
+}  // namespace
+
+VAESNE_API int vaesne_sincos(const float* x, int64_t period, int64_t rows, const float* div, int nf,
+                             float* out, int64_t ldo, void* stream) {
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(sincos_kernel, dim3(blocks_for(rows * nf, NT, 65536)), dim3(NT), 0,
+                     (hipStream_t)stream, x, period, rows, div, nf, out, ldo);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_embed_fwd(const int64_t* idx, int64_t period, int64_t rows,
+                                const float* table, int E, const float* base, int64_t ldb,
+                                float* out, int64_t ldo, void* stream) {
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(blocks_for(rows * E, NT, 65536)), dim3(NT), 0,
+                     (hipStream_t)stream, idx, period, rows, table, E, base, ldb, out, ldo);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int64_t vaesne_embed_bwd_workspace(int64_t rows, int E, int nb) {
+  return (int64_t)256 * nb * E * (int64_t)sizeof(float);
+}
+
+VAESNE_API int vaesne_embed_bwd(const int64_t* idx, int64_t period, int64_t rows,
+                                const float* dout, int64_t lddo, int E, int nb, float* dtable,
+                                int accum, float* workspace, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (E > NT || nb > 16 || nb < 1) return (int)hipErrorInvalidValue;
+  int groups = NT / E;
+  int G = (int)((rows + groups - 1) / groups);
+  if (G > 256) G = 256;
+  if (G < 1) G = 1;
+  if (nb <= 2)
+    hipLaunchKernelGGL(embed_bwd_kernel<2>, dim3(G), dim3(NT), 0, s, idx, period, rows, dout, lddo,
+                       E, nb, workspace);
+  else if (nb <= 8)
+    hipLaunchKernelGGL(embed_bwd_kernel<8>, dim3(G), dim3(NT), 0, s, idx, period, rows, dout, lddo,
+                       E, nb, workspace);
+  else
+    hipLaunchKernelGGL(embed_bwd_kernel<16>, dim3(G), dim3(NT), 0, s, idx, period, rows, dout,
+                       lddo, E, nb, workspace);
+  VAESNE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((nb * E + 255) / 256), dim3(256), 0, s, workspace, G,
+                     nb * E, dtable, accum);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+// out[f] (+)= sum_g in[g*F + f]  (gradient of a broadcast / repeat over G)
+VAESNE_API int vaesne_sum_leading(const float* in, int G, int F, float* out, int accum,
+                                  void* stream) {
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3((F + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     in, G, F, out, accum);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_latent_head_fwd(const float* bott, int B, int n, float* mu, float* scale,
+                                      void* stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(latent_head_fwd_kernel, dim3(blocks_for((int64_t)B * n)), dim3(NT), 0,
+                     (hipStream_t)stream, bott, B, n, mu, scale);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_latent_head_bwd(const float* bott, int B, int n, const float* dmu,
+                                      const float* dscale, float* dbott, void* stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(latent_head_bwd_kernel, dim3(blocks_for((int64_t)B * n)), dim3(NT), 0,
+                     (hipStream_t)stream, bott, B, n, dmu, dscale, dbott);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_uniform(float* u, int64_t n, const int64_t* rng_state, uint32_t call_id,
+                              void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(uniform_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream, u, n,
+                     rng_state, call_id);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_rsample_fwd(const float* loc, const float* scale, const float* u, int K,
+                                  int64_t n, float* z, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(rsample_fwd_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream,
+                     loc, scale, u, K, n, z);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_rsample_bwd(const float* dz, const float* u, int K, int64_t n, float* dloc,
+                                  float* dscale, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(rsample_bwd_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream,
+                     dz, u, K, n, dloc, dscale);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_mask_scale(const uint8_t* mask, int64_t n, int K, float big, float* out,
+                                 void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(mask_scale_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream,
+                     mask, n, K, big, out);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_adamw(float* p, const float* g, float* m, float* v, int64_t n,
+                            const float* step, float lr, float b1, float b2, float eps, float wd,
+                            void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(adamw_kernel, dim3(blocks_for(n, NT, 4096)), dim3(NT), 0,
+                     (hipStream_t)stream, p, g, m, v, n, step, lr, b1, b2, eps, wd);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_step_advance(float* step, int64_t* rng_state, void* stream) {
+  hipLaunchKernelGGL(incr_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, rng_state);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+// Pack (unpack=0: dst <- srcs) or unpack (unpack=1: srcs <- dst) up to
+// `count` tensors at a time; host passes parallel arrays.
+VAESNE_API int vaesne_pack(const float* const* srcs, const int64_t* offs, const int64_t* ns,
+                           int count, float* dst, int unpack, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  for (int base = 0; base < count; base += PACK_MAX) {
+    PackArgs a{};
+    a.count = count - base < PACK_MAX ? count - base : PACK_MAX;
+    int64_t maxn = 1;
+    for (int i = 0; i < a.count; ++i) {
+      a.src[i] = srcs[base + i];
+      a.off[i] = offs[base + i];
+      a.n[i] = ns[base + i];
+      if (a.n[i] > maxn) maxn = a.n[i];
+    }
+    unsigned gx = blocks_for(maxn, NT, 64);
+    hipLaunchKernelGGL(pack_kernel, dim3(gx, a.count), dim3(NT), 0, s, a, dst, unpack);
+    VAESNE_CHECK_LAUNCH();
+  }
+  return 0;
+}
