@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU session: parity tests -> smoke -> bench -> rocprofv3 kernel stats.
+# Each GPU step has its own time limit; a fault/abort/timeout ends the script.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 1 = assertion failures, not a GPU fault
+STAGES="${STAGES:-tests smoke bench prof}"
+for s in $STAGES; do
+  case $s in
+    tests) timeout -k 10 900 python -m pytest tests -m gpu -q -rf --timeout 300 ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1; rc=$?;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?;;
+    bench) timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?;;
+    prof)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof.log 2>&1; rc=$?;;
+  esac
+  echo "$s rc=$rc"
+  tail -5 gpurun_out/*.log 2>/dev/null | tail -0
+  ok $rc || exit $rc
+done

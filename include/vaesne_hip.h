@@ -91,6 +91,29 @@ int vaesne_attn_bwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, 
                     int H, int Lq, int Lk, int dh, float p_drop, const int64_t* rng_state,
                     uint32_t call_id, float* workspace, void* stream);
 
+/* ---- fused decoder-block tail --------------------------------------------------
+ * Everything of a decoder TransformerBlock after its masked self-attention core
+ * (util_layers.py:292-307 as called by SpectraLayers.py:61-62 and
+ * PhotometricLayers.py:66-67): out_proj -> +Drop -> LN1 -> cross-attention over
+ * the Lc <= 8 context tokens (unmasked) -> out_proj -> +Drop -> LN2 -> FFN(GELU)
+ * -> +Drop -> LN3 [-> the next block's packed in_proj].  E=32, H=4, dh=8, ff=32.
+ * x, O, y: [M, 32] with M = Nseq * L; kvc [Nseq, Lc, 64] = context k | v;
+ * w: HOST array of 18 device pointers {Wo1, bo1, g1, be1, Wq, bq, Wo2, bo2, g2,
+ * be2, W1, b1, W2, b2, g3, be3, Wn, bn} (Wq/bq = cross in_proj rows [0, 32);
+ * Wn/bn = next self in_proj [96, 32] / [96], null when not fused; qkv [M, 96]).
+ * bwd: grads = HOST array of 18 device pointers (same order, null = skip);
+ * y = the forward output; dqkv required iff Wn; workspace sized by
+ * vaesne_dec_tail_workspace. */
+int64_t vaesne_dec_tail_workspace(int M, int L, int Lc);
+int vaesne_dec_tail_fwd(const float* x, const float* O, const float* kvc, int M, int L, int Lc,
+                        const float* const* w, float p_drop, const int64_t* rng_state,
+                        uint32_t call_id, float* y, float* qkv, void* stream);
+int vaesne_dec_tail_bwd(const float* x, const float* O, const float* kvc, int M, int L, int Lc,
+                        const float* const* w, float p_drop, const int64_t* rng_state,
+                        uint32_t call_id, const float* y, const float* dy, const float* dqkv,
+                        float* dx, float* dO, float* dkvc, float* const* grads,
+                        float* workspace, void* stream);
+
 /* ---- embeddings ------------------------------------------------------------
  * [sin(x*div) | cos(x*div)]: util_layers.py:125-129 (plain, 16 freqs) and
  * :142-146 (MLP form, 32 freqs).  x is read at index r % period, so the

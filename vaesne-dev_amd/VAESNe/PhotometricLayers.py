@@ -8,7 +8,8 @@ from torch import nn
 
 from . import _ops
 from .util_layers import (MLP, Linear, SinusoidalMLPPositionalEmbedding,
-                          SinusoidalPositionalEmbedding, TransformerBlock, singlelayerMLP)
+                          SinusoidalPositionalEmbedding, TransformerBlock, decoder_stack,
+                          singlelayerMLP)
 
 
 class photometricTransformerDecoder(nn.Module):
@@ -36,8 +37,7 @@ class photometricTransformerDecoder(nn.Module):
         x = _ops.embedding(band, self.bandembd.weight, base=self.sinusoidal_time_embd(time))
         h = x
         bottleneck = self.contextfc(bottleneck)
-        for transformerblock in self.transformerblocks:
-            h = transformerblock(h, bottleneck, mask=mask)
+        h = decoder_stack(self.transformerblocks, h, bottleneck, mask)
         return self.get_photo(x, h).squeeze(-1)   # get_photo(x + h)
 
 

@@ -10,7 +10,8 @@ from torch import nn
 
 from . import _ops
 from .util_layers import (MLP, Linear, SinusoidalMLPPositionalEmbedding,
-                          SinusoidalPositionalEmbedding, TransformerBlock, singlelayerMLP)
+                          SinusoidalPositionalEmbedding, TransformerBlock, decoder_stack,
+                          singlelayerMLP)
 
 
 class spectraTransformerDecoder(nn.Module):
@@ -34,8 +35,7 @@ class spectraTransformerDecoder(nn.Module):
         phase_embd = self.phase_embd_layer(phase[:, None])
         h = x
         bottleneck = torch.cat([self.contextfc(bottleneck), phase_embd], dim=1)
-        for transformerblock in self.transformerblocks:
-            h = transformerblock(h, bottleneck, mask=mask)
+        h = decoder_stack(self.transformerblocks, h, bottleneck, mask)
         return self.get_flux(x, h).squeeze(-1)   # get_flux(x + h)
 
 

@@ -42,6 +42,10 @@ SIGNATURES = {
     "vaesne_attn_bwd": (I32, [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, P, I64, I64, P, P,
                               I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I32, I32, I32, I32,
                               I32, F32, P, U32, P, P]),
+    "vaesne_dec_tail_workspace": (I64, [I32, I32, I32]),
+    "vaesne_dec_tail_fwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P]),
+    "vaesne_dec_tail_bwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P, P, P, P, PP,
+                                  P, P]),
     "vaesne_sincos": (I32, [P, I64, I64, P, I32, P, I64, P]),
     "vaesne_embed_fwd": (I32, [P, I64, I64, P, I32, P, I64, P, I64, P]),
     "vaesne_embed_bwd_workspace": (I64, [I64, I32, I32]),

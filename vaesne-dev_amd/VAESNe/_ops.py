@@ -503,3 +503,53 @@ class ElboFn(torch.autograd.Function):
                      sc.data_ptr(), pzl.data_ptr(), pzs.data_ptr(), K, B, n, g.data_ptr(),
                      dloc.data_ptr(), dmu.data_ptr(), dsc.data_ptr(), stream())
         return None, None, dloc, None, dmu, dsc, None, None
+
+
+# ---------------------------------------------------------------------------
+# fused decoder-block tail (include/vaesne_hip.h: vaesne_dec_tail_*)
+# ---------------------------------------------------------------------------
+class DecTailFn(torch.autograd.Function):
+    """(x, O, kvc, 16-18 weights) -> (y [, qkv_next]) for one decoder block."""
+
+    @staticmethod
+    def forward(ctx, L, p, x, O, kvc, *w):
+        _lib.require_device(x, O, kvc)
+        x, O, kvc = x.contiguous(), O.contiguous(), kvc.contiguous()
+        M = x.numel() // 32
+        Lc = kvc.shape[1]
+        w = [None if t is None else t.contiguous() for t in w]
+        nxt = w[16] is not None
+        y = torch.empty((M, 32), dtype=torch.float32, device=x.device)
+        qkv = torch.empty((M, 96), dtype=torch.float32, device=x.device) if nxt else None
+        st = rng.state(x.device) if p > 0 else None
+        cid = rng.next_call_id() if p > 0 else 0
+        lib.dec_tail_fwd(x.data_ptr(), O.data_ptr(), kvc.data_ptr(), M, L, Lc, _lib.ptr_array(w),
+                         float(p), ptr(st), cid, y.data_ptr(), ptr(qkv), stream())
+        ctx.meta = (M, L, Lc, float(p), cid, nxt, x.shape)
+        ctx.save_for_backward(x, O, kvc, y, st, *w)
+        y = y.view(x.shape)
+        if nxt:
+            return y, qkv.view(*x.shape[:-1], 96)
+        return y, None
+
+    @staticmethod
+    def backward(ctx, dy, dqkv):
+        x, O, kvc, y, st, *w = ctx.saved_tensors
+        M, L, Lc, p, cid, nxt, xshape = ctx.meta
+        dev = x.device
+        dy = torch.zeros_like(y) if dy is None else dy.contiguous()
+        if nxt:
+            dqkv = torch.zeros((M, 96), dtype=torch.float32, device=dev) if dqkv is None \
+                else dqkv.contiguous()
+        else:
+            dqkv = None
+        dx = torch.empty_like(x)
+        dO = torch.empty_like(O)
+        dkvc = torch.empty_like(kvc)
+        ng = ctx.needs_input_grad[5:]
+        gw = [torch.empty_like(t) if (t is not None and ng[i]) else None for i, t in enumerate(w)]
+        ws = _ws(lib.dec_tail_workspace(M, L, Lc), dev)
+        lib.dec_tail_bwd(x.data_ptr(), O.data_ptr(), kvc.data_ptr(), M, L, Lc, _lib.ptr_array(w),
+                         p, ptr(st), cid, y.data_ptr(), dy.data_ptr(), ptr(dqkv), dx.data_ptr(),
+                         dO.data_ptr(), dkvc.data_ptr(), _lib.ptr_array(gw), ws.data_ptr(), stream())
+        return (None, None, dx.view(xshape), dO, dkvc, *gw)

@@ -188,6 +188,50 @@ class TransformerBlock(nn.Module):
         return _ops.add_layernorm(x, f, self.layernorm3, p)
 
 
+def _fusable_decoder_block(blk):
+    E = blk.layernorm1.normalized_shape[0]
+    return (blk.context_self_attn is None and E == 32 and blk.self_attn.num_heads == 4
+            and blk.cross_attn.num_heads == 4 and blk.ffn[0].out_features == 32
+            and abs(blk.cross_attn.dropout - blk.dropout.p) < 1e-12
+            and all(ln.eps == 1e-5 for ln in (blk.layernorm1, blk.layernorm2, blk.layernorm3)))
+
+
+def decoder_stack(blocks, x, context, mask=None):
+    """`for blk in blocks: x = blk(x, context, mask=mask)` for the decoders
+    (SpectraLayers.py:61-62, PhotometricLayers.py:66-67).  With the reference's
+    decoder shape (E 32, 4 heads, ff 32, no context self-attention) each block
+    runs as: masked self-attention kernel -> ONE fused tail kernel (out_proj,
+    LN1, cross-attention over the context tokens, LN2, FFN, LN3, and the next
+    block's in_proj).  Other shapes take the per-op path (TransformerBlock)."""
+    blocks = list(blocks)
+    if not blocks or not all(_fusable_decoder_block(b) for b in blocks) or x.dim() != 3 \
+            or context.shape[1] > 8:
+        for blk in blocks:
+            x = blk(x, context, mask=mask)
+        return x
+    E = 32
+    L = x.shape[1]
+    b0 = blocks[0].self_attn
+    qkv = _ops.linear(x, b0.in_proj_weight, b0.in_proj_bias)
+    for i, blk in enumerate(blocks):
+        p_attn = blk.self_attn.dropout if blk.training else 0.0
+        p = blk.dropout.p if blk.training else 0.0
+        O = _ops.self_attention(qkv, mask, blk.self_attn.num_heads, p_attn)
+        Wc, bc = blk.cross_attn.in_proj_weight, blk.cross_attn.in_proj_bias
+        kvc = _ops.linear(context, Wc[E:], bc[E:])
+        nxt = blocks[i + 1].self_attn if i + 1 < len(blocks) else None
+        x, qkv = _ops.DecTailFn.apply(
+            L, p, x, O, kvc,
+            blk.self_attn.out_proj.weight, blk.self_attn.out_proj.bias,
+            blk.layernorm1.weight, blk.layernorm1.bias, Wc[:E], bc[:E],
+            blk.cross_attn.out_proj.weight, blk.cross_attn.out_proj.bias,
+            blk.layernorm2.weight, blk.layernorm2.bias,
+            blk.ffn[0].weight, blk.ffn[0].bias, blk.ffn[2].weight, blk.ffn[2].bias,
+            blk.layernorm3.weight, blk.layernorm3.bias,
+            None if nxt is None else nxt.in_proj_weight, None if nxt is None else nxt.in_proj_bias)
+    return x
+
+
 ############## vae use ###################
 def get_mean(d, K=100):
     """util_layers.py:313-323."""

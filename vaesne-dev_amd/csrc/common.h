@@ -106,3 +106,20 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
 __host__ __device__ __forceinline__ int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 }  // namespace vaesne
+
+namespace vaesne {
+// Deterministic column sum of a [G][F] partial buffer: out[f] = sum_g P[g][f].
+// 1024-thread block = 64 columns x 16 g-slices; slice s sums g = s, s+16, ...
+// in order, then the 16 slice sums are added in order (fixed association, so
+// results are bitwise reproducible; 16x the parallelism of a serial loop).
+// `split` routes f < split to out0 and f >= split to out1 (out1 may be null).
+__global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ P, int G, int F,
+                                                      int64_t ld,
+                                                      float* __restrict__ out0,
+                                                      float* __restrict__ out1, int split,
+                                                      int accum);
+int launch_colsum(const float* P, int G, int F, float* out0, float* out1, int split, int accum,
+                  hipStream_t s);
+// same over columns [0, F) of rows with stride ld (P[g*ld + f]) -> out[f]
+int launch_colsum_strided(const float* P, int G, int F, int64_t ld, float* out, hipStream_t s);
+}  // namespace vaesne

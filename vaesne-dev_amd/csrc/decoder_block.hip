@@ -1,0 +1,783 @@
+// Fused decoder-block tail of VAESNe (TransformerBlock.forward after the masked
+// self-attention core, util_layers.py:285-309, as used by the decoders
+// spectraTransformerDecoder SpectraLayers.py:55-63 and
+// photometricTransformerDecoder PhotometricLayers.py:66-68):
+//
+//   a1 = O Wo1^T + bo1                   self-attn out_proj
+//   x1 = LN1(x + Drop(a1))
+//   q  = x1 Wq^T + bq                    cross-attn in_proj rows [0, E)
+//   c  = Drop(softmax(q k^T / sqrt(dh))) v   over the Lc <= 8 context tokens
+//                                        (k, v = projected decoder context, unmasked)
+//   a2 = c Wo2^T + bo2;   x2 = LN2(x1 + Drop(a2))
+//   f  = W2 gelu(W1 x2 + b1) + b2;   y = LN3(x2 + Drop(f))
+//   [qkv_next = y Wn^T + bn]             the NEXT block's self-attn in_proj
+//
+// E = 32, H = 4, dh = 8, ff = 32 (every cannon script).  One launch replaces
+// ~20 op-level launches (and ~40 in the backward) and all their HBM round trips.
+//
+// Layout ("feature layout" of v_mfma_f32_32x32x2_f32): a wave owns 32 tokens;
+// lane l holds token t = l & 31 and the 16 features F(r, h) = (r&3) + 8(r>>2) + 4h,
+// h = l >> 5, r = 0..15 — exactly the rows an MFMA accumulator D[o][t] gives
+// lane l.  So y = W x is 16 MFMAs with A = W (from LDS) and B = x straight from
+// the previous accumulator: no shuffles between layers.  LayerNorm = 16 in-lane
+// adds + one cross-half swap; each head's 8 dims are regs 4hd..4hd+3 of both halves.
+//
+// Backward: recompute the forward in registers, run the chain in reverse, and
+// accumulate every weight gradient dW = sum_t g_t x_t^T with MFMAs whose
+// contraction runs over the wave's 32 tokens (operands staged in LDS rows).
+// Per-workgroup partials -> fixed-order column sum (bitwise reproducible).
+// Context (k, v) gradients are per sequence: a workgroup only ever covers
+// tokens of ONE sequence, so they accumulate in the same way.
+#include "common.h"
+
+using namespace vaesne;
+
+namespace {
+
+constexpr int E = 32, H = 4, DH = 8, LP = 33;  // LP: padded LDS row (floats)
+constexpr int NW = 4, NT = 256;               // waves / threads per workgroup
+constexpr int LCMAX = 8;
+
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int F(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ f16v mfma(float a, float b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+struct Tail {
+  // activations
+  const float* x;      // [M, 32] block input (residual stream)
+  const float* O;      // [M, 32] self-attention core output
+  const float* kvc;    // [Nseq, Lc, 64] projected context: k | v
+  int M, L, Lc;        // tokens, tokens per sequence, context tokens
+  // weights (row-major nn.Linear [out, in]) and vectors
+  const float *Wo1, *bo1, *g1, *be1, *Wq, *bq, *Wo2, *bo2, *g2, *be2;
+  const float *W1, *b1, *W2, *b2, *g3, *be3, *Wn, *bn;   // Wn/bn may be null
+  float p_drop;        // residual / attention-probability dropout
+  uint32_t thr; float inv_keep;
+  const int64_t* rng; uint32_t call_id;
+  int chunk;           // tokens per workgroup (multiple of 128)
+  // forward outputs
+  float* y;            // [M, 32]
+  float* qkv;          // [M, 96] (if Wn)
+  // backward
+  const float* dy;     // [M, 32]
+  const float* dqkv;   // [M, 96] (if Wn)
+  float* dx;           // [M, 32]
+  float* dO;           // [M, 32]
+  float* wpart;        // [G][WPART]
+  float* cpart;        // [chunks][Nseq * Lc * 64]
+};
+
+// --- LDS image of the weights --------------------------------------------
+struct __attribute__((aligned(16))) Smem {
+  float Wo1[E * LP], Wq[E * LP], Wo2[E * LP], W1[E * LP], W2[E * LP], Wn[3 * E * LP];
+  float bo1[E], bq[E], bo2[E], b1[E], b2[E], bn[3 * E];
+  float g1[E], be1[E], g2[E], be2[E], g3[E], be3[E];
+  float kv[LCMAX * 2 * E];
+};
+
+__device__ void stage_w(float* dst, const float* src, int rows) {
+  for (int i = threadIdx.x; i < rows * E; i += NT) dst[(i / E) * LP + (i % E)] = src[i];
+}
+__device__ void stage_v(float* dst, const float* src, int n) {
+  for (int i = threadIdx.x; i < n; i += NT) dst[i] = src ? src[i] : 0.f;
+}
+
+__device__ void stage_all(Smem& S, const Tail& a, bool next) {
+  stage_w(S.Wo1, a.Wo1, E); stage_w(S.Wq, a.Wq, E); stage_w(S.Wo2, a.Wo2, E);
+  stage_w(S.W1, a.W1, E); stage_w(S.W2, a.W2, E);
+  if (next) { stage_w(S.Wn, a.Wn, 3 * E); stage_v(S.bn, a.bn, 3 * E); }
+  stage_v(S.bo1, a.bo1, E); stage_v(S.bq, a.bq, E); stage_v(S.bo2, a.bo2, E);
+  stage_v(S.b1, a.b1, E); stage_v(S.b2, a.b2, E);
+  stage_v(S.g1, a.g1, E); stage_v(S.be1, a.be1, E); stage_v(S.g2, a.g2, E);
+  stage_v(S.be2, a.be2, E); stage_v(S.g3, a.g3, E); stage_v(S.be3, a.be3, E);
+}
+
+// y[r] = b[F(r,h)] + sum_k W[F(r,h)][k] x[k]      (x, y in feature layout)
+__device__ __forceinline__ void mv(const float* W, const float* b, const float (&x)[16],
+                                   float (&y)[16], int lane) {
+  const int o = lane & 31, h = lane >> 5;
+  f16v acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = b ? b[F(r, h)] : 0.f;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = mfma(W[o * LP + F(s, h)], x[s], acc);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) y[r] = acc[r];
+}
+// y (+)= W^T g   (backward data):  y[k] = sum_o W[o][k] g[o]
+__device__ __forceinline__ void mvt(const float* W, const float (&g)[16], f16v& acc, int lane) {
+  const int i = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = mfma(W[F(s, h) * LP + i], g[s], acc);
+}
+
+__device__ __forceinline__ void load_row(const float* p, int64_t row, int h, float (&v)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    float4 t = *reinterpret_cast<const float4*>(p + row * E + 8 * g + 4 * h);
+    v[4 * g] = t.x; v[4 * g + 1] = t.y; v[4 * g + 2] = t.z; v[4 * g + 3] = t.w;
+  }
+}
+__device__ __forceinline__ void store_row(float* p, int64_t row, int ld, int off, int h,
+                                          const float (&v)[16]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+    *reinterpret_cast<float4*>(p + row * ld + off + 8 * g + 4 * h) =
+        make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+}
+
+// LayerNorm over the 32 features of a token (16 in-lane + the other half-wave)
+__device__ __forceinline__ void layernorm(float (&v)[16], float& rstd, float (&xh)[16]) {
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s += v[r];
+  s += __shfl_xor(s, 32, 64);
+  const float mu = s * (1.f / E);
+  float q = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { float d = v[r] - mu; q = fmaf(d, d, q); }
+  q += __shfl_xor(q, 32, 64);
+  rstd = rsqrtf(q * (1.f / E) + 1e-5f);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) xh[r] = (v[r] - mu) * rstd;
+}
+// d(LN input) from d(LN output) g (gamma already applied by caller? no: raw)
+__device__ __forceinline__ void layernorm_bwd(const float (&g)[16], const float (&xh)[16],
+                                              const float* gamma, float rstd, int h,
+                                              float (&dv)[16]) {
+  float a = 0.f, b = 0.f;
+  float gg[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    gg[r] = g[r] * gamma[F(r, h)];
+    a += gg[r];
+    b = fmaf(gg[r], xh[r], b);
+  }
+  a += __shfl_xor(a, 32, 64);
+  b += __shfl_xor(b, 32, 64);
+  a *= (1.f / E);
+  b *= (1.f / E);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dv[r] = rstd * (gg[r] - a - xh[r] * b);
+}
+
+// residual-dropout keep scales for one site, element (row, F(r,h))
+__device__ __forceinline__ void drop_res(uint32_t key, int64_t row, int h, uint32_t thr,
+                                         float inv_keep, float (&sc)[16]) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    uint32_t bits = rand_u32(key, (uint64_t)row * E + F(r, h));
+    sc[r] = (bits & 0xffffu) >= thr ? inv_keep : 0.f;
+  }
+}
+__device__ __forceinline__ uint32_t site_key(uint32_t key, uint32_t site) {
+  return mix32(key ^ (0x632be5abu * (site + 1)));
+}
+
+__device__ __forceinline__ float gelu(float x) { return gelu_erf(x); }
+
+// cross attention of one token over the Lc context tokens (all heads):
+// p[hd][j] (pre-dropout), keep bits, c (feature layout)
+template <int LC>
+__device__ __forceinline__ void cross_fwd(const float* kv, int Lc, const float (&q)[16], int h,
+                                          uint32_t akey, int64_t row, bool drop, uint32_t thr,
+                                          float inv_keep, float (&p)[H][LC], uint32_t& keepm,
+                                          float (&c)[16]) {
+  const float scale = 0.35355339059327373f;  // 1/sqrt(8)
+  keepm = 0u;
+#pragma unroll
+  for (int hd = 0; hd < H; ++hd) {
+    float s[LC];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < LC; ++j) {
+      float part = 0.f;
+      if (j < Lc) {
+        const float* kj = kv + j * 2 * E + 8 * hd + 4 * h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) part = fmaf(q[4 * hd + i], kj[i], part);
+      }
+      part += __shfl_xor(part, 32, 64);
+      s[j] = j < Lc ? part * scale : -INFINITY;
+      mx = fmaxf(mx, s[j]);
+    }
+    float l = 0.f;
+#pragma unroll
+    for (int j = 0; j < LC; ++j) {
+      float e = j < Lc ? __expf(s[j] - mx) : 0.f;
+      s[j] = e;
+      l += e;
+    }
+    const float il = 1.f / l;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[4 * hd + i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < LC; ++j) {
+      float pj = s[j] * il;
+      p[hd][j] = pj;
+      float pd = pj;
+      if (drop && j < Lc) {
+        uint32_t bits = rand_u32(akey, ((uint64_t)row * H + hd) * LCMAX + j);
+        bool kp = (bits & 0xffffu) >= thr;
+        keepm |= (kp ? 1u : 0u) << (hd * LCMAX + j);
+        pd = kp ? pj * inv_keep : 0.f;
+      } else {
+        keepm |= 1u << (hd * LCMAX + j);
+      }
+      if (j < Lc) {
+        const float* vj = kv + j * 2 * E + E + 8 * hd + 4 * h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) c[4 * hd + i] = fmaf(pd, vj[i], c[4 * hd + i]);
+      }
+    }
+  }
+}
+
+// ============================== forward ====================================
+template <int LC, bool NEXT, bool DROP>
+__global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
+  __shared__ Smem S;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int chunks = (a.L + a.chunk - 1) / a.chunk;
+  const int seq = blockIdx.x / chunks, ch = blockIdx.x % chunks;
+  stage_all(S, a, NEXT);
+  for (int i = threadIdx.x; i < a.Lc * 2 * E; i += NT) S.kv[i] = a.kvc[(int64_t)seq * a.Lc * 2 * E + i];
+  __syncthreads();
+  const uint32_t key = DROP ? key_of(a.rng, a.call_id) : 0u;
+  const int t0 = ch * a.chunk, t1 = min(a.L, t0 + a.chunk);
+  for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32) {
+    const int tok = tt + (lane & 31);
+    const bool valid = tok < t1;
+    const int64_t row = (int64_t)seq * a.L + (valid ? tok : t1 - 1);
+    float xin[16], v[16], xh[16], rs;
+    load_row(a.O, row, h, v);
+    mv(S.Wo1, S.bo1, v, v, lane);                          // a1
+    load_row(a.x, row, h, xin);
+    if (DROP) {
+      float sc[16];
+      drop_res(site_key(key, 0), row, h, a.thr, a.inv_keep, sc);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] *= sc[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += xin[r];
+    layernorm(v, rs, xh);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xin[r] = fmaf(xh[r], S.g1[F(r, h)], S.be1[F(r, h)]);  // x1
+    float q[16], c[16], p[H][LC];
+    uint32_t km;
+    mv(S.Wq, S.bq, xin, q, lane);
+    cross_fwd<LC>(S.kv, a.Lc, q, h, site_key(key, 3), row, DROP, a.thr, a.inv_keep, p, km, c);
+    mv(S.Wo2, S.bo2, c, v, lane);                           // a2
+    if (DROP) {
+      float sc[16];
+      drop_res(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] *= sc[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += xin[r];
+    layernorm(v, rs, xh);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xin[r] = fmaf(xh[r], S.g2[F(r, h)], S.be2[F(r, h)]);  // x2
+    mv(S.W1, S.b1, xin, v, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = gelu(v[r]);
+    mv(S.W2, S.b2, v, v, lane);                             // f
+    if (DROP) {
+      float sc[16];
+      drop_res(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] *= sc[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += xin[r];
+    layernorm(v, rs, xh);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = fmaf(xh[r], S.g3[F(r, h)], S.be3[F(r, h)]);    // y
+    if (valid) store_row(a.y, row, E, 0, h, v);
+    if (NEXT) {
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        float o[16];
+        mv(S.Wn + cc * E * LP, S.bn + cc * E, v, o, lane);
+        if (valid) store_row(a.qkv, row, 3 * E, cc * E, h, o);
+      }
+    }
+  }
+}
+
+// ============================== backward ===================================
+// Phase (a), dec_tail_bwd_data: per token, recompute the forward, run the chain
+// in reverse, write dx / dO and the per-token vectors the weight gradients need
+// into a scratch buffer laid out [vector][M][32] (SoA, coalesced rows).
+// Phase (b), dec_tail_wgrad: per workgroup (one sequence chunk) contract those
+// vectors over tokens with MFMAs -> per-workgroup partials -> column sums.
+enum Vec {
+  V_DA1 = 0, V_DQ, V_DA2, V_DF1, V_DF2, V_X1, V_C, V_X2, V_GL,
+  V_DLN1, V_DLN1X, V_DLN2, V_DLN2X, V_DLN3, V_DLN3X, V_Q, V_DC, V_DS, V_PD, NVEC
+};
+
+template <int LC, bool NEXT, bool DROP>
+__global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restrict__ scr) {
+  __shared__ Smem S;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int chunks = (a.L + a.chunk - 1) / a.chunk;
+  const int seq = blockIdx.x / chunks, ch = blockIdx.x % chunks;
+  stage_all(S, a, NEXT);
+  for (int i = threadIdx.x; i < a.Lc * 2 * E; i += NT) S.kv[i] = a.kvc[(int64_t)seq * a.Lc * 2 * E + i];
+  __syncthreads();
+  const uint32_t key = DROP ? key_of(a.rng, a.call_id) : 0u;
+  const float scale = 0.35355339059327373f;
+  const int64_t MS = (int64_t)a.M * E;   // stride between scratch vectors
+  auto SV = [&](int v) { return scr + v * MS; };
+  const int t0 = ch * a.chunk, t1 = min(a.L, t0 + a.chunk);
+  for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32) {
+    const int tok = tt + (lane & 31);
+    const bool valid = tok < t1;
+    const int64_t row = (int64_t)seq * a.L + (valid ? tok : t1 - 1);
+    // ---------------- forward recompute -----------------
+    float xh1[16], xh2[16], xh3[16], q[16], c[16], f1[16];
+    float rs1, rs2, rs3, p[H][LC];
+    uint32_t km, k0 = 0xffffffffu, k1 = 0xffffffffu, k2 = 0xffffffffu;
+    {
+      float v[16], t[16];
+      load_row(a.O, row, h, t);
+      mv(S.Wo1, S.bo1, t, v, lane);
+      load_row(a.x, row, h, t);
+      if (DROP) {
+        float sc[16];
+        drop_res(site_key(key, 0), row, h, a.thr, a.inv_keep, sc);
+        k0 = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; k0 |= (sc[r] != 0.f ? 1u : 0u) << r; }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] += t[r];
+      layernorm(v, rs1, xh1);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t[r] = fmaf(xh1[r], S.g1[F(r, h)], S.be1[F(r, h)]);   // x1
+      mv(S.Wq, S.bq, t, q, lane);
+      cross_fwd<LC>(S.kv, a.Lc, q, h, site_key(key, 3), row, DROP, a.thr, a.inv_keep, p, km, c);
+      mv(S.Wo2, S.bo2, c, v, lane);
+      if (DROP) {
+        float sc[16];
+        drop_res(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
+        k1 = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; k1 |= (sc[r] != 0.f ? 1u : 0u) << r; }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] += t[r];
+      layernorm(v, rs2, xh2);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t[r] = fmaf(xh2[r], S.g2[F(r, h)], S.be2[F(r, h)]);   // x2
+      mv(S.W1, S.b1, t, f1, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = gelu(f1[r]);
+      mv(S.W2, S.b2, v, v, lane);
+      if (DROP) {
+        float sc[16];
+        drop_res(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
+        k2 = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; k2 |= (sc[r] != 0.f ? 1u : 0u) << r; }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] += t[r];
+      layernorm(v, rs3, xh3);
+    }
+    const float ik = DROP ? a.inv_keep : 1.f;
+    // ---------------- backward -----------------
+    float d[16];
+    load_row(a.dy, row, h, d);
+    if (NEXT) {
+      f16v acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = d[r];
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        float g3[16];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          float4 t = *reinterpret_cast<const float4*>(a.dqkv + row * 3 * E + cc * E + 8 * g4 + 4 * h);
+          g3[4 * g4] = t.x; g3[4 * g4 + 1] = t.y; g3[4 * g4 + 2] = t.z; g3[4 * g4 + 3] = t.w;
+        }
+        mvt(S.Wn + cc * E * LP, g3, acc, lane);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) d[r] = acc[r];
+    }
+    float t[16];
+    // LN3
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = d[r] * xh3[r];
+    if (valid) { store_row(SV(V_DLN3), row, E, 0, h, d); store_row(SV(V_DLN3X), row, E, 0, h, t); }
+    layernorm_bwd(d, xh3, S.g3, rs3, h, d);                 // dv3 (residual into x2)
+    // FFN
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = ((k2 >> r) & 1u) ? d[r] * ik : 0.f;   // df2
+    if (valid) store_row(SV(V_DF2), row, E, 0, h, t);
+    {
+      float gl[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gl[r] = gelu(f1[r]);
+      if (valid) store_row(SV(V_GL), row, E, 0, h, gl);
+      f16v acc = {};
+      mvt(S.W2, t, acc, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t[r] = acc[r] * gelu_erf_grad(f1[r]);   // df1
+    }
+    if (valid) store_row(SV(V_DF1), row, E, 0, h, t);
+    {
+      f16v acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = d[r];
+      mvt(S.W1, t, acc, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) d[r] = acc[r];                        // dx2
+    }
+    {
+      float x2[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x2[r] = fmaf(xh2[r], S.g2[F(r, h)], S.be2[F(r, h)]);
+      if (valid) store_row(SV(V_X2), row, E, 0, h, x2);
+    }
+    // LN2
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = d[r] * xh2[r];
+    if (valid) { store_row(SV(V_DLN2), row, E, 0, h, d); store_row(SV(V_DLN2X), row, E, 0, h, t); }
+    layernorm_bwd(d, xh2, S.g2, rs2, h, d);                 // dv2 (residual into x1)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = ((k1 >> r) & 1u) ? d[r] * ik : 0.f;   // da2
+    if (valid) { store_row(SV(V_DA2), row, E, 0, h, t); store_row(SV(V_C), row, E, 0, h, c); }
+    float dc[16];
+    {
+      f16v acc = {};
+      mvt(S.Wo2, t, acc, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dc[r] = acc[r];
+    }
+    if (valid) { store_row(SV(V_DC), row, E, 0, h, dc); store_row(SV(V_Q), row, E, 0, h, q); }
+    // cross attention backward (dq -> reuse t)
+    {
+      float dsv[32], pdv[32];   // j' = 4j + hd
+#pragma unroll
+      for (int k = 0; k < 32; ++k) { dsv[k] = 0.f; pdv[k] = 0.f; }
+#pragma unroll
+      for (int hd = 0; hd < H; ++hd) {
+        float dp[LC];
+        float Dsum = 0.f;
+#pragma unroll
+        for (int j = 0; j < LC; ++j) {
+          float part = 0.f;
+          if (j < a.Lc) {
+            const float* vj = S.kv + j * 2 * E + E + 8 * hd + 4 * h;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) part = fmaf(dc[4 * hd + i], vj[i], part);
+          }
+          part += __shfl_xor(part, 32, 64);
+          const bool kp = (km >> (hd * LCMAX + j)) & 1u;
+          dp[j] = (j < a.Lc && kp) ? part * ik : 0.f;
+          pdv[4 * j + hd] = (j < a.Lc && kp) ? p[hd][j] * ik : 0.f;
+          Dsum = fmaf(p[hd][j], dp[j], Dsum);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[4 * hd + i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < LC; ++j) {
+          const float ds = j < a.Lc ? p[hd][j] * (dp[j] - Dsum) * scale : 0.f;
+          dsv[4 * j + hd] = ds;
+          if (j < a.Lc) {
+            const float* kj = S.kv + j * 2 * E + 8 * hd + 4 * h;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) t[4 * hd + i] = fmaf(ds, kj[i], t[4 * hd + i]);
+          }
+        }
+      }
+      // ds / pd rows: both half-waves hold identical values; half h writes
+      // j' in [16h, 16h+16)
+      if (valid) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int k = 16 * h + 4 * g4;
+          *reinterpret_cast<float4*>(SV(V_DS) + row * E + k) =
+              make_float4(dsv[k], dsv[k + 1], dsv[k + 2], dsv[k + 3]);
+          *reinterpret_cast<float4*>(SV(V_PD) + row * E + k) =
+              make_float4(pdv[k], pdv[k + 1], pdv[k + 2], pdv[k + 3]);
+        }
+      }
+    }
+    if (valid) store_row(SV(V_DQ), row, E, 0, h, t);
+    {
+      f16v acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = d[r];
+      mvt(S.Wq, t, acc, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) d[r] = acc[r];                        // dx1
+    }
+    {
+      float x1[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) x1[r] = fmaf(xh1[r], S.g1[F(r, h)], S.be1[F(r, h)]);
+      if (valid) store_row(SV(V_X1), row, E, 0, h, x1);
+    }
+    // LN1
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = d[r] * xh1[r];
+    if (valid) { store_row(SV(V_DLN1), row, E, 0, h, d); store_row(SV(V_DLN1X), row, E, 0, h, t); }
+    layernorm_bwd(d, xh1, S.g1, rs1, h, d);                 // dv1 = dx
+    if (valid) store_row(a.dx, row, E, 0, h, d);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = ((k0 >> r) & 1u) ? d[r] * ik : 0.f;   // da1
+    if (valid) store_row(SV(V_DA1), row, E, 0, h, t);
+    {
+      f16v acc = {};
+      mvt(S.Wo1, t, acc, lane);
+      float dO[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dO[r] = acc[r];
+      if (valid) store_row(a.dO, row, E, 0, h, dO);
+    }
+  }
+}
+
+// gradient partial layout per workgroup (floats)
+constexpr int OFF_WO1 = 0, OFF_WQ = 1024, OFF_WO2 = 2048, OFF_W1 = 3072, OFF_W2 = 4096,
+              OFF_WN = 5120, OFF_BO1 = 8192, OFF_BQ = 8224, OFF_BO2 = 8256, OFF_B1 = 8288,
+              OFF_B2 = 8320, OFF_BN = 8352, OFF_G1 = 8448, OFF_BE1 = 8480, OFF_G2 = 8512,
+              OFF_BE2 = 8544, OFF_G3 = 8576, OFF_BE3 = 8608, WPART = 8640;
+
+// acc[o][k] += sum_t G[t][o] X[t][k] over the wave's 32 tokens (rows r0..r0+31,
+// rows >= rmax contribute 0); operands read straight from L2 / HBM
+__device__ __forceinline__ void wg_tile(const float* G, int ldg, const float* X, int ldx,
+                                        int64_t r0, int64_t rmax, f16v& acc, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int64_t t = r0 + 2 * s + h;
+    const bool ok = t < rmax;
+    const float g = ok ? G[t * ldg + c] : 0.f;
+    const float x = ok ? X[t * ldx + c] : 0.f;
+    acc = mfma(g, x, acc);
+  }
+}
+__device__ __forceinline__ float cs_tile(const float* G, int ldg, int64_t r0, int64_t rmax,
+                                         int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t t = r0 + 16 * h + i;
+    s += t < rmax ? G[t * ldg + c] : 0.f;
+  }
+  return s;
+}
+
+template <bool NEXT>
+__global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __restrict__ scr) {
+  __shared__ float red[NW * 2048];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int chunks = (a.L + a.chunk - 1) / a.chunk;
+  const int seq = blockIdx.x / chunks, ch = blockIdx.x % chunks;
+  const int64_t MS = (int64_t)a.M * E;
+  auto SV = [&](int v) { return scr + v * MS; };
+  f16v gWo1 = {}, gWq = {}, gWo2 = {}, gW1 = {}, gW2 = {}, gWn0 = {}, gWn1 = {}, gWn2 = {};
+  f16v gK = {}, gV = {};
+  float cs[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) cs[i] = 0.f;
+  const int t0 = ch * a.chunk, t1 = min(a.L, t0 + a.chunk);
+  const int64_t base = (int64_t)seq * a.L;
+  const int64_t rmax = base + t1;
+  for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32) {
+    const int64_t r0 = base + tt;
+    wg_tile(SV(V_DA1), E, a.O, E, r0, rmax, gWo1, lane);
+    wg_tile(SV(V_DQ), E, SV(V_X1), E, r0, rmax, gWq, lane);
+    wg_tile(SV(V_DA2), E, SV(V_C), E, r0, rmax, gWo2, lane);
+    wg_tile(SV(V_DF1), E, SV(V_X2), E, r0, rmax, gW1, lane);
+    wg_tile(SV(V_DF2), E, SV(V_GL), E, r0, rmax, gW2, lane);
+    wg_tile(SV(V_Q), E, SV(V_DS), E, r0, rmax, gK, lane);
+    wg_tile(SV(V_DC), E, SV(V_PD), E, r0, rmax, gV, lane);
+    if (NEXT) {
+      wg_tile(a.dqkv, 3 * E, a.y, E, r0, rmax, gWn0, lane);
+      wg_tile(a.dqkv + E, 3 * E, a.y, E, r0, rmax, gWn1, lane);
+      wg_tile(a.dqkv + 2 * E, 3 * E, a.y, E, r0, rmax, gWn2, lane);
+      cs[5] += cs_tile(a.dqkv, 3 * E, r0, rmax, lane);
+      cs[6] += cs_tile(a.dqkv + E, 3 * E, r0, rmax, lane);
+      cs[7] += cs_tile(a.dqkv + 2 * E, 3 * E, r0, rmax, lane);
+    }
+    cs[0] += cs_tile(SV(V_DA1), E, r0, rmax, lane);
+    cs[1] += cs_tile(SV(V_DQ), E, r0, rmax, lane);
+    cs[2] += cs_tile(SV(V_DA2), E, r0, rmax, lane);
+    cs[3] += cs_tile(SV(V_DF1), E, r0, rmax, lane);
+    cs[4] += cs_tile(SV(V_DF2), E, r0, rmax, lane);
+    cs[8] += cs_tile(SV(V_DLN1X), E, r0, rmax, lane);
+    cs[9] += cs_tile(SV(V_DLN1), E, r0, rmax, lane);
+    cs[10] += cs_tile(SV(V_DLN2X), E, r0, rmax, lane);
+    cs[11] += cs_tile(SV(V_DLN2), E, r0, rmax, lane);
+    cs[12] += cs_tile(SV(V_DLN3X), E, r0, rmax, lane);
+    cs[13] += cs_tile(SV(V_DLN3), E, r0, rmax, lane);
+  }
+  // fixed-order workgroup reduction -> one partial per workgroup
+  float* out = a.wpart + (int64_t)blockIdx.x * WPART;
+  auto reduce_mat = [&](const f16v& acc, int off) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave * 1024 + F(r, h) * 32 + (lane & 31)] = acc[r];
+    __syncthreads();
+    for (int i = threadIdx.x; i < 1024; i += NT)
+      out[off + i] = ((red[i] + red[1024 + i]) + red[2048 + i]) + red[3072 + i];
+  };
+  reduce_mat(gWo1, OFF_WO1); reduce_mat(gWq, OFF_WQ); reduce_mat(gWo2, OFF_WO2);
+  reduce_mat(gW1, OFF_W1); reduce_mat(gW2, OFF_W2);
+  if (NEXT) { reduce_mat(gWn0, OFF_WN); reduce_mat(gWn1, OFF_WN + 1024); reduce_mat(gWn2, OFF_WN + 2048); }
+  const int coff[14] = {OFF_BO1, OFF_BQ, OFF_BO2, OFF_B1, OFF_B2, OFF_BN, OFF_BN + 32, OFF_BN + 64,
+                        OFF_G1, OFF_BE1, OFF_G2, OFF_BE2, OFF_G3, OFF_BE3};
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 14; ++i) red[wave * 1024 + i * 64 + lane] = cs[i];
+  __syncthreads();
+  for (int k = threadIdx.x; k < 14 * 32; k += NT) {
+    const int i = k / 32, c = k % 32;
+    if (!NEXT && i >= 5 && i <= 7) continue;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[w * 1024 + i * 64 + c] + red[w * 1024 + i * 64 + 32 + c];
+    out[coff[i] + c] = s;
+  }
+  // context grads: gK[f = F(r,h)][j' = lane&31], valid where (j' & 3) == f >> 3
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    red[wave * 2048 + F(r, h) * 32 + (lane & 31)] = gK[r];
+    red[wave * 2048 + 1024 + F(r, h) * 32 + (lane & 31)] = gV[r];
+  }
+  __syncthreads();
+  const int nseq = a.M / a.L;
+  float* cp = a.cpart + ((int64_t)ch * nseq + seq) * a.Lc * 2 * E;
+  for (int i = threadIdx.x; i < a.Lc * 2 * E; i += NT) {
+    const int j = i / (2 * E), ff = i % (2 * E);
+    const int isv = ff >= E, f = ff % E;
+    const int idx = (isv ? 1024 : 0) + f * 32 + 4 * j + (f >> 3);
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[w * 2048 + idx];
+    cp[i] = s;
+  }
+}
+
+template <int LC, bool NEXT, bool DROP>
+int launch_fwd(const Tail& a, int grid, float*, hipStream_t s) {
+  hipLaunchKernelGGL((dec_tail_fwd<LC, NEXT, DROP>), dim3(grid), dim3(NT), 0, s, a);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+template <int LC, bool NEXT, bool DROP>
+int launch_bwd(const Tail& a, int grid, float* scr, hipStream_t s) {
+  hipLaunchKernelGGL((dec_tail_bwd_data<LC, NEXT, DROP>), dim3(grid), dim3(NT), 0, s, a, scr);
+  VAESNE_CHECK_LAUNCH();
+  hipLaunchKernelGGL((dec_tail_wgrad<NEXT>), dim3(grid), dim3(NT), 0, s, a, (const float*)scr);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+template <bool FWD>
+int dispatch(const Tail& a, int grid, float* scr, hipStream_t s) {
+  const bool next = a.Wn != nullptr, drop = a.p_drop > 0.f;
+#define VAESNE_TAIL_CASE(LCV)                                                                   \
+  if (next && drop) return FWD ? launch_fwd<LCV, true, true>(a, grid, scr, s) : launch_bwd<LCV, true, true>(a, grid, scr, s); \
+  if (next) return FWD ? launch_fwd<LCV, true, false>(a, grid, scr, s) : launch_bwd<LCV, true, false>(a, grid, scr, s);       \
+  if (drop) return FWD ? launch_fwd<LCV, false, true>(a, grid, scr, s) : launch_bwd<LCV, false, true>(a, grid, scr, s);       \
+  return FWD ? launch_fwd<LCV, false, false>(a, grid, scr, s) : launch_bwd<LCV, false, false>(a, grid, scr, s);
+  if (a.Lc <= 4) { VAESNE_TAIL_CASE(4) }
+  VAESNE_TAIL_CASE(8)
+#undef VAESNE_TAIL_CASE
+}
+
+Tail make(const float* x, const float* O, const float* kvc, int M, int L, int Lc,
+          const float* const* w, float p_drop, const int64_t* rng, uint32_t call_id) {
+  Tail a{};
+  a.x = x; a.O = O; a.kvc = kvc; a.M = M; a.L = L; a.Lc = Lc;
+  a.Wo1 = w[0]; a.bo1 = w[1]; a.g1 = w[2]; a.be1 = w[3]; a.Wq = w[4]; a.bq = w[5];
+  a.Wo2 = w[6]; a.bo2 = w[7]; a.g2 = w[8]; a.be2 = w[9]; a.W1 = w[10]; a.b1 = w[11];
+  a.W2 = w[12]; a.b2 = w[13]; a.g3 = w[14]; a.be3 = w[15]; a.Wn = w[16]; a.bn = w[17];
+  a.p_drop = p_drop; a.thr = drop_thr16(p_drop);
+  a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  a.rng = rng; a.call_id = call_id;
+  a.chunk = L <= 256 ? ((L + 127) / 128) * 128 : 256;
+  return a;
+}
+
+bool shapes_ok(int M, int L, int Lc) {
+  return M > 0 && L > 0 && M % L == 0 && Lc >= 1 && Lc <= LCMAX;
+}
+
+}  // namespace
+
+VAESNE_API int64_t vaesne_dec_tail_workspace(int M, int L, int Lc) {
+  if (!shapes_ok(M, L, Lc)) return 0;
+  const int chunk = L <= 256 ? ((L + 127) / 128) * 128 : 256;
+  const int chunks = (L + chunk - 1) / chunk;
+  const int64_t G = (int64_t)(M / L) * chunks;
+  return (G * WPART + (int64_t)chunks * (M / L) * Lc * 2 * E + (int64_t)NVEC * M * E) *
+         (int64_t)sizeof(float);
+}
+
+VAESNE_API int vaesne_dec_tail_fwd(const float* x, const float* O, const float* kvc, int M, int L,
+                                   int Lc, const float* const* w, float p_drop,
+                                   const int64_t* rng, uint32_t call_id, float* y, float* qkv,
+                                   void* stream) {
+  if (!shapes_ok(M, L, Lc)) return (int)hipErrorInvalidValue;
+  Tail a = make(x, O, kvc, M, L, Lc, w, p_drop, rng, call_id);
+  a.y = y; a.qkv = qkv;
+  if (a.Wn && !qkv) return (int)hipErrorInvalidValue;
+  const int grid = (M / L) * ((L + a.chunk - 1) / a.chunk);
+  return dispatch<true>(a, grid, nullptr, (hipStream_t)stream);
+}
+
+// grads: [Wo1, bo1, g1, be1, Wq, bq, Wo2, bo2, g2, be2, W1, b1, W2, b2, g3, be3, Wn, bn]
+// (same order as w; the Wn/bn entries only when fused), dkvc [Nseq, Lc, 64].
+VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* kvc, int M, int L,
+                                   int Lc, const float* const* w, float p_drop,
+                                   const int64_t* rng, uint32_t call_id, const float* y,
+                                   const float* dy, const float* dqkv, float* dx, float* dO,
+                                   float* dkvc,
+                                   float* const* grads, float* workspace, void* stream) {
+  if (!shapes_ok(M, L, Lc)) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  Tail a = make(x, O, kvc, M, L, Lc, w, p_drop, rng, call_id);
+  a.dy = dy; a.dqkv = dqkv; a.dx = dx; a.dO = dO;
+  if (a.Wn && !dqkv) return (int)hipErrorInvalidValue;
+  const int chunks = (L + a.chunk - 1) / a.chunk;
+  const int grid = (M / L) * chunks;
+  a.y = const_cast<float*>(y);
+  a.wpart = workspace;
+  a.cpart = workspace + (int64_t)grid * WPART;
+  float* scr = a.cpart + (int64_t)chunks * (M / L) * Lc * 2 * E;
+  int rc = dispatch<false>(a, grid, scr, s);
+  if (rc) return rc;
+  // fixed-order sums of the per-workgroup partials
+  struct Seg { int off, n, gi; };
+  const Seg segs[] = {{OFF_WO1, 1024, 0}, {OFF_BO1, 32, 1}, {OFF_G1, 32, 2}, {OFF_BE1, 32, 3},
+                      {OFF_WQ, 1024, 4}, {OFF_BQ, 32, 5}, {OFF_WO2, 1024, 6}, {OFF_BO2, 32, 7},
+                      {OFF_G2, 32, 8}, {OFF_BE2, 32, 9}, {OFF_W1, 1024, 10}, {OFF_B1, 32, 11},
+                      {OFF_W2, 1024, 12}, {OFF_B2, 32, 13}, {OFF_G3, 32, 14}, {OFF_BE3, 32, 15},
+                      {OFF_WN, 3072, 16}, {OFF_BN, 96, 17}};
+  // one column sum over the whole [grid][WPART] buffer into a staging area is
+  // simplest: colsum writes directly to each gradient tensor segment.
+  for (const Seg& sg : segs) {
+    if (sg.gi >= 16 && !a.Wn) continue;
+    if (!grads[sg.gi]) continue;
+    rc = launch_colsum_strided(workspace + sg.off, grid, sg.n, WPART, grads[sg.gi], s);
+    if (rc) return rc;
+  }
+  // context grads: sum over chunks -> dkvc [Nseq * Lc * 64]
+  return launch_colsum(a.cpart, chunks, (M / L) * Lc * 2 * E, dkvc, nullptr,
+                       (M / L) * Lc * 2 * E, 0, s);
+}

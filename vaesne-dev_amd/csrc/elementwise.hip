@@ -88,15 +88,6 @@ __global__ __launch_bounds__(NT) void embed_bwd_kernel(const int64_t* __restrict
   }
 }
 
-__global__ void reduce_rows_kernel(const float* __restrict__ partial, int G, int F,
-                                   float* __restrict__ out, int accum) {
-  int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= F) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += partial[(int64_t)g * F + f];
-  out[f] = accum ? out[f] + s : s;
-}
-
 // bottleneck [B, 2*Lz, Dz] -> mu [B, Lz*Dz], scale [B, Lz*Dz]
 __global__ void latent_head_fwd_kernel(const float* __restrict__ bott, int B, int n,
                                        float* __restrict__ mu, float* __restrict__ scale) {
@@ -275,19 +266,13 @@ VAESNE_API int vaesne_embed_bwd(const int64_t* idx, int64_t period, int64_t rows
     hipLaunchKernelGGL(embed_bwd_kernel<16>, dim3(G), dim3(NT), 0, s, idx, period, rows, dout,
                        lddo, E, nb, workspace);
   VAESNE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((nb * E + 255) / 256), dim3(256), 0, s, workspace, G,
-                     nb * E, dtable, accum);
-  VAESNE_CHECK_LAUNCH();
-  return 0;
+  return launch_colsum(workspace, G, nb * E, dtable, nullptr, nb * E, accum, s);
 }
 
 // out[f] (+)= sum_g in[g*F + f]  (gradient of a broadcast / repeat over G)
 VAESNE_API int vaesne_sum_leading(const float* in, int G, int F, float* out, int accum,
                                   void* stream) {
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3((F + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     in, G, F, out, accum);
-  VAESNE_CHECK_LAUNCH();
-  return 0;
+  return launch_colsum(in, G, F, out, nullptr, F, accum, (hipStream_t)stream);
 }
 
 VAESNE_API int vaesne_latent_head_fwd(const float* bott, int B, int n, float* mu, float* scale,

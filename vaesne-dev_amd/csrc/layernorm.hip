@@ -168,20 +168,6 @@ __global__ __launch_bounds__(NT) void add_ln_bwd_kernel(
   }
 }
 
-__global__ void reduce_partials(const float* __restrict__ partial, int G, int F,
-                                float* __restrict__ out0, float* __restrict__ out1, int split,
-                                int accum) {
-  int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= F) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += partial[(int64_t)g * F + f];
-  if (f < split) {
-    if (out0) out0[f] = accum ? out0[f] + s : s;
-  } else {
-    if (out1) out1[f - split] = accum ? out1[f - split] + s : s;
-  }
-}
-
 int ln_grid(int64_t M) {
   int64_t b = (M + NT - 1) / NT;
   return (int)(b < 1024 ? (b < 1 ? 1 : b) : 1024);
@@ -237,10 +223,7 @@ VAESNE_API int vaesne_add_ln_bwd(const float* dy, int64_t lddy, const float* x, 
     return (int)hipErrorInvalidValue;
   }
   VAESNE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(reduce_partials, dim3(1), dim3(2 * E), 0, s, workspace, G, 2 * E, dgamma,
-                     dbeta, E, accum_param);
-  VAESNE_CHECK_LAUNCH();
-  return 0;
+  return launch_colsum(workspace, G, 2 * E, dgamma, dbeta, E, accum_param, s);
 }
 
 // generic fixed-order partial-sum reduction (used by the host for other
@@ -248,9 +231,5 @@ VAESNE_API int vaesne_add_ln_bwd(const float* dy, int64_t lddy, const float* x, 
 // out1[f - split] likewise for f >= split.
 VAESNE_API int vaesne_reduce_partials(const float* partial, int G, int F, float* out0, float* out1,
                                       int split, int accum, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(reduce_partials, dim3((F + 255) / 256), dim3(256), 0, s, partial, G, F, out0,
-                     out1, split, accum);
-  VAESNE_CHECK_LAUNCH();
-  return 0;
+  return launch_colsum(partial, G, F, out0, out1, split, accum, (hipStream_t)stream);
 }

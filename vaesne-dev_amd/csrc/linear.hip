@@ -230,28 +230,12 @@ __global__ __launch_bounds__(NT) void linear_wgrad_kernel(WgtArgs p) {
       for (int e = 0; e < E; ++e) acc[e] = fmaf(Dz[rr * p.O + fo[e]], Xs[rr * I1 + fi[e]], acc[e]);
     }
   }
+  // partial layout [G][O*I (dW) | O (db)] so one column-sum splits at O*I
   float* out = p.partial + (int64_t)blockIdx.x * F;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     int f = threadIdx.x + NT * e;
-    if (f < F) out[f] = acc[e];
-  }
-}
-
-// sum partial[g][f] over g (fixed order) -> dW (f < O*I as [O][I]) and db
-__global__ void linear_wgrad_reduce(const float* __restrict__ partial, int G, int O, int I,
-                                    float* __restrict__ dW, float* __restrict__ db, int accum) {
-  const int I1 = I + 1;
-  const int F = O * I1;
-  int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= F) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += partial[(int64_t)g * F + f];
-  int o = f / I1, i = f - o * I1;
-  if (i < I) {
-    if (dW) dW[o * I + i] = accum ? dW[o * I + i] + s : s;
-  } else {
-    if (db) db[o] = accum ? db[o] + s : s;
+    if (f < F) out[fi[e] < p.I ? fo[e] * p.I + fi[e] : p.O * p.I + fo[e]] = acc[e];
   }
 }
 
@@ -324,8 +308,5 @@ VAESNE_API int vaesne_linear_bwd_weight(const float* dy, int64_t lddy, const flo
       return (int)hipErrorInvalidValue;
     VAESNE_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(linear_wgrad_reduce, dim3((F + 255) / 256), dim3(256), 0, s, workspace, G, O,
-                     I, dW, db, accum);
-  VAESNE_CHECK_LAUNCH();
-  return 0;
+  return launch_colsum(workspace, G, F, dW, db, O * I, accum, s);
 }
