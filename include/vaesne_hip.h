@@ -75,21 +75,23 @@ int vaesne_reduce_partials(const float* partial, int G, int F, float* out0, floa
  * (self, key_padding_mask), :297 (context self), :301 (cross); arithmetic of
  * torch/nn/functional.py:6559-6594: q/sqrt(dh), -inf key mask, softmax,
  * dropout(p) on the probabilities, P v.  Flash-style: scores never stored.
+ * The key_padding_mask enters as an additive key bias kbias [B, Lk] (0 or -inf,
+ * built once per mask by vaesne_mask_bias; null = no mask).
  * lse [B,H,Lq] (log2 domain) is saved for the backward.  dh in {8, 16}. */
+int vaesne_mask_bias(const uint8_t* mask, int64_t n, float* out, void* stream);
 int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
                     int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls,
-                    const uint8_t* kpm, int64_t m_bs, float* o, int64_t o_bs, int64_t o_ls,
+                    const float* kbias, int64_t kb_bs, float* o, int64_t o_bs, int64_t o_ls,
                     float* lse, int B, int H, int Lq, int Lk, int dh, float p_drop,
                     const int64_t* rng_state, uint32_t call_id, void* stream);
-int64_t vaesne_attn_bwd_workspace(int B, int H, int Lq);
 int vaesne_attn_bwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
                     int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls,
-                    const uint8_t* kpm, int64_t m_bs, const float* o, int64_t o_bs,
+                    const float* kbias, int64_t kb_bs, const float* o, int64_t o_bs,
                     int64_t o_ls, const float* lse, const float* dout, int64_t do_bs,
                     int64_t do_ls, float* dq, int64_t dq_bs, int64_t dq_ls, float* dk,
                     int64_t dk_bs, int64_t dk_ls, float* dv, int64_t dv_bs, int64_t dv_ls, int B,
                     int H, int Lq, int Lk, int dh, float p_drop, const int64_t* rng_state,
-                    uint32_t call_id, float* workspace, void* stream);
+                    uint32_t call_id, void* stream);
 
 /* ---- fused decoder-block tail --------------------------------------------------
  * Everything of a decoder TransformerBlock after its masked self-attention core
@@ -101,9 +103,10 @@ int vaesne_attn_bwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, 
  * w: HOST array of 18 device pointers {Wo1, bo1, g1, be1, Wq, bq, Wo2, bo2, g2,
  * be2, W1, b1, W2, b2, g3, be3, Wn, bn} (Wq/bq = cross in_proj rows [0, 32);
  * Wn/bn = next self in_proj [96, 32] / [96], null when not fused; qkv [M, 96]).
- * bwd: grads = HOST array of 18 device pointers (same order, null = skip);
- * y = the forward output; dqkv required iff Wn; workspace sized by
- * vaesne_dec_tail_workspace. */
+ * bwd: gflat = ONE device buffer receiving every parameter gradient of the
+ * block at the offsets vaesne_dec_tail_grad_layout() reports (same order as w;
+ * returns the buffer length, 8640 floats); y = the forward output; dqkv
+ * required iff Wn; workspace sized by vaesne_dec_tail_workspace. */
 int64_t vaesne_dec_tail_workspace(int M, int L, int Lc);
 int vaesne_dec_tail_fwd(const float* x, const float* O, const float* kvc, int M, int L, int Lc,
                         const float* const* w, float p_drop, const int64_t* rng_state,
@@ -111,8 +114,9 @@ int vaesne_dec_tail_fwd(const float* x, const float* O, const float* kvc, int M,
 int vaesne_dec_tail_bwd(const float* x, const float* O, const float* kvc, int M, int L, int Lc,
                         const float* const* w, float p_drop, const int64_t* rng_state,
                         uint32_t call_id, const float* y, const float* dy, const float* dqkv,
-                        float* dx, float* dO, float* dkvc, float* const* grads,
-                        float* workspace, void* stream);
+                        float* dx, float* dO, float* dkvc, float* gflat, float* workspace,
+                        void* stream);
+int vaesne_dec_tail_grad_layout(int* offsets);
 
 /* ---- embeddings ------------------------------------------------------------
  * [sin(x*div) | cos(x*div)]: util_layers.py:125-129 (plain, 16 freqs) and

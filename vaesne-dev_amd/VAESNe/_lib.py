@@ -36,16 +36,17 @@ SIGNATURES = {
     "vaesne_add_ln_bwd": (I32, [P, I64, P, I64, P, I64, I64, I32, P, P, P, F32, P, U32, P, I64,
                                 I32, P, I64, I32, P, P, I32, P, P]),
     "vaesne_reduce_partials": (I32, [P, I32, I32, P, P, I32, I32, P]),
+    "vaesne_mask_bias": (I32, [P, I64, P, P]),
     "vaesne_attn_fwd": (I32, [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, P, I64, I64, P, I32,
                               I32, I32, I32, I32, F32, P, U32, P]),
-    "vaesne_attn_bwd_workspace": (I64, [I32, I32, I32]),
     "vaesne_attn_bwd": (I32, [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, P, I64, I64, P, P,
                               I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I32, I32, I32, I32,
-                              I32, F32, P, U32, P, P]),
+                              I32, F32, P, U32, P]),
     "vaesne_dec_tail_workspace": (I64, [I32, I32, I32]),
     "vaesne_dec_tail_fwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P]),
-    "vaesne_dec_tail_bwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P, P, P, P, PP,
+    "vaesne_dec_tail_bwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P, P, P, P, P,
                                   P, P]),
+    "vaesne_dec_tail_grad_layout": (I32, [C.POINTER(I32)]),
     "vaesne_sincos": (I32, [P, I64, I64, P, I32, P, I64, P]),
     "vaesne_embed_fwd": (I32, [P, I64, I64, P, I32, P, I64, P, I64, P]),
     "vaesne_embed_bwd_workspace": (I64, [I64, I32, I32]),
@@ -69,6 +70,9 @@ SIGNATURES = {
     "vaesne_step_advance": (I32, [P, P, P]),
     "vaesne_pack": (I32, [PP, C.POINTER(I64), C.POINTER(I64), I32, P, I32, P]),
 }
+
+# int-returning entry points whose result is a value, not a hipError_t
+VALUE_RETURNING = {"vaesne_dec_tail_grad_layout"}
 
 _lib = None
 
@@ -100,7 +104,7 @@ class _Fn:
 
         def call(*args):
             rc = fn(*args)
-            if fn.restype is I32 and rc != 0:
+            if fn.restype is I32 and rc != 0 and ("vaesne_" + name) not in VALUE_RETURNING:
                 raise RuntimeError(f"vaesne_{name} failed: hipError {rc}")
             return rc
         return call

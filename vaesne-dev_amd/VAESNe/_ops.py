@@ -161,48 +161,67 @@ def add_layernorm(x, res, ln, p):
 # ---------------------------------------------------------------------------
 # attention core
 # ---------------------------------------------------------------------------
-def _attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, mask, B, H, Lq, Lk, dh, p, dev):
+def key_bias(mask):
+    """key_padding_mask (bool, True = ignore) -> additive key bias (0 / -inf),
+    the attention kernels' mask format.  Build once, reuse across layers."""
+    if mask is None:
+        return None
+    m = _mask_u8(mask)
+    out = torch.empty(m.shape, dtype=torch.float32, device=m.device)
+    lib.mask_bias(m.data_ptr(), m.numel(), out.data_ptr(), stream())
+    return out
+
+
+def _bias_of(mask, kbias):
+    if kbias is not None:
+        return kbias.contiguous()
+    if mask is None:
+        return None
+    if mask.dtype == torch.float32:
+        return mask.contiguous()
+    return key_bias(mask)
+
+
+def _attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, kbias, B, H, Lq, Lk, dh, p, dev):
     E = H * dh
     o = torch.empty((B, Lq, E), dtype=torch.float32, device=dev)
     lse = torch.empty((B, H, Lq), dtype=torch.float32, device=dev)
     st = rng.state(dev) if p > 0 else None
     cid = rng.next_call_id() if p > 0 else 0
-    lib.attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, ptr(mask), Lk, o.data_ptr(), Lq * E, E,
+    lib.attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, ptr(kbias), Lk, o.data_ptr(), Lq * E, E,
                  lse.data_ptr(), B, H, Lq, Lk, dh, float(p), ptr(st), cid, stream())
     return o, lse, st, cid
 
 
 class SelfAttnFn(torch.autograd.Function):
-    """Packed qkv [B, L, 3E] -> o [B, L, E] (self-attention, key padding mask)."""
+    """Packed qkv [B, L, 3E] -> o [B, L, E] (self-attention, additive key bias)."""
 
     @staticmethod
-    def forward(ctx, qkv, mask, H, p):
+    def forward(ctx, qkv, kbias, H, p):
         _lib.require_device(qkv)
         qkv = qkv.contiguous()
         B, L, E3 = qkv.shape
         E = E3 // 3
         dh = E // H
-        m = _mask_u8(mask)
         base = qkv.data_ptr()
         o, lse, st, cid = _attn_fwd(base, L * E3, E3, base + 4 * E, L * E3, E3, base + 8 * E,
-                                    L * E3, E3, m, B, H, L, L, dh, p, qkv.device)
+                                    L * E3, E3, kbias, B, H, L, L, dh, p, qkv.device)
         ctx.dims = (B, L, E, H, dh, float(p), cid)
-        ctx.save_for_backward(qkv, m, o, lse, st)
+        ctx.save_for_backward(qkv, kbias, o, lse, st)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qkv, m, o, lse, st = ctx.saved_tensors
+        qkv, kbias, o, lse, st = ctx.saved_tensors
         B, L, E, H, dh, p, cid = ctx.dims
         do = do.contiguous()
         E3 = 3 * E
         dqkv = torch.empty_like(qkv)
-        ws = _ws(lib.attn_bwd_workspace(B, H, L), do.device)
         b, d = qkv.data_ptr(), dqkv.data_ptr()
-        lib.attn_bwd(b, L * E3, E3, b + 4 * E, L * E3, E3, b + 8 * E, L * E3, E3, ptr(m), L,
+        lib.attn_bwd(b, L * E3, E3, b + 4 * E, L * E3, E3, b + 8 * E, L * E3, E3, ptr(kbias), L,
                      o.data_ptr(), L * E, E, lse.data_ptr(), do.data_ptr(), L * E, E,
                      d, L * E3, E3, d + 4 * E, L * E3, E3, d + 8 * E, L * E3, E3,
-                     B, H, L, L, dh, p, ptr(st), cid, ws.data_ptr(), stream())
+                     B, H, L, L, dh, p, ptr(st), cid, stream())
         return dqkv, None, None, None
 
 
@@ -210,44 +229,42 @@ class CrossAttnFn(torch.autograd.Function):
     """q [B, Lq, E], packed kv [B, Lk, 2E] -> o [B, Lq, E]."""
 
     @staticmethod
-    def forward(ctx, q, kv, mask, H, p):
+    def forward(ctx, q, kv, kbias, H, p):
         _lib.require_device(q, kv)
         q = q.contiguous()
         kv = kv.contiguous()
         B, Lq, E = q.shape
         Lk = kv.shape[1]
         dh = E // H
-        m = _mask_u8(mask)
         kb = kv.data_ptr()
         o, lse, st, cid = _attn_fwd(q.data_ptr(), Lq * E, E, kb, Lk * 2 * E, 2 * E, kb + 4 * E,
-                                    Lk * 2 * E, 2 * E, m, B, H, Lq, Lk, dh, p, q.device)
+                                    Lk * 2 * E, 2 * E, kbias, B, H, Lq, Lk, dh, p, q.device)
         ctx.dims = (B, Lq, Lk, E, H, dh, float(p), cid)
-        ctx.save_for_backward(q, kv, m, o, lse, st)
+        ctx.save_for_backward(q, kv, kbias, o, lse, st)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, kv, m, o, lse, st = ctx.saved_tensors
+        q, kv, kbias, o, lse, st = ctx.saved_tensors
         B, Lq, Lk, E, H, dh, p, cid = ctx.dims
         do = do.contiguous()
         dq = torch.empty_like(q)
         dkv = torch.empty_like(kv)
-        ws = _ws(lib.attn_bwd_workspace(B, H, Lq), do.device)
         kb, dkb = kv.data_ptr(), dkv.data_ptr()
         lib.attn_bwd(q.data_ptr(), Lq * E, E, kb, Lk * 2 * E, 2 * E, kb + 4 * E, Lk * 2 * E,
-                     2 * E, ptr(m), Lk, o.data_ptr(), Lq * E, E, lse.data_ptr(), do.data_ptr(),
+                     2 * E, ptr(kbias), Lk, o.data_ptr(), Lq * E, E, lse.data_ptr(), do.data_ptr(),
                      Lq * E, E, dq.data_ptr(), Lq * E, E, dkb, Lk * 2 * E, 2 * E, dkb + 4 * E,
-                     Lk * 2 * E, 2 * E, B, H, Lq, Lk, dh, p, ptr(st), cid, ws.data_ptr(),
-                     stream())
+                     Lk * 2 * E, 2 * E, B, H, Lq, Lk, dh, p, ptr(st), cid, stream())
         return dq, dkv, None, None, None
 
 
-def self_attention(qkv, mask, num_heads, p):
-    return SelfAttnFn.apply(qkv, mask, num_heads, float(p))
+def self_attention(qkv, mask, num_heads, p, kbias=None):
+    """mask: bool key_padding_mask (True = ignore) or None; kbias: a prebuilt key_bias."""
+    return SelfAttnFn.apply(qkv, _bias_of(mask, kbias), num_heads, float(p))
 
 
-def cross_attention(q, kv, mask, num_heads, p):
-    return CrossAttnFn.apply(q, kv, mask, num_heads, float(p))
+def cross_attention(q, kv, mask, num_heads, p, kbias=None):
+    return CrossAttnFn.apply(q, kv, _bias_of(mask, kbias), num_heads, float(p))
 
 
 # ---------------------------------------------------------------------------
@@ -508,6 +525,18 @@ class ElboFn(torch.autograd.Function):
 # ---------------------------------------------------------------------------
 # fused decoder-block tail (include/vaesne_hip.h: vaesne_dec_tail_*)
 # ---------------------------------------------------------------------------
+_TAIL_LAYOUT = None
+
+
+def _tail_layout():
+    global _TAIL_LAYOUT
+    if _TAIL_LAYOUT is None:
+        arr = (C.c_int * 18)()
+        total = lib.dec_tail_grad_layout(arr)
+        _TAIL_LAYOUT = (list(arr), total)
+    return _TAIL_LAYOUT
+
+
 class DecTailFn(torch.autograd.Function):
     """(x, O, kvc, 16-18 weights) -> (y [, qkv_next]) for one decoder block."""
 
@@ -546,10 +575,13 @@ class DecTailFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         dO = torch.empty_like(O)
         dkvc = torch.empty_like(kvc)
-        ng = ctx.needs_input_grad[5:]
-        gw = [torch.empty_like(t) if (t is not None and ng[i]) else None for i, t in enumerate(w)]
+        offs, total = _tail_layout()
+        gflat = torch.empty(total, dtype=torch.float32, device=dev)
         ws = _ws(lib.dec_tail_workspace(M, L, Lc), dev)
         lib.dec_tail_bwd(x.data_ptr(), O.data_ptr(), kvc.data_ptr(), M, L, Lc, _lib.ptr_array(w),
                          p, ptr(st), cid, y.data_ptr(), dy.data_ptr(), ptr(dqkv), dx.data_ptr(),
-                         dO.data_ptr(), dkvc.data_ptr(), _lib.ptr_array(gw), ws.data_ptr(), stream())
+                         dO.data_ptr(), dkvc.data_ptr(), gflat.data_ptr(), ws.data_ptr(), stream())
+        ng = ctx.needs_input_grad[5:]
+        gw = [gflat[o:o + t.numel()].view_as(t) if (t is not None and ng[i]) else None
+              for i, (t, o) in enumerate(zip(w, offs))]
         return (None, None, dx.view(xshape), dO, dkvc, *gw)

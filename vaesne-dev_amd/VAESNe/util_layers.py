@@ -213,10 +213,11 @@ def decoder_stack(blocks, x, context, mask=None):
     L = x.shape[1]
     b0 = blocks[0].self_attn
     qkv = _ops.linear(x, b0.in_proj_weight, b0.in_proj_bias)
+    kbias = _ops.key_bias(mask)          # one mask conversion for all layers
     for i, blk in enumerate(blocks):
         p_attn = blk.self_attn.dropout if blk.training else 0.0
         p = blk.dropout.p if blk.training else 0.0
-        O = _ops.self_attention(qkv, mask, blk.self_attn.num_heads, p_attn)
+        O = _ops.self_attention(qkv, None, blk.self_attn.num_heads, p_attn, kbias=kbias)
         Wc, bc = blk.cross_attn.in_proj_weight, blk.cross_attn.in_proj_bias
         kvc = _ops.linear(context, Wc[E:], bc[E:])
         nxt = blocks[i + 1].self_attn if i + 1 < len(blocks) else None

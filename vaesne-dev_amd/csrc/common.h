@@ -82,7 +82,15 @@ __device__ __forceinline__ uint32_t attn_row_key(uint32_t key, uint32_t row) {
   return mix32(key ^ (row * 0x9e3779b1u));
 }
 __device__ __forceinline__ uint32_t attn_pair_bits(uint32_t row_key, uint32_t kp) {
-  return mix32(row_key ^ (kp * 0x85ebca6bu + 0xc2b2ae35u));
+  // row_key is already a full-avalanche hash of the row, so one
+  // xorshift-multiply round over the key-pair Weyl sequence suffices
+  // (keep rate, neighbour-key/row correlations and 16-bit uniformity checked
+  // against the 2-round mixer; one v_mul_lo_u32 instead of three).
+  uint32_t x = row_key ^ (kp * 0x9e3779b9u);
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  return x;
 }
 
 // keep threshold: an element is DROPPED when its 16-bit value < thr16,

@@ -579,96 +579,94 @@ __device__ __forceinline__ float cs_tile(const float* G, int ldg, int64_t r0, in
   return s;
 }
 
-template <bool NEXT>
+// one workgroup per (job, sequence chunk); job = which weight matrix (or the
+// LayerNorm vectors, or the context k / v gradients).  A single accumulator per
+// wave keeps occupancy high so the streamed operand loads overlap.
+enum Job { J_WO1 = 0, J_WQ, J_WO2, J_W1, J_W2, J_WN0, J_WN1, J_WN2, J_K, J_V, J_LN, NJOB };
+
 __global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __restrict__ scr) {
-  __shared__ float red[NW * 2048];
+  __shared__ float red[NW * 1024];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int job = blockIdx.y;
+  const bool next = a.Wn != nullptr;
+  if (!next && job >= J_WN0 && job <= J_WN2) return;
   const int chunks = (a.L + a.chunk - 1) / a.chunk;
   const int seq = blockIdx.x / chunks, ch = blockIdx.x % chunks;
   const int64_t MS = (int64_t)a.M * E;
-  auto SV = [&](int v) { return scr + v * MS; };
-  f16v gWo1 = {}, gWq = {}, gWo2 = {}, gW1 = {}, gW2 = {}, gWn0 = {}, gWn1 = {}, gWn2 = {};
-  f16v gK = {}, gV = {};
-  float cs[14];
-#pragma unroll
-  for (int i = 0; i < 14; ++i) cs[i] = 0.f;
-  const int t0 = ch * a.chunk, t1 = min(a.L, t0 + a.chunk);
-  const int64_t base = (int64_t)seq * a.L;
-  const int64_t rmax = base + t1;
-  for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32) {
-    const int64_t r0 = base + tt;
-    wg_tile(SV(V_DA1), E, a.O, E, r0, rmax, gWo1, lane);
-    wg_tile(SV(V_DQ), E, SV(V_X1), E, r0, rmax, gWq, lane);
-    wg_tile(SV(V_DA2), E, SV(V_C), E, r0, rmax, gWo2, lane);
-    wg_tile(SV(V_DF1), E, SV(V_X2), E, r0, rmax, gW1, lane);
-    wg_tile(SV(V_DF2), E, SV(V_GL), E, r0, rmax, gW2, lane);
-    wg_tile(SV(V_Q), E, SV(V_DS), E, r0, rmax, gK, lane);
-    wg_tile(SV(V_DC), E, SV(V_PD), E, r0, rmax, gV, lane);
-    if (NEXT) {
-      wg_tile(a.dqkv, 3 * E, a.y, E, r0, rmax, gWn0, lane);
-      wg_tile(a.dqkv + E, 3 * E, a.y, E, r0, rmax, gWn1, lane);
-      wg_tile(a.dqkv + 2 * E, 3 * E, a.y, E, r0, rmax, gWn2, lane);
-      cs[5] += cs_tile(a.dqkv, 3 * E, r0, rmax, lane);
-      cs[6] += cs_tile(a.dqkv + E, 3 * E, r0, rmax, lane);
-      cs[7] += cs_tile(a.dqkv + 2 * E, 3 * E, r0, rmax, lane);
+  const float* G = nullptr;
+  const float* X = nullptr;
+  int ldg = E;
+  int boff = -1, moff = -1;
+  switch (job) {
+    case J_WO1: G = scr + V_DA1 * MS; X = a.O; moff = OFF_WO1; boff = OFF_BO1; break;
+    case J_WQ: G = scr + V_DQ * MS; X = scr + V_X1 * MS; moff = OFF_WQ; boff = OFF_BQ; break;
+    case J_WO2: G = scr + V_DA2 * MS; X = scr + V_C * MS; moff = OFF_WO2; boff = OFF_BO2; break;
+    case J_W1: G = scr + V_DF1 * MS; X = scr + V_X2 * MS; moff = OFF_W1; boff = OFF_B1; break;
+    case J_W2: G = scr + V_DF2 * MS; X = scr + V_GL * MS; moff = OFF_W2; boff = OFF_B2; break;
+    case J_WN0: case J_WN1: case J_WN2: {
+      const int c = job - J_WN0;
+      G = a.dqkv + c * E; ldg = 3 * E; X = a.y; moff = OFF_WN + 1024 * c; boff = OFF_BN + 32 * c;
+      break;
     }
-    cs[0] += cs_tile(SV(V_DA1), E, r0, rmax, lane);
-    cs[1] += cs_tile(SV(V_DQ), E, r0, rmax, lane);
-    cs[2] += cs_tile(SV(V_DA2), E, r0, rmax, lane);
-    cs[3] += cs_tile(SV(V_DF1), E, r0, rmax, lane);
-    cs[4] += cs_tile(SV(V_DF2), E, r0, rmax, lane);
-    cs[8] += cs_tile(SV(V_DLN1X), E, r0, rmax, lane);
-    cs[9] += cs_tile(SV(V_DLN1), E, r0, rmax, lane);
-    cs[10] += cs_tile(SV(V_DLN2X), E, r0, rmax, lane);
-    cs[11] += cs_tile(SV(V_DLN2), E, r0, rmax, lane);
-    cs[12] += cs_tile(SV(V_DLN3X), E, r0, rmax, lane);
-    cs[13] += cs_tile(SV(V_DLN3), E, r0, rmax, lane);
+    case J_K: G = scr + V_Q * MS; X = scr + V_DS * MS; break;
+    case J_V: G = scr + V_DC * MS; X = scr + V_PD * MS; break;
+    default: break;
   }
-  // fixed-order workgroup reduction -> one partial per workgroup
+  const int t0 = ch * a.chunk, t1 = min(a.L, t0 + a.chunk);
+  const int64_t base = (int64_t)seq * a.L, rmax = base + t1;
   float* out = a.wpart + (int64_t)blockIdx.x * WPART;
-  auto reduce_mat = [&](const f16v& acc, int off) {
+  if (job == J_LN) {
+    const int voff[6] = {V_DLN1X, V_DLN1, V_DLN2X, V_DLN2, V_DLN3X, V_DLN3};
+    const int ooff[6] = {OFF_G1, OFF_BE1, OFF_G2, OFF_BE2, OFF_G3, OFF_BE3};
+    float cs[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32)
+#pragma unroll
+      for (int i = 0; i < 6; ++i) cs[i] += cs_tile(scr + voff[i] * MS, E, base + tt, rmax, lane);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) red[i * 256 + threadIdx.x] = cs[i];
     __syncthreads();
+    if (threadIdx.x < 6 * 32) {
+      const int i = threadIdx.x / 32, c = threadIdx.x % 32;
+      float sum = 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[wave * 1024 + F(r, h) * 32 + (lane & 31)] = acc[r];
-    __syncthreads();
-    for (int i = threadIdx.x; i < 1024; i += NT)
-      out[off + i] = ((red[i] + red[1024 + i]) + red[2048 + i]) + red[3072 + i];
-  };
-  reduce_mat(gWo1, OFF_WO1); reduce_mat(gWq, OFF_WQ); reduce_mat(gWo2, OFF_WO2);
-  reduce_mat(gW1, OFF_W1); reduce_mat(gW2, OFF_W2);
-  if (NEXT) { reduce_mat(gWn0, OFF_WN); reduce_mat(gWn1, OFF_WN + 1024); reduce_mat(gWn2, OFF_WN + 2048); }
-  const int coff[14] = {OFF_BO1, OFF_BQ, OFF_BO2, OFF_B1, OFF_B2, OFF_BN, OFF_BN + 32, OFF_BN + 64,
-                        OFF_G1, OFF_BE1, OFF_G2, OFF_BE2, OFF_G3, OFF_BE3};
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 14; ++i) red[wave * 1024 + i * 64 + lane] = cs[i];
-  __syncthreads();
-  for (int k = threadIdx.x; k < 14 * 32; k += NT) {
-    const int i = k / 32, c = k % 32;
-    if (!NEXT && i >= 5 && i <= 7) continue;
-    float s = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) s += red[w * 1024 + i * 64 + c] + red[w * 1024 + i * 64 + 32 + c];
-    out[coff[i] + c] = s;
+      for (int w = 0; w < NW; ++w) sum += red[i * 256 + w * 64 + c] + red[i * 256 + w * 64 + 32 + c];
+      out[ooff[i] + c] = sum;
+    }
+    return;
   }
-  // context grads: gK[f = F(r,h)][j' = lane&31], valid where (j' & 3) == f >> 3
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    red[wave * 2048 + F(r, h) * 32 + (lane & 31)] = gK[r];
-    red[wave * 2048 + 1024 + F(r, h) * 32 + (lane & 31)] = gV[r];
+  f16v acc = {};
+  float cs = 0.f;
+  for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32) {
+    wg_tile(G, ldg, X, E, base + tt, rmax, acc, lane);
+    if (boff >= 0) cs += cs_tile(G, ldg, base + tt, rmax, lane);
   }
-  __syncthreads();
-  const int nseq = a.M / a.L;
-  float* cp = a.cpart + ((int64_t)ch * nseq + seq) * a.Lc * 2 * E;
-  for (int i = threadIdx.x; i < a.Lc * 2 * E; i += NT) {
-    const int j = i / (2 * E), ff = i % (2 * E);
-    const int isv = ff >= E, f = ff % E;
-    const int idx = (isv ? 1024 : 0) + f * 32 + 4 * j + (f >> 3);
-    float s = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) s += red[w * 2048 + idx];
-    cp[i] = s;
+  for (int r = 0; r < 16; ++r) red[wave * 1024 + F(r, h) * 32 + (lane & 31)] = acc[r];
+  __syncthreads();
+  if (job == J_K || job == J_V) {
+    // acc[f = F(r,h)][j' = lane&31] is valid where (j' & 3) == f >> 3, j = j' >> 2 < Lc
+    const int nseq = a.M / a.L;
+    float* cp = a.cpart + ((int64_t)ch * nseq + seq) * a.Lc * 2 * E + (job == J_V ? E : 0);
+    for (int i = threadIdx.x; i < a.Lc * E; i += NT) {
+      const int j = i / E, f = i % E;
+      const int idx = f * 32 + 4 * j + (f >> 3);
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) sum += red[w * 1024 + idx];
+      cp[j * 2 * E + f] = sum;
+    }
+    return;
+  }
+  for (int i = threadIdx.x; i < 1024; i += NT)
+    out[moff + i] = ((red[i] + red[1024 + i]) + red[2048 + i]) + red[3072 + i];
+  __syncthreads();
+  red[threadIdx.x] = cs;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) sum += red[w * 64 + threadIdx.x] + red[w * 64 + 32 + threadIdx.x];
+    out[boff + threadIdx.x] = sum;
   }
 }
 
@@ -682,7 +680,7 @@ template <int LC, bool NEXT, bool DROP>
 int launch_bwd(const Tail& a, int grid, float* scr, hipStream_t s) {
   hipLaunchKernelGGL((dec_tail_bwd_data<LC, NEXT, DROP>), dim3(grid), dim3(NT), 0, s, a, scr);
   VAESNE_CHECK_LAUNCH();
-  hipLaunchKernelGGL((dec_tail_wgrad<NEXT>), dim3(grid), dim3(NT), 0, s, a, (const float*)scr);
+  hipLaunchKernelGGL(dec_tail_wgrad, dim3(grid, NJOB), dim3(NT), 0, s, a, (const float*)scr);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
@@ -741,14 +739,13 @@ VAESNE_API int vaesne_dec_tail_fwd(const float* x, const float* O, const float* 
   return dispatch<true>(a, grid, nullptr, (hipStream_t)stream);
 }
 
-// grads: [Wo1, bo1, g1, be1, Wq, bq, Wo2, bo2, g2, be2, W1, b1, W2, b2, g3, be3, Wn, bn]
-// (same order as w; the Wn/bn entries only when fused), dkvc [Nseq, Lc, 64].
+// gflat [8640]: every parameter gradient of the block in the layout of the
+// per-workgroup partials (see include/vaesne_hip.h); dkvc [Nseq, Lc, 64].
 VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* kvc, int M, int L,
                                    int Lc, const float* const* w, float p_drop,
                                    const int64_t* rng, uint32_t call_id, const float* y,
                                    const float* dy, const float* dqkv, float* dx, float* dO,
-                                   float* dkvc,
-                                   float* const* grads, float* workspace, void* stream) {
+                                   float* dkvc, float* gflat, float* workspace, void* stream) {
   if (!shapes_ok(M, L, Lc)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   Tail a = make(x, O, kvc, M, L, Lc, w, p_drop, rng, call_id);
@@ -762,22 +759,18 @@ VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* 
   float* scr = a.cpart + (int64_t)chunks * (M / L) * Lc * 2 * E;
   int rc = dispatch<false>(a, grid, scr, s);
   if (rc) return rc;
-  // fixed-order sums of the per-workgroup partials
-  struct Seg { int off, n, gi; };
-  const Seg segs[] = {{OFF_WO1, 1024, 0}, {OFF_BO1, 32, 1}, {OFF_G1, 32, 2}, {OFF_BE1, 32, 3},
-                      {OFF_WQ, 1024, 4}, {OFF_BQ, 32, 5}, {OFF_WO2, 1024, 6}, {OFF_BO2, 32, 7},
-                      {OFF_G2, 32, 8}, {OFF_BE2, 32, 9}, {OFF_W1, 1024, 10}, {OFF_B1, 32, 11},
-                      {OFF_W2, 1024, 12}, {OFF_B2, 32, 13}, {OFF_G3, 32, 14}, {OFF_BE3, 32, 15},
-                      {OFF_WN, 3072, 16}, {OFF_BN, 96, 17}};
-  // one column sum over the whole [grid][WPART] buffer into a staging area is
-  // simplest: colsum writes directly to each gradient tensor segment.
-  for (const Seg& sg : segs) {
-    if (sg.gi >= 16 && !a.Wn) continue;
-    if (!grads[sg.gi]) continue;
-    rc = launch_colsum_strided(workspace + sg.off, grid, sg.n, WPART, grads[sg.gi], s);
-    if (rc) return rc;
-  }
+  // fixed-order sums of the per-workgroup partials: all parameters in one pass
+  rc = launch_colsum(workspace, grid, WPART, gflat, nullptr, WPART, 0, s);
+  if (rc) return rc;
   // context grads: sum over chunks -> dkvc [Nseq * Lc * 64]
   return launch_colsum(a.cpart, chunks, (M / L) * Lc * 2 * E, dkvc, nullptr,
                        (M / L) * Lc * 2 * E, 0, s);
+}
+
+VAESNE_API int vaesne_dec_tail_grad_layout(int* offsets) {
+  const int off[18] = {OFF_WO1, OFF_BO1, OFF_G1, OFF_BE1, OFF_WQ, OFF_BQ, OFF_WO2, OFF_BO2,
+                       OFF_G2, OFF_BE2, OFF_W1, OFF_B1, OFF_W2, OFF_B2, OFF_G3, OFF_BE3,
+                       OFF_WN, OFF_BN};
+  for (int i = 0; i < 18; ++i) offsets[i] = off[i];
+  return WPART;
 }
