@@ -172,19 +172,21 @@ def roofline(device, B):
     do = torch.randn(N, L, E, device=device)
     dqkv = torch.empty_like(qkv)
     st = rng.state(device)
+    bits = torch.empty(lib_size := _lib.lib.attn_keep_bits_size(N, H, L, L), dtype=torch.uint8,
+                       device=device)
     b, d = qkv.data_ptr(), dqkv.data_ptr()
     lib, s3 = _lib.lib, L * 3 * E
 
     def fwd():
         lib.attn_fwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E, kbias.data_ptr(), L,
                      o.data_ptr(), L * E, E, lse.data_ptr(), N, H, L, L, dh, 0.1, st.data_ptr(), 7,
-                     _lib.stream())
+                     bits.data_ptr(), _lib.stream())
 
     def bwd():
         lib.attn_bwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E, kbias.data_ptr(), L,
                      o.data_ptr(), L * E, E, lse.data_ptr(), do.data_ptr(), L * E, E,
                      d, s3, 3 * E, d + 4 * E, s3, 3 * E, d + 8 * E, s3, 3 * E,
-                     N, H, L, L, dh, 0.1, st.data_ptr(), 7, _lib.stream())
+                     N, H, L, L, dh, 0.1, bits.data_ptr(), _lib.stream())
 
     t_f = time_kernel(fwd, 20, device)
     t_b = time_kernel(bwd, 20, device)

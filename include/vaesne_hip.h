@@ -77,21 +77,26 @@ int vaesne_reduce_partials(const float* partial, int G, int F, float* out0, floa
  * dropout(p) on the probabilities, P v.  Flash-style: scores never stored.
  * The key_padding_mask enters as an additive key bias kbias [B, Lk] (0 or -inf,
  * built once per mask by vaesne_mask_bias; null = no mask).
- * lse [B,H,Lq] (log2 domain) is saved for the backward.  dh in {8, 16}. */
+ * lse [B,H,Lq] (log2 domain) is saved for the backward.  dh in {8, 16}.
+ * Dropout (p_drop > 0): the forward draws the keep mask from the counter RNG
+ * and stores it in keep_bits (1 bit per score, vaesne_attn_keep_bits_size
+ * bytes); the backward reads it. */
 int vaesne_mask_bias(const uint8_t* mask, int64_t n, float* out, void* stream);
+int64_t vaesne_attn_keep_bits_size(int B, int H, int Lq, int Lk);
 int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
                     int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls,
                     const float* kbias, int64_t kb_bs, float* o, int64_t o_bs, int64_t o_ls,
                     float* lse, int B, int H, int Lq, int Lk, int dh, float p_drop,
-                    const int64_t* rng_state, uint32_t call_id, void* stream);
+                    const int64_t* rng_state, uint32_t call_id, uint32_t* keep_bits,
+                    void* stream);
 int vaesne_attn_bwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
                     int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls,
                     const float* kbias, int64_t kb_bs, const float* o, int64_t o_bs,
                     int64_t o_ls, const float* lse, const float* dout, int64_t do_bs,
                     int64_t do_ls, float* dq, int64_t dq_bs, int64_t dq_ls, float* dk,
                     int64_t dk_bs, int64_t dk_ls, float* dv, int64_t dv_bs, int64_t dv_ls, int B,
-                    int H, int Lq, int Lk, int dh, float p_drop, const int64_t* rng_state,
-                    uint32_t call_id, void* stream);
+                    int H, int Lq, int Lk, int dh, float p_drop, const uint32_t* keep_bits,
+                    void* stream);
 
 /* ---- fused decoder-block tail --------------------------------------------------
  * Everything of a decoder TransformerBlock after its masked self-attention core

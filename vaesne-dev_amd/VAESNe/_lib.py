@@ -37,11 +37,12 @@ SIGNATURES = {
                                 I32, P, I64, I32, P, P, I32, P, P]),
     "vaesne_reduce_partials": (I32, [P, I32, I32, P, P, I32, I32, P]),
     "vaesne_mask_bias": (I32, [P, I64, P, P]),
+    "vaesne_attn_keep_bits_size": (I64, [I32, I32, I32, I32]),
     "vaesne_attn_fwd": (I32, [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, P, I64, I64, P, I32,
-                              I32, I32, I32, I32, F32, P, U32, P]),
+                              I32, I32, I32, I32, F32, P, U32, P, P]),
     "vaesne_attn_bwd": (I32, [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, P, I64, I64, P, P,
                               I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I32, I32, I32, I32,
-                              I32, F32, P, U32, P]),
+                              I32, F32, P, P]),
     "vaesne_dec_tail_workspace": (I64, [I32, I32, I32]),
     "vaesne_dec_tail_fwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P]),
     "vaesne_dec_tail_bwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P, P, P, P, P,
