@@ -8,7 +8,8 @@ only exchange is ONE all-reduce of the flat fp32 gradient per step
 
   * m_iwae is a SUM over the batch  -> all-reduce SUM reproduces the
     single-process full-batch gradient exactly (up to summation order);
-  * elbo is a MEAN over K*B         -> all-reduce SUM / world (equal shards).
+  * elbo is a MEAN over K*B         -> each rank scales its gradient by its
+    shard's share of the batch (b_r / B; 1/world for equal shards), then SUM.
 
 Parameters are broadcast from rank 0 once at setup.  Backend "nccl" is RCCL on
 ROCm; "gloo" is used by the CPU-side tests of the process-group logic.
@@ -45,6 +46,15 @@ def shard(batch, rank=None, world_size=None):
     return tuple(cut(t) for t in batch)
 
 
+def shard_fraction(B, rank=None, world_size=None):
+    """b_r / B for the contiguous split `shard` makes (the weight of this
+    rank's mean-objective gradient in the global mean)."""
+    if rank is None:
+        rank, world_size = world()
+    b = B // world_size
+    return ((B - rank * b) if rank == world_size - 1 else b) / B
+
+
 def broadcast_parameters(module, src=0):
     """Make every rank start from rank `src`'s parameters (and buffers)."""
     if world()[1] == 1:
@@ -55,26 +65,29 @@ def broadcast_parameters(module, src=0):
 
 
 class GradAllReduce:
-    """Hook for FusedAdamW(grad_hook=...): one all-reduce of the flat gradient."""
+    """Hook for FusedAdamW(grad_hook=...): one all-reduce of the flat gradient.
+    For reduction="mean", `weight` is this rank's shard fraction b_r / B
+    (None = 1/world, equal shards); training_step sets it per batch."""
 
-    def __init__(self, reduction="sum", group=None):
+    def __init__(self, reduction="sum", group=None, weight=None):
         if reduction not in ("sum", "mean"):
             raise ValueError(reduction)
         self.reduction = reduction
         self.group = group
+        self.weight = weight
 
     def __call__(self, flat_grad):
         ws = world()[1]
         if ws == 1:
             return
-        dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.group)
         if self.reduction == "mean":
-            flat_grad.div_(ws)
+            flat_grad.mul_(self.weight if self.weight is not None else 1.0 / ws)
+        dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.group)
 
 
-def allreduce_grads(params, reduction="sum"):
+def allreduce_grads(params, reduction="sum", weight=None):
     """For optimizers other than FusedAdamW: flatten p.grad, all-reduce once,
-    write back."""
+    write back.  `weight` as in GradAllReduce."""
     ws = world()[1]
     if ws == 1:
         return
@@ -82,9 +95,9 @@ def allreduce_grads(params, reduction="sum"):
     if not ps:
         return
     flat = torch.cat([p.grad.reshape(-1) for p in ps])
-    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
     if reduction == "mean":
-        flat.div_(ws)
+        flat.mul_(weight if weight is not None else 1.0 / ws)
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
     o = 0
     for p in ps:
         n = p.grad.numel()

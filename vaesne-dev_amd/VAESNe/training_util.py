@@ -35,18 +35,21 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
             x = [tuple(_x.to(device) for _x in modality) for modality in x]
         else:
             x = tuple(_x.to(device) for _x in x)
+        w = 1.0
         if ws > 1:
+            B = (x[0][0] if multimodal else x[0]).shape[0]
+            w = D.shard_fraction(B, rank, ws) if reduction == "mean" else 1.0
+            if isinstance(optimizer, FusedAdamW) and isinstance(optimizer.grad_hook, D.GradAllReduce):
+                optimizer.grad_hook.weight = w if reduction == "mean" else None
             x = D.shard(x, rank, ws)
         loss = -loss_fn(network, x)
         loss.backward()
         if ws > 1 and not isinstance(optimizer, FusedAdamW):
-            D.allreduce_grads(network.parameters(), reduction)
+            D.allreduce_grads(network.parameters(), reduction, weight=w)
         optimizer.step()
         if ws > 1:
-            loss = loss.detach().clone()
+            loss = loss.detach().clone() * w
             torch.distributed.all_reduce(loss)
-            if reduction == "mean":
-                loss /= ws
         total_loss += loss.detach().cpu().item()
         num_batches += 1.
         if release_memory:
