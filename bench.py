@@ -155,12 +155,14 @@ def time_kernel(fn, iters, device):
 
 
 def roofline(device, B):
-    """Spectra-decoder masked self-attention (N = K*B sequences x 982 tokens,
-    4 heads x dh 8, dropout 0.1), the dominant op of the step.
-    Algorithmic FLOPs: forward 4*dh per score (QK^T + PV), backward 8*dh per
-    score (S, dP, dV, dK, dQ products: recompute of S included as the
-    flash-backward's algorithmic work is usually quoted without it -> 4 products
-    = 8*dh counted here)."""
+    """Spectra-decoder masked self-attention at its step shape (N = K*B
+    sequences x 982 tokens, 4 heads x dh 8, dropout 0.1, 5 % key padding),
+    the dominant op of the step.  The roofline kernel is
+    attn_bwd_kv_kernel, the most expensive single kernel of the step; the
+    forward and the dQ kernel are reported beside it.  Algorithmic FLOPs per
+    score: fwd 4*dh (QK^T, PV), bwd_kv 8*dh (S, dP, dV, dK), bwd_q 6*dh
+    (S, dP, dQ) -- the flash backward's recomputation of S counts, as the
+    kernels must do it."""
     from VAESNe import _lib, rng
     N, L, E, H, dh = CFG["K"] * B, CFG["Ls"], CFG["model_dim"], CFG["num_heads"], 8
     qkv = torch.randn(N, L, 3 * E, device=device)
@@ -172,40 +174,40 @@ def roofline(device, B):
     do = torch.randn(N, L, E, device=device)
     dqkv = torch.empty_like(qkv)
     st = rng.state(device)
-    bits = torch.empty(lib_size := _lib.lib.attn_keep_bits_size(N, H, L, L), dtype=torch.uint8,
-                       device=device)
-    b, d = qkv.data_ptr(), dqkv.data_ptr()
-    lib, s3 = _lib.lib, L * 3 * E
+    lib = _lib.lib
+    bits = torch.empty(lib.attn_keep_bits_size(N, H, L, L), dtype=torch.uint8, device=device)
+    b, d, s3 = qkv.data_ptr(), dqkv.data_ptr(), L * 3 * E
 
     def fwd():
         lib.attn_fwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E, kbias.data_ptr(), L,
                      o.data_ptr(), L * E, E, lse.data_ptr(), N, H, L, L, dh, 0.1, st.data_ptr(), 7,
                      bits.data_ptr(), _lib.stream())
 
-    def bwd():
-        lib.attn_bwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E, kbias.data_ptr(), L,
-                     o.data_ptr(), L * E, E, lse.data_ptr(), do.data_ptr(), L * E, E,
-                     d, s3, 3 * E, d + 4 * E, s3, 3 * E, d + 8 * E, s3, 3 * E,
-                     N, H, L, L, dh, 0.1, bits.data_ptr(), _lib.stream())
+    def bwd(fn):
+        return lambda: fn(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E,
+                          kbias.data_ptr(), L, o.data_ptr(), L * E, E, lse.data_ptr(),
+                          do.data_ptr(), L * E, E, d, s3, 3 * E, d + 4 * E, s3, 3 * E, d + 8 * E,
+                          s3, 3 * E, N, H, L, L, dh, 0.1, st.data_ptr(), 7, bits.data_ptr(),
+                          _lib.stream())
 
-    t_f = time_kernel(fwd, 20, device)
-    t_b = time_kernel(bwd, 20, device)
+    fwd()
     scores = N * H * L * L
-    f_fwd = scores * 4 * dh
-    f_bwd = scores * 8 * dh
-    res = dict(
-        fwd=dict(kernel="attn_fwd_kernel", ms=t_f * 1e3, tflops=f_fwd / t_f / 1e12),
-        bwd=dict(kernel="attn_bwd (kv+q)", ms=t_b * 1e3, tflops=f_bwd / t_b / 1e12))
-    dom = "bwd" if t_b >= t_f else "fwd"
-    a = res[dom]["tflops"]
-    return dict(bound="mfma", kernel=res[dom]["kernel"], achieved=round(a, 3),
-                peak=FP32_PEAK_TFLOPS, unit="TFLOP/s", frac=round(a / FP32_PEAK_TFLOPS, 4),
-                traffic=None, launch_ms=round(res[dom]["ms"], 4),
-                flops_per_launch=f_bwd if dom == "bwd" else f_fwd,
+    res = {}
+    for name, kern, fn, fl in [("fwd", "attn_fwd_kernel", fwd, 4 * dh),
+                               ("bwd_kv", "attn_bwd_kv_kernel", bwd(lib.attn_bwd_kv), 8 * dh),
+                               ("bwd_q", "attn_bwd_q_kernel", bwd(lib.attn_bwd_q), 6 * dh)]:
+        t = time_kernel(fn, 20, device)
+        res[name] = dict(kernel=kern, ms=t * 1e3, tflops=scores * fl / t / 1e12,
+                         flops_per_launch=scores * fl)
+    r = res["bwd_kv"]
+    a = r["tflops"]
+    return dict(bound="mfma", kernel=r["kernel"], achieved=round(a, 3), peak=FP32_PEAK_TFLOPS,
+                unit="TFLOP/s", frac=round(a / FP32_PEAK_TFLOPS, 4), traffic=None,
+                launch_ms=round(r["ms"], 4), flops_per_launch=r["flops_per_launch"],
                 detail={k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                             for kk, vv in v.items()} for k, v in res.items()},
-                note="fp32 VALU kernel; peak = FP32 157.3 TF (vector = matrix rate on gfx950); "
-                     "scores per launch = K*B*H*982^2")
+                note="fp32 packed-VALU kernel; peak = FP32 157.3 TF (vector = f32-MFMA rate on "
+                     "gfx950); scores per launch = K*B*H*982^2 = %d" % scores)
 
 
 def cpu_baseline(sample_B=2, steps=2):

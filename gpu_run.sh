@@ -15,6 +15,9 @@ for s in $STAGES; do
     prof)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof.log 2>&1; rc=$?;;
   esac
   echo "$s rc=$rc"
-  tail -5 gpurun_out/*.log 2>/dev/null | tail -0
   ok $rc || exit $rc
+  # a GPU fault inside pytest still exits 1: stop the session there
+  if grep -qsE "illegal memory access|Memory access fault|hipErrorIllegalAddress|HSA_STATUS_ERROR" gpurun_out/pytest_gpu.log gpurun_out/smoke.log gpurun_out/bench.err; then
+    echo "GPU fault reported in $s; stopping"; exit 3
+  fi
 done

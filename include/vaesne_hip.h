@@ -89,14 +89,36 @@ int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, 
                     float* lse, int B, int H, int Lq, int Lk, int dh, float p_drop,
                     const int64_t* rng_state, uint32_t call_id, uint32_t* keep_bits,
                     void* stream);
+/* Backward.  Query-tiled shapes read the forward's keep_bits; the few-query
+ * path (Lq <= 16: the encoders' latent tokens, one fused key-parallel kernel)
+ * re-derives the keep decisions from (rng_state, call_id), which must be the
+ * forward's.  vaesne_attn_bwd = vaesne_attn_bwd_kv (dK, dV) then
+ * vaesne_attn_bwd_q (dQ); the split entries exist so a profiler can time each
+ * kernel alone (they run the whole fused kernel on the few-query path). */
 int vaesne_attn_bwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
-                    int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls,
-                    const float* kbias, int64_t kb_bs, const float* o, int64_t o_bs,
-                    int64_t o_ls, const float* lse, const float* dout, int64_t do_bs,
-                    int64_t do_ls, float* dq, int64_t dq_bs, int64_t dq_ls, float* dk,
-                    int64_t dk_bs, int64_t dk_ls, float* dv, int64_t dv_bs, int64_t dv_ls, int B,
-                    int H, int Lq, int Lk, int dh, float p_drop, const uint32_t* keep_bits,
+                    int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls, const float* kbias,
+                    int64_t kb_bs, const float* o, int64_t o_bs, int64_t o_ls, const float* lse,
+                    const float* dout, int64_t do_bs, int64_t do_ls, float* dq, int64_t dq_bs,
+                    int64_t dq_ls, float* dk, int64_t dk_bs, int64_t dk_ls, float* dv, int64_t dv_bs,
+                    int64_t dv_ls, int B, int H, int Lq, int Lk, int dh, float p_drop,
+                    const int64_t* rng_state, uint32_t call_id, const uint32_t* keep_bits,
                     void* stream);
+int vaesne_attn_bwd_kv(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
+                       int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls, const float* kbias,
+                       int64_t kb_bs, const float* o, int64_t o_bs, int64_t o_ls, const float* lse,
+                       const float* dout, int64_t do_bs, int64_t do_ls, float* dq, int64_t dq_bs,
+                       int64_t dq_ls, float* dk, int64_t dk_bs, int64_t dk_ls, float* dv, int64_t dv_bs,
+                       int64_t dv_ls, int B, int H, int Lq, int Lk, int dh, float p_drop,
+                       const int64_t* rng_state, uint32_t call_id, const uint32_t* keep_bits,
+                       void* stream);
+int vaesne_attn_bwd_q(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
+                      int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls, const float* kbias,
+                      int64_t kb_bs, const float* o, int64_t o_bs, int64_t o_ls, const float* lse,
+                      const float* dout, int64_t do_bs, int64_t do_ls, float* dq, int64_t dq_bs,
+                      int64_t dq_ls, float* dk, int64_t dk_bs, int64_t dk_ls, float* dv, int64_t dv_bs,
+                      int64_t dv_ls, int B, int H, int Lq, int Lk, int dh, float p_drop,
+                      const int64_t* rng_state, uint32_t call_id, const uint32_t* keep_bits,
+                      void* stream);
 
 /* ---- fused decoder-block tail --------------------------------------------------
  * Everything of a decoder TransformerBlock after its masked self-attention core

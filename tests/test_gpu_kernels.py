@@ -41,6 +41,9 @@ def _rand_mask(B, L, p, g, keep_first=True):
     (2, 983, 983, True, 0.05),     # spectra encoder context self-attention (cfg 5)
     (4, 60, 60, True, 0.1),        # photometry decoder self-attention
     (3, 8, 983, False, 0.05),      # encoder cross-attention (queries = latent tokens)
+    (3, 13, 983, False, 0.05),     # few-query path, two ragged query groups
+    (4, 16, 60, False, 0.1),       # latent_len 8 (16 latent tokens) over a light curve
+    (5, 8, 8, True, 0.0),          # encoder latent self-attention
     (5, 982, 5, False, 0.0),       # spectra decoder cross-attention (4 latent + phase)
     (2, 37, 1, False, 0.0),        # a single key
     (2, 300, 257, False, 0.9),     # heavy ragged masking
@@ -115,9 +118,11 @@ def _probe_attention_mask(B, Lq, Lk, j0, p, seed_call):
     return keep, q, kv, mask
 
 
-def test_attention_dropout_statistics_and_backward_mask():
+@pytest.mark.parametrize("B,Lq,Lk", [(4, 512, 130), (128, 8, 130), (96, 13, 983)])
+def test_attention_dropout_statistics_and_backward_mask(B, Lq, Lk):
+    """Query-tiled (Lq=512) and key-parallel few-query (Lq<=16) kernels."""
     from VAESNe import _ops, rng
-    B, Lq, Lk, p = 4, 512, 130, 0.1
+    p = 0.1
     keep, q, kv, mask = _probe_attention_mask(B, Lq, Lk, 100, p, 777)
     assert set(torch.unique(keep).tolist()) <= {0.0, 1.0}
     rate = 1 - keep.mean().item()

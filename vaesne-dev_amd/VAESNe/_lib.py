@@ -25,6 +25,10 @@ F32 = C.c_float
 PP = C.POINTER(C.c_void_p)
 
 # name -> (restype, argtypes).  Mirrors include/vaesne_hip.h one to one.
+_ATTN_BWD = (I32, [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, P, I64, I64, P, P, I64, I64, P,
+                   I64, I64, P, I64, I64, P, I64, I64, I32, I32, I32, I32, I32, F32, P, U32, P,
+                   P])
+
 SIGNATURES = {
     "vaesne_linear_fwd": (I32, [P, I64, P, I64, I64, I32, P, P, I32, P, I64, P, I64, I32, I32, P]),
     "vaesne_linear_bwd_data": (I32, [P, I64, P, I64, I32, I64, I32, P, I32, P, I64, I32, P]),
@@ -40,9 +44,9 @@ SIGNATURES = {
     "vaesne_attn_keep_bits_size": (I64, [I32, I32, I32, I32]),
     "vaesne_attn_fwd": (I32, [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, P, I64, I64, P, I32,
                               I32, I32, I32, I32, F32, P, U32, P, P]),
-    "vaesne_attn_bwd": (I32, [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, P, I64, I64, P, P,
-                              I64, I64, P, I64, I64, P, I64, I64, P, I64, I64, I32, I32, I32, I32,
-                              I32, F32, P, P]),
+    "vaesne_attn_bwd": _ATTN_BWD,
+    "vaesne_attn_bwd_kv": _ATTN_BWD,
+    "vaesne_attn_bwd_q": _ATTN_BWD,
     "vaesne_dec_tail_workspace": (I64, [I32, I32, I32]),
     "vaesne_dec_tail_fwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P]),
     "vaesne_dec_tail_bwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P, P, P, P, P,

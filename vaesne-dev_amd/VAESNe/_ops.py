@@ -194,7 +194,7 @@ def _attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, kbias, B, H, Lq, Lk, dh, p, dev):
         bits = torch.empty((n + 3) // 4, dtype=torch.int32, device=dev)
     lib.attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, ptr(kbias), Lk, o.data_ptr(), Lq * E, E,
                  lse.data_ptr(), B, H, Lq, Lk, dh, float(p), ptr(st), cid, ptr(bits), stream())
-    return o, lse, bits
+    return o, lse, bits, st, cid
 
 
 class SelfAttnFn(torch.autograd.Function):
@@ -208,16 +208,17 @@ class SelfAttnFn(torch.autograd.Function):
         E = E3 // 3
         dh = E // H
         base = qkv.data_ptr()
-        o, lse, bits = _attn_fwd(base, L * E3, E3, base + 4 * E, L * E3, E3, base + 8 * E,
-                                 L * E3, E3, kbias, B, H, L, L, dh, p, qkv.device)
-        ctx.dims = (B, L, E, H, dh, float(p))
-        ctx.save_for_backward(qkv, kbias, o, lse, bits)
+        o, lse, bits, st, cid = _attn_fwd(base, L * E3, E3, base + 4 * E, L * E3, E3,
+                                          base + 8 * E, L * E3, E3, kbias, B, H, L, L, dh, p,
+                                          qkv.device)
+        ctx.dims = (B, L, E, H, dh, float(p), cid)
+        ctx.save_for_backward(qkv, kbias, o, lse, bits, st)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qkv, kbias, o, lse, bits = ctx.saved_tensors
-        B, L, E, H, dh, p = ctx.dims
+        qkv, kbias, o, lse, bits, st = ctx.saved_tensors
+        B, L, E, H, dh, p, cid = ctx.dims
         do = do.contiguous()
         E3 = 3 * E
         dqkv = torch.empty_like(qkv)
@@ -225,7 +226,7 @@ class SelfAttnFn(torch.autograd.Function):
         lib.attn_bwd(b, L * E3, E3, b + 4 * E, L * E3, E3, b + 8 * E, L * E3, E3, ptr(kbias), L,
                      o.data_ptr(), L * E, E, lse.data_ptr(), do.data_ptr(), L * E, E,
                      d, L * E3, E3, d + 4 * E, L * E3, E3, d + 8 * E, L * E3, E3,
-                     B, H, L, L, dh, p, ptr(bits), stream())
+                     B, H, L, L, dh, p, ptr(st), cid, ptr(bits), stream())
         return dqkv, None, None, None
 
 
@@ -241,16 +242,17 @@ class CrossAttnFn(torch.autograd.Function):
         Lk = kv.shape[1]
         dh = E // H
         kb = kv.data_ptr()
-        o, lse, bits = _attn_fwd(q.data_ptr(), Lq * E, E, kb, Lk * 2 * E, 2 * E, kb + 4 * E,
-                                 Lk * 2 * E, 2 * E, kbias, B, H, Lq, Lk, dh, p, q.device)
-        ctx.dims = (B, Lq, Lk, E, H, dh, float(p))
-        ctx.save_for_backward(q, kv, kbias, o, lse, bits)
+        o, lse, bits, st, cid = _attn_fwd(q.data_ptr(), Lq * E, E, kb, Lk * 2 * E, 2 * E,
+                                          kb + 4 * E, Lk * 2 * E, 2 * E, kbias, B, H, Lq, Lk,
+                                          dh, p, q.device)
+        ctx.dims = (B, Lq, Lk, E, H, dh, float(p), cid)
+        ctx.save_for_backward(q, kv, kbias, o, lse, bits, st)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, kv, kbias, o, lse, bits = ctx.saved_tensors
-        B, Lq, Lk, E, H, dh, p = ctx.dims
+        q, kv, kbias, o, lse, bits, st = ctx.saved_tensors
+        B, Lq, Lk, E, H, dh, p, cid = ctx.dims
         do = do.contiguous()
         dq = torch.empty_like(q)
         dkv = torch.empty_like(kv)
@@ -258,7 +260,7 @@ class CrossAttnFn(torch.autograd.Function):
         lib.attn_bwd(q.data_ptr(), Lq * E, E, kb, Lk * 2 * E, 2 * E, kb + 4 * E, Lk * 2 * E,
                      2 * E, ptr(kbias), Lk, o.data_ptr(), Lq * E, E, lse.data_ptr(), do.data_ptr(),
                      Lq * E, E, dq.data_ptr(), Lq * E, E, dkb, Lk * 2 * E, 2 * E, dkb + 4 * E,
-                     Lk * 2 * E, 2 * E, B, H, Lq, Lk, dh, p, ptr(bits), stream())
+                     Lk * 2 * E, 2 * E, B, H, Lq, Lk, dh, p, ptr(st), cid, ptr(bits), stream())
         return dq, dkv, None, None, None
 
 

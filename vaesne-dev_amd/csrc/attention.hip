@@ -99,45 +99,46 @@ __device__ __forceinline__ void stage(float* dst, const float* __restrict__ src,
 }
 
 // ============================== forward ====================================
-// lane owns queries i + {0, 1, 2, 3} * NTT (pairs A = {0,1}, B = {2,3})
-template <int DH, int NTT, bool DROP>
+// lane owns 2*NP queries: pair p = {i + (2p) NTT, i + (2p+1) NTT}
+template <int DH, int NTT, int NP, bool DROP>
 __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Ks[TK * DH];
   __shared__ __attribute__((aligned(16))) float Vs[TK * DH];
   __shared__ float Kb[TK];
-  constexpr int QB = 4 * NTT;
+  constexpr int R = 2 * NP;
+  constexpr int QB = R * NTT;
   const int nqb = (a.Lq + QB - 1) / QB;
   const int qb = blockIdx.x % nqb;
   const int bh = blockIdx.x / nqb;
   const int b = bh / a.H, h = bh - b * a.H;
-  int qi[4], qc[4];
+  int qi[R], qc[R];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < R; ++u) {
     qi[u] = qb * QB + u * NTT + threadIdx.x;
     qc[u] = min(qi[u], a.Lq - 1);
   }
-  f2 qA[DH], qB[DH], oA[DH], oB[DH];
+  f2 q[NP][DH], o[NP][DH], m[NP], l[NP];
   {
-    float t0[DH], t1[DH], t2[DH], t3[DH];
     const float* qbase = a.q + (int64_t)b * a.q_bs + h * DH;
-    ldr<DH>(qbase + (int64_t)qc[0] * a.q_ls, t0);
-    ldr<DH>(qbase + (int64_t)qc[1] * a.q_ls, t1);
-    ldr<DH>(qbase + (int64_t)qc[2] * a.q_ls, t2);
-    ldr<DH>(qbase + (int64_t)qc[3] * a.q_ls, t3);
 #pragma unroll
-    for (int d = 0; d < DH; ++d) {
-      qA[d] = (f2){t0[d], t1[d]} * a.scale_log2;
-      qB[d] = (f2){t2[d], t3[d]} * a.scale_log2;
-      oA[d] = bc(0.f);
-      oB[d] = bc(0.f);
+    for (int p = 0; p < NP; ++p) {
+      float t0[DH], t1[DH];
+      ldr<DH>(qbase + (int64_t)qc[2 * p] * a.q_ls, t0);
+      ldr<DH>(qbase + (int64_t)qc[2 * p + 1] * a.q_ls, t1);
+#pragma unroll
+      for (int d = 0; d < DH; ++d) {
+        q[p][d] = (f2){t0[d], t1[d]} * a.scale_log2;
+        o[p][d] = bc(0.f);
+      }
+      m[p] = bc(-INFINITY);
+      l[p] = bc(0.f);
     }
   }
-  f2 mA = bc(-INFINITY), mB = bc(-INFINITY), lA = bc(0.f), lB = bc(0.f);
-  uint32_t rk[4] = {0u, 0u, 0u, 0u};
+  uint32_t rk[R];
   if (DROP) {
     const uint32_t skey = key_of(a.rng_state, a.call_id);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) rk[u] = attn_row_key(skey, (uint32_t)((int64_t)bh * a.Lq + qc[u]));
+    for (int u = 0; u < R; ++u) rk[u] = attn_row_key(skey, (uint32_t)((int64_t)bh * a.Lq + qc[u]));
   }
   const float* kg = a.k + (int64_t)b * a.k_bs + h * DH;
   const float* vg = a.v + (int64_t)b * a.v_bs + h * DH;
@@ -152,70 +153,80 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
       Kb[i] = kt + i < a.Lk ? (kbg ? kbg[kt + i] : 0.f) : -INFINITY;
     __syncthreads();
     const int kend = min(TK, a.Lk - kt);
-    uint32_t w[4] = {0u, 0u, 0u, 0u};   // keep bits of the current 32-key word
+    uint32_t w[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) w[u] = 0u;
     for (int g0 = 0; g0 < kend; g0 += 8) {
-      f2 sA[8], sB[8];
-      f2 xA = mA, xB = mB;
+      f2 s[NP][8];
+      f2 x[NP];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) x[p] = m[p];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         float kr[DH];
         lrow<DH>(Ks + (g0 + u) * DH, kr);
         const float kb = Kb[g0 + u];
-        f2 aA = bc(kb), aB = bc(kb);
 #pragma unroll
-        for (int d = 0; d < DH; ++d) {
-          aA = fma2(qA[d], bc(kr[d]), aA);
-          aB = fma2(qB[d], bc(kr[d]), aB);
+        for (int p = 0; p < NP; ++p) {
+          f2 acc = bc(kb);
+#pragma unroll
+          for (int d = 0; d < DH; ++d) acc = fma2(q[p][d], bc(kr[d]), acc);
+          s[p][u] = acc;
+          x[p] = __builtin_elementwise_max(x[p], acc);
         }
-        sA[u] = aA;
-        sB[u] = aB;
-        xA = __builtin_elementwise_max(xA, aA);
-        xB = __builtin_elementwise_max(xB, aB);
       }
-      // rows whose keys are all masked so far keep m = -inf: exponent origin 0
-      const f2 uA = (f2){xA.x == -INFINITY ? 0.f : xA.x, xA.y == -INFINITY ? 0.f : xA.y};
-      const f2 uB = (f2){xB.x == -INFINITY ? 0.f : xB.x, xB.y == -INFINITY ? 0.f : xB.y};
-      const f2 cA = ex2(mA - uA), cB = ex2(mB - uB);
-      mA = xA; mB = xB;
-      lA *= cA; lB *= cB;
+      f2 mu[NP];
 #pragma unroll
-      for (int d = 0; d < DH; ++d) { oA[d] *= cA; oB[d] *= cB; }
+      for (int p = 0; p < NP; ++p) {
+        // rows whose keys are all masked so far keep m = -inf: exponent origin 0
+        mu[p] = (f2){x[p].x == -INFINITY ? 0.f : x[p].x, x[p].y == -INFINITY ? 0.f : x[p].y};
+        const f2 c = ex2(m[p] - mu[p]);
+        m[p] = x[p];
+        l[p] *= c;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) o[p][d] *= c;
+      }
 #pragma unroll
       for (int u = 0; u < 8; u += 2) {
-        f2 pA0 = ex2(sA[u] - uA), pA1 = ex2(sA[u + 1] - uA);
-        f2 pB0 = ex2(sB[u] - uB), pB1 = ex2(sB[u + 1] - uB);
-        lA += pA0 + pA1;
-        lB += pB0 + pB1;
+        f2 p0[NP], p1[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          p0[p] = ex2(s[p][u] - mu[p]);
+          p1[p] = ex2(s[p][u + 1] - mu[p]);
+          l[p] += p0[p] + p1[p];
+        }
         if (DROP) {
           const uint32_t kp = (uint32_t)((kt + g0 + u) >> 1);
           const int sh = (g0 + u) & 31;
-          uint32_t kk[4];
+          uint32_t kk[R];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
+          for (int t = 0; t < R; ++t) {
             const uint32_t bits = attn_pair_bits(rk[t], kp);
             kk[t] = ((bits & 0xffffu) >= a.thr ? 1u : 0u) | ((bits >> 16) >= a.thr ? 2u : 0u);
             w[t] |= kk[t] << sh;
           }
-          pA0 = sel2(kk[0] & 1u, kk[1] & 1u, pA0);
-          pA1 = sel2(kk[0] & 2u, kk[1] & 2u, pA1);
-          pB0 = sel2(kk[2] & 1u, kk[3] & 1u, pB0);
-          pB1 = sel2(kk[2] & 2u, kk[3] & 2u, pB1);
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            p0[p] = sel2(kk[2 * p] & 1u, kk[2 * p + 1] & 1u, p0[p]);
+            p1[p] = sel2(kk[2 * p] & 2u, kk[2 * p + 1] & 2u, p1[p]);
+          }
         }
         float v0[DH], v1[DH];
         lrow<DH>(Vs + (g0 + u) * DH, v0);
         lrow<DH>(Vs + (g0 + u + 1) * DH, v1);
 #pragma unroll
         for (int d = 0; d < DH; ++d) {
-          oA[d] = fma2(pA0, bc(v0[d]), oA[d]);
-          oB[d] = fma2(pB0, bc(v0[d]), oB[d]);
-          oA[d] = fma2(pA1, bc(v1[d]), oA[d]);
-          oB[d] = fma2(pB1, bc(v1[d]), oB[d]);
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            o[p][d] = fma2(p0[p], bc(v0[d]), o[p][d]);
+            o[p][d] = fma2(p1[p], bc(v1[d]), o[p][d]);
+          }
         }
       }
       if (DROP && (((g0 + 8) & 31) == 0 || g0 + 8 >= kend)) {
         const int word = (kt + g0) >> 5;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < R; ++t) {
           if (qi[t] < a.Lq) bitp[(int64_t)word * a.Lq + qi[t]] = w[t];
           w[t] = 0u;
         }
@@ -224,78 +235,76 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   }
   // l == 0 (every key masked) -> 0/0 = NaN, as the reference's -inf softmax
   const float ik = DROP ? a.inv_keep : 1.f;
-  const f2 iA = bc(ik) / lA, iB = bc(ik) / lB;
-  float r[4][DH];
 #pragma unroll
-  for (int d = 0; d < DH; ++d) {
-    r[0][d] = oA[d].x * iA.x; r[1][d] = oA[d].y * iA.y;
-    r[2][d] = oB[d].x * iB.x; r[3][d] = oB[d].y * iB.y;
-  }
-  const float lse4[4] = {mA.x + __log2f(lA.x), mA.y + __log2f(lA.y), mB.x + __log2f(lB.x),
-                         mB.y + __log2f(lB.y)};
+  for (int p = 0; p < NP; ++p) {
+    const f2 inv = bc(ik) / l[p];
+    float r0[DH], r1[DH];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    if (qi[u] < a.Lq) {
-      str<DH>(a.o_out + (int64_t)b * a.o_bs + (int64_t)qi[u] * a.o_ls + h * DH, r[u]);
-      a.lse[(int64_t)bh * a.Lq + qi[u]] = lse4[u];
+    for (int d = 0; d < DH; ++d) { r0[d] = o[p][d].x * inv.x; r1[d] = o[p][d].y * inv.y; }
+    const int i0 = qi[2 * p], i1 = qi[2 * p + 1];
+    if (i0 < a.Lq) {
+      str<DH>(a.o_out + (int64_t)b * a.o_bs + (int64_t)i0 * a.o_ls + h * DH, r0);
+      a.lse[(int64_t)bh * a.Lq + i0] = m[p].x + __log2f(l[p].x);
+    }
+    if (i1 < a.Lq) {
+      str<DH>(a.o_out + (int64_t)b * a.o_bs + (int64_t)i1 * a.o_ls + h * DH, r1);
+      a.lse[(int64_t)bh * a.Lq + i1] = m[p].y + __log2f(l[p].y);
     }
   }
 }
 
 // ============================== dK, dV =====================================
-// lane owns keys k0 .. k0+3 (k0 = 4*lane + block offset): pairs A = {k0, k0+1},
-// B = {k0+2, k0+3}; queries stream through LDS tiles
-template <int DH, int NTT, bool DROP>
+// lane owns 2*NP adjacent keys key0 .. key0 + 2NP - 1 (pairs of adjacent keys);
+// queries stream through LDS tiles
+template <int DH, int NTT, int NP, bool DROP>
 __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
+  constexpr int R = 2 * NP;
+  constexpr int KB = R * NTT;
+  constexpr int NWB = (KB + 31) / 32;       // bitmap words of this key block
   __shared__ __attribute__((aligned(16))) float Qs[TK * DH];
   __shared__ __attribute__((aligned(16))) float Ds_[TK * DH];   // dO tile
   __shared__ float Ls[TK], Dd[TK];
-  __shared__ uint32_t Ws[TK * (4 * NTT / 32)];
-  constexpr int KB = 4 * NTT;
-  constexpr int NWB = KB / 32;              // bitmap words of this key block
+  __shared__ uint32_t Ws[TK * NWB];
   const int nkb = (a.Lk + KB - 1) / KB;
   const int kb = blockIdx.x % nkb;
   const int bh = blockIdx.x / nkb;
   const int b = bh / a.H, h = bh - b * a.H;
-  const int key0 = kb * KB + 4 * threadIdx.x;
-  f2 kA[DH], kB_[DH], vA[DH], vB[DH], dkA[DH], dkB[DH], dvA[DH], dvB[DH];
+  const int key0 = kb * KB + R * threadIdx.x;
+  f2 k[NP][DH], v[NP][DH], dk[NP][DH], dv[NP][DH], kbias[NP];
   {
-    float t[4][DH];
     const float* kbase = a.k + (int64_t)b * a.k_bs + h * DH;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) ldr<DH>(kbase + (int64_t)min(key0 + u, a.Lk - 1) * a.k_ls, t[u]);
-#pragma unroll
-    for (int d = 0; d < DH; ++d) {
-      kA[d] = (f2){t[0][d], t[1][d]};     // the streamed Q tile carries the scale
-      kB_[d] = (f2){t[2][d], t[3][d]};
-    }
     const float* vbase = a.v + (int64_t)b * a.v_bs + h * DH;
+    const float* kbp = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) ldr<DH>(vbase + (int64_t)min(key0 + u, a.Lk - 1) * a.v_ls, t[u]);
+    for (int p = 0; p < NP; ++p) {
+      const int j0 = key0 + 2 * p, j1 = j0 + 1;
+      float t0[DH], t1[DH];
+      ldr<DH>(kbase + (int64_t)min(j0, a.Lk - 1) * a.k_ls, t0);
+      ldr<DH>(kbase + (int64_t)min(j1, a.Lk - 1) * a.k_ls, t1);
 #pragma unroll
-    for (int d = 0; d < DH; ++d) {
-      vA[d] = (f2){t[0][d], t[1][d]};
-      vB[d] = (f2){t[2][d], t[3][d]};
-      dkA[d] = bc(0.f); dkB[d] = bc(0.f); dvA[d] = bc(0.f); dvB[d] = bc(0.f);
+      for (int d = 0; d < DH; ++d) k[p][d] = (f2){t0[d], t1[d]};   // the Q tile carries the scale
+      ldr<DH>(vbase + (int64_t)min(j0, a.Lk - 1) * a.v_ls, t0);
+      ldr<DH>(vbase + (int64_t)min(j1, a.Lk - 1) * a.v_ls, t1);
+#pragma unroll
+      for (int d = 0; d < DH; ++d) {
+        v[p][d] = (f2){t0[d], t1[d]};
+        dk[p][d] = bc(0.f);
+        dv[p][d] = bc(0.f);
+      }
+      // key bias: -inf for masked or out-of-range keys -> p = 0
+      kbias[p] = (f2){j0 < a.Lk ? (kbp ? kbp[j0] : 0.f) : -INFINITY,
+                      j1 < a.Lk ? (kbp ? kbp[j1] : 0.f) : -INFINITY};
     }
   }
-  f2 bA, bB;   // key bias (-inf for masked or out-of-range keys -> p = 0)
-  {
-    const float* kbp = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
-    float t[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) t[u] = key0 + u < a.Lk ? (kbp ? kbp[key0 + u] : 0.f) : -INFINITY;
-    bA = (f2){t[0], t[1]};
-    bB = (f2){t[2], t[3]};
-  }
-  const int wl = threadIdx.x >> 3;               // my bitmap word within the block
-  const int sh = (4 * threadIdx.x) & 31;         // my 4 bits within it
+  const int wl = (R * threadIdx.x) >> 5;         // my bitmap word within the block
+  const int sh = (R * threadIdx.x) & 31;         // my first bit within it
   const float* qg = a.q + (int64_t)b * a.q_bs + h * DH;
   const float* dg = a.dout + (int64_t)b * a.do_bs + h * DH;
   const float* og = a.o + (int64_t)b * a.o_bs + h * DH;
   const float* lg = a.lse + (int64_t)bh * a.Lq;
   const uint32_t* bitp = DROP ? a.bits + (int64_t)bh * a.nw * a.Lq : nullptr;
-  const int wfirst = kb * NWB;
+  const int wfirst = (kb * KB) >> 5;
+  const f2 ik = bc(a.inv_keep);
   for (int qt = 0; qt < a.Lq; qt += TK) {
     __syncthreads();
     stage<DH, NTT>(Qs, qg, a.q_ls, qt, a.Lq, a.scale_log2);
@@ -328,103 +337,95 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
       lrow<DH>(Qs + i * DH, qr);
       lrow<DH>(Ds_ + i * DH, dr);
       const f2 li = bc(Ls[i]), Di = bc(Dd[i]);
-      f2 sA = bA, sB = bB, gA = bc(0.f), gB = bc(0.f);
+      const uint32_t kw = DROP ? (Ws[i * NWB + wl] >> sh) : 0xffffffffu;
 #pragma unroll
-      for (int d = 0; d < DH; ++d) {
-        sA = fma2(kA[d], bc(qr[d]), sA);
-        sB = fma2(kB_[d], bc(qr[d]), sB);
-        gA = fma2(vA[d], bc(dr[d]), gA);
-        gB = fma2(vB[d], bc(dr[d]), gB);
-      }
-      const f2 pA = ex2(sA - li), pB = ex2(sB - li);
-      f2 aA = pA, aB = pB, dPA = gA, dPB = gB;
-      if (DROP) {
-        const uint32_t kw = Ws[i * NWB + wl] >> sh;
-        const f2 ik = bc(a.inv_keep);
-        aA = sel2(kw & 1u, kw & 2u, pA * ik);
-        aB = sel2(kw & 4u, kw & 8u, pB * ik);
-        dPA = sel2(kw & 1u, kw & 2u, gA * ik);
-        dPB = sel2(kw & 4u, kw & 8u, gB * ik);
-      }
-      const f2 dSA = pA * (dPA - Di), dSB = pB * (dPB - Di);
+      for (int p = 0; p < NP; ++p) {
+        f2 s = kbias[p], g = bc(0.f);
 #pragma unroll
-      for (int d = 0; d < DH; ++d) {
-        dvA[d] = fma2(aA, bc(dr[d]), dvA[d]);
-        dvB[d] = fma2(aB, bc(dr[d]), dvB[d]);
-        dkA[d] = fma2(dSA, bc(qr[d]), dkA[d]);
-        dkB[d] = fma2(dSB, bc(qr[d]), dkB[d]);
+        for (int d = 0; d < DH; ++d) {
+          s = fma2(k[p][d], bc(qr[d]), s);
+          g = fma2(v[p][d], bc(dr[d]), g);
+        }
+        const f2 pr = ex2(s - li);
+        f2 aP = pr, dP = g;
+        if (DROP) {
+          const uint32_t m0 = (kw >> (2 * p)) & 1u, m1 = (kw >> (2 * p + 1)) & 1u;
+          aP = sel2(m0, m1, pr * ik);
+          dP = sel2(m0, m1, g * ik);
+        }
+        const f2 dS = pr * (dP - Di);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+          dv[p][d] = fma2(aP, bc(dr[d]), dv[p][d]);
+          dk[p][d] = fma2(dS, bc(qr[d]), dk[p][d]);
+        }
       }
     }
   }
   // dK = sum_i dS_i q_i * scale = (scale / scale_log2) * sum_i dS_i Qs_i
   const float kf = a.scale / a.scale_log2;
-  float r[4][DH];
 #pragma unroll
-  for (int d = 0; d < DH; ++d) {
-    r[0][d] = dkA[d].x * kf; r[1][d] = dkA[d].y * kf; r[2][d] = dkB[d].x * kf; r[3][d] = dkB[d].y * kf;
+  for (int p = 0; p < NP; ++p) {
+    const int j0 = key0 + 2 * p, j1 = j0 + 1;
+    float r0[DH], r1[DH];
+#pragma unroll
+    for (int d = 0; d < DH; ++d) { r0[d] = dk[p][d].x * kf; r1[d] = dk[p][d].y * kf; }
+    if (j0 < a.Lk) str<DH>(a.dk + (int64_t)b * a.dk_bs + (int64_t)j0 * a.dk_ls + h * DH, r0);
+    if (j1 < a.Lk) str<DH>(a.dk + (int64_t)b * a.dk_bs + (int64_t)j1 * a.dk_ls + h * DH, r1);
+#pragma unroll
+    for (int d = 0; d < DH; ++d) { r0[d] = dv[p][d].x; r1[d] = dv[p][d].y; }
+    if (j0 < a.Lk) str<DH>(a.dv + (int64_t)b * a.dv_bs + (int64_t)j0 * a.dv_ls + h * DH, r0);
+    if (j1 < a.Lk) str<DH>(a.dv + (int64_t)b * a.dv_bs + (int64_t)j1 * a.dv_ls + h * DH, r1);
   }
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-    if (key0 + u < a.Lk) str<DH>(a.dk + (int64_t)b * a.dk_bs + (int64_t)(key0 + u) * a.dk_ls + h * DH, r[u]);
-#pragma unroll
-  for (int d = 0; d < DH; ++d) {
-    r[0][d] = dvA[d].x; r[1][d] = dvA[d].y; r[2][d] = dvB[d].x; r[3][d] = dvB[d].y;
-  }
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-    if (key0 + u < a.Lk) str<DH>(a.dv + (int64_t)b * a.dv_bs + (int64_t)(key0 + u) * a.dv_ls + h * DH, r[u]);
 }
 
 // ================================ dQ =======================================
-template <int DH, int NTT, bool DROP>
+template <int DH, int NTT, int NP, bool DROP>
 __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Ks[TK * DH];
   __shared__ __attribute__((aligned(16))) float Vs[TK * DH];
   __shared__ float Kb[TK];
-  constexpr int QB = 4 * NTT;
+  constexpr int R = 2 * NP;
+  constexpr int QB = R * NTT;
   const int nqb = (a.Lq + QB - 1) / QB;
   const int qb = blockIdx.x % nqb;
   const int bh = blockIdx.x / nqb;
   const int b = bh / a.H, h = bh - b * a.H;
-  int qi[4], qc[4];
+  int qi[R], qc[R];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < R; ++u) {
     qi[u] = qb * QB + u * NTT + threadIdx.x;
     qc[u] = min(qi[u], a.Lq - 1);
   }
-  f2 qA[DH], qB[DH], gA_[DH], gB_[DH], dqA[DH], dqB[DH];
-  f2 DA, DB, lA, lB;
+  f2 q[NP][DH], g[NP][DH], dq[NP][DH], D[NP], lse[NP];
   {
-    float t[4][DH], o4[4][DH];
     const float* qbase = a.q + (int64_t)b * a.q_bs + h * DH;
     const float* dbase = a.dout + (int64_t)b * a.do_bs + h * DH;
     const float* obase = a.o + (int64_t)b * a.o_bs + h * DH;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) ldr<DH>(qbase + (int64_t)qc[u] * a.q_ls, t[u]);
-#pragma unroll
-    for (int d = 0; d < DH; ++d) {
-      qA[d] = (f2){t[0][d], t[1][d]} * a.scale_log2;
-      qB[d] = (f2){t[2][d], t[3][d]} * a.scale_log2;
-      dqA[d] = bc(0.f); dqB[d] = bc(0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      ldr<DH>(dbase + (int64_t)qc[u] * a.do_ls, t[u]);
-      ldr<DH>(obase + (int64_t)qc[u] * a.o_ls, o4[u]);
-    }
-    float Dv[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int d = 0; d < DH; ++d) {
-      gA_[d] = (f2){t[0][d], t[1][d]};
-      gB_[d] = (f2){t[2][d], t[3][d]};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) Dv[u] = fmaf(t[u][d], o4[u][d], Dv[u]);
-    }
-    DA = (f2){Dv[0], Dv[1]};
-    DB = (f2){Dv[2], Dv[3]};
     const float* lp = a.lse + (int64_t)bh * a.Lq;
-    lA = (f2){lp[qc[0]], lp[qc[1]]};
-    lB = (f2){lp[qc[2]], lp[qc[3]]};
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      float t0[DH], t1[DH], o0[DH], o1[DH];
+      ldr<DH>(qbase + (int64_t)qc[2 * p] * a.q_ls, t0);
+      ldr<DH>(qbase + (int64_t)qc[2 * p + 1] * a.q_ls, t1);
+#pragma unroll
+      for (int d = 0; d < DH; ++d) {
+        q[p][d] = (f2){t0[d], t1[d]} * a.scale_log2;
+        dq[p][d] = bc(0.f);
+      }
+      ldr<DH>(dbase + (int64_t)qc[2 * p] * a.do_ls, t0);
+      ldr<DH>(dbase + (int64_t)qc[2 * p + 1] * a.do_ls, t1);
+      ldr<DH>(obase + (int64_t)qc[2 * p] * a.o_ls, o0);
+      ldr<DH>(obase + (int64_t)qc[2 * p + 1] * a.o_ls, o1);
+      f2 Dp = bc(0.f);
+#pragma unroll
+      for (int d = 0; d < DH; ++d) {
+        g[p][d] = (f2){t0[d], t1[d]};
+        Dp = fma2(g[p][d], (f2){o0[d], o1[d]}, Dp);
+      }
+      D[p] = Dp;
+      lse[p] = (f2){lp[qc[2 * p]], lp[qc[2 * p + 1]]};
+    }
   }
   const float* kg = a.k + (int64_t)b * a.k_bs + h * DH;
   const float* vg = a.v + (int64_t)b * a.v_bs + h * DH;
@@ -439,49 +440,270 @@ __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
       Kb[i] = kt + i < a.Lk ? (kbg ? kbg[kt + i] : 0.f) : -INFINITY;
     __syncthreads();
     const int kend = min(TK, a.Lk - kt);
-    uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+    uint32_t w[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) w[u] = 0xffffffffu;
     for (int j = 0; j < kend; ++j) {
       if (DROP && (j & 31) == 0) {
         const int word = (kt + j) >> 5;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) w[u] = bitp[(int64_t)word * a.Lq + qc[u]];
+        for (int u = 0; u < R; ++u) w[u] = bitp[(int64_t)word * a.Lq + qc[u]];
       }
       float kr[DH], vr[DH];
       lrow<DH>(Ks + j * DH, kr);
       lrow<DH>(Vs + j * DH, vr);
       const float kb = Kb[j];
-      f2 sA = bc(kb), sB = bc(kb), tA = bc(0.f), tB = bc(0.f);
+      const int s = j & 31;
 #pragma unroll
-      for (int d = 0; d < DH; ++d) {
-        sA = fma2(qA[d], bc(kr[d]), sA);
-        sB = fma2(qB[d], bc(kr[d]), sB);
-        tA = fma2(gA_[d], bc(vr[d]), tA);
-        tB = fma2(gB_[d], bc(vr[d]), tB);
-      }
-      const f2 pA = ex2(sA - lA), pB = ex2(sB - lB);
-      f2 dPA = tA * ik, dPB = tB * ik;
-      if (DROP) {
-        const int s = j & 31;
-        dPA = sel2((w[0] >> s) & 1u, (w[1] >> s) & 1u, dPA);
-        dPB = sel2((w[2] >> s) & 1u, (w[3] >> s) & 1u, dPB);
-      }
-      const f2 dSA = pA * (dPA - DA), dSB = pB * (dPB - DB);
+      for (int p = 0; p < NP; ++p) {
+        f2 sc = bc(kb), t = bc(0.f);
 #pragma unroll
-      for (int d = 0; d < DH; ++d) {
-        dqA[d] = fma2(dSA, bc(kr[d]), dqA[d]);
-        dqB[d] = fma2(dSB, bc(kr[d]), dqB[d]);
+        for (int d = 0; d < DH; ++d) {
+          sc = fma2(q[p][d], bc(kr[d]), sc);
+          t = fma2(g[p][d], bc(vr[d]), t);
+        }
+        const f2 pr = ex2(sc - lse[p]);
+        f2 dP = t * ik;
+        if (DROP) dP = sel2((w[2 * p] >> s) & 1u, (w[2 * p + 1] >> s) & 1u, dP);
+        const f2 dS = pr * (dP - D[p]);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) dq[p][d] = fma2(dS, bc(kr[d]), dq[p][d]);
       }
     }
   }
-  float r[4][DH];
 #pragma unroll
-  for (int d = 0; d < DH; ++d) {
-    r[0][d] = dqA[d].x * a.scale; r[1][d] = dqA[d].y * a.scale;
-    r[2][d] = dqB[d].x * a.scale; r[3][d] = dqB[d].y * a.scale;
+  for (int p = 0; p < NP; ++p) {
+    float r0[DH], r1[DH];
+#pragma unroll
+    for (int d = 0; d < DH; ++d) { r0[d] = dq[p][d].x * a.scale; r1[d] = dq[p][d].y * a.scale; }
+    const int i0 = qi[2 * p], i1 = qi[2 * p + 1];
+    if (i0 < a.Lq) str<DH>(a.dq + (int64_t)b * a.dq_bs + (int64_t)i0 * a.dq_ls + h * DH, r0);
+    if (i1 < a.Lq) str<DH>(a.dq + (int64_t)b * a.dq_bs + (int64_t)i1 * a.dq_ls + h * DH, r1);
   }
+}
+
+// ======================= few queries (Lq <= 16) ===========================
+// The encoders' latent queries (2*latent_len = 8 rows) attend to the whole
+// light curve / spectrum (60 / 983 keys).  Query-parallel tiling leaves 56 of
+// 64 lanes idle there, so these kernels go key-parallel: one 256-thread
+// workgroup per (b, h, group of SQ=8 queries), each thread owns keys
+// j = tid, tid+256, ..., the softmax max / sum and the output rows are block
+// reductions.  Backward is ONE kernel per (b, h): dK_j / dV_j are thread-local
+// sums over the (<= 16) queries, dQ a block reduction.  Dropout decisions are
+// re-derived from the same counter hash (attn_pair_bits) in both directions,
+// so no bitmap is written.
+constexpr int SNT = 256, SNW = SNT / 64, SQ = 8;
+
+// sum (or max) of v[0..N) over the workgroup; result in out[0..N) (LDS)
+template <int N, bool MAX>
+__device__ __forceinline__ void block_reduce(float (&v)[N], float* red, float* out) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
-    if (qi[u] < a.Lq) str<DH>(a.dq + (int64_t)b * a.dq_bs + (int64_t)qi[u] * a.dq_ls + h * DH, r[u]);
+  for (int i = 0; i < N; ++i) {
+    float x = v[i];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float y = __shfl_xor(x, off, 64);
+      x = MAX ? fmaxf(x, y) : x + y;
+    }
+    if (lane == 0) red[w * N + i] = x;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < N; i += SNT) {
+    float x = red[i];
+#pragma unroll
+    for (int ww = 1; ww < SNW; ++ww) x = MAX ? fmaxf(x, red[ww * N + i]) : x + red[ww * N + i];
+    out[i] = x;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ bool keep_of(uint32_t rk, int j, uint32_t thr) {
+  const uint32_t bits = attn_pair_bits(rk, (uint32_t)(j >> 1));
+  return ((j & 1) ? (bits >> 16) : (bits & 0xffffu)) >= thr;
+}
+
+template <int DH, bool DROP>
+__global__ __launch_bounds__(SNT) void attn_fwd_smallq_kernel(AttnArgs a) {
+  constexpr int NV = SQ * (DH + 1);
+  __shared__ float qs[SQ * DH];
+  __shared__ float red[SNW * NV];
+  __shared__ float res[NV];
+  const int bh = blockIdx.x, b = bh / a.H, h = bh - b * a.H;
+  const int q0 = blockIdx.y * SQ;
+  const int nq = min(SQ, a.Lq - q0);
+  if (threadIdx.x < SQ * DH) {
+    const int i = threadIdx.x / DH, d = threadIdx.x - i * DH;
+    qs[threadIdx.x] = i < nq ? a.q[(int64_t)b * a.q_bs + (int64_t)(q0 + i) * a.q_ls + h * DH + d] * a.scale_log2 : 0.f;
+  }
+  __syncthreads();
+  float q[SQ][DH];
+#pragma unroll
+  for (int i = 0; i < SQ; ++i) lrow<DH>(qs + i * DH, q[i]);
+  uint32_t rk[SQ];
+  if (DROP) {
+    const uint32_t skey = key_of(a.rng_state, a.call_id);
+#pragma unroll
+    for (int i = 0; i < SQ; ++i)
+      rk[i] = attn_row_key(skey, (uint32_t)((int64_t)bh * a.Lq + q0 + min(i, nq - 1)));
+  }
+  const float* kg = a.k + (int64_t)b * a.k_bs + h * DH;
+  const float* vg = a.v + (int64_t)b * a.v_bs + h * DH;
+  const float* kbg = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
+  // pass 1: row maxima
+  float m[SQ];
+#pragma unroll
+  for (int i = 0; i < SQ; ++i) m[i] = -INFINITY;
+  for (int j = threadIdx.x; j < a.Lk; j += SNT) {
+    float kr[DH];
+    ldr<DH>(kg + (int64_t)j * a.k_ls, kr);
+    const float kb = kbg ? kbg[j] : 0.f;
+#pragma unroll
+    for (int i = 0; i < SQ; ++i) {
+      float sc = kb;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) sc = fmaf(q[i][d], kr[d], sc);
+      m[i] = fmaxf(m[i], sc);
+    }
+  }
+  block_reduce<SQ, true>(m, red, res);
+  float mu[SQ];
+#pragma unroll
+  for (int i = 0; i < SQ; ++i) {
+    m[i] = res[i];
+    mu[i] = m[i] == -INFINITY ? 0.f : m[i];    // fully masked row -> l = 0 -> NaN output
+  }
+  __syncthreads();
+  // pass 2: l (undropped) and o (dropped) partial sums
+  float acc[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) acc[i] = 0.f;
+  for (int j = threadIdx.x; j < a.Lk; j += SNT) {
+    float kr[DH], vr[DH];
+    ldr<DH>(kg + (int64_t)j * a.k_ls, kr);
+    ldr<DH>(vg + (int64_t)j * a.v_ls, vr);
+    const float kb = kbg ? kbg[j] : 0.f;
+#pragma unroll
+    for (int i = 0; i < SQ; ++i) {
+      float sc = kb;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) sc = fmaf(q[i][d], kr[d], sc);
+      float p = ex2(sc - mu[i]);
+      acc[i] += p;
+      if (DROP && !keep_of(rk[i], j, a.thr)) p = 0.f;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) acc[SQ + i * DH + d] = fmaf(p, vr[d], acc[SQ + i * DH + d]);
+    }
+  }
+  block_reduce<NV, false>(acc, red, res);
+  const float ik = DROP ? a.inv_keep : 1.f;
+  if (threadIdx.x < nq * DH) {
+    const int i = threadIdx.x / DH, d = threadIdx.x - i * DH;
+    a.o_out[(int64_t)b * a.o_bs + (int64_t)(q0 + i) * a.o_ls + h * DH + d] = res[SQ + threadIdx.x] * ik / res[i];
+  }
+  if (threadIdx.x < nq) {
+    const int i = threadIdx.x;
+    a.lse[(int64_t)bh * a.Lq + q0 + i] = m[i] + __log2f(res[i]);
+  }
+}
+
+template <int DH, bool DROP>
+__global__ __launch_bounds__(SNT) void attn_bwd_smallq_kernel(AttnArgs a) {
+  constexpr int SQ = 64 / DH;   // query group: dQ partials SQ*DH = 64 registers
+  __shared__ float qs[SQ * DH], gs[SQ * DH], lsh[SQ], Dsh[SQ];
+  __shared__ float red[SNW * SQ * DH];
+  __shared__ float res[SQ * DH];
+  const int bh = blockIdx.x, b = bh / a.H, h = bh - b * a.H;
+  const float* kg = a.k + (int64_t)b * a.k_bs + h * DH;
+  const float* vg = a.v + (int64_t)b * a.v_bs + h * DH;
+  const float* kbg = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
+  const float ik = DROP ? a.inv_keep : 1.f;
+  const float kf = a.scale / a.scale_log2;
+  const uint32_t skey = DROP ? key_of(a.rng_state, a.call_id) : 0u;
+  for (int q0 = 0; q0 < a.Lq; q0 += SQ) {
+    const int nq = min(SQ, a.Lq - q0);
+    __syncthreads();
+    if (threadIdx.x < SQ * DH) {
+      const int i = threadIdx.x / DH, d = threadIdx.x - i * DH;
+      const int64_t r = q0 + i;
+      qs[threadIdx.x] = i < nq ? a.q[(int64_t)b * a.q_bs + r * a.q_ls + h * DH + d] * a.scale_log2 : 0.f;
+      gs[threadIdx.x] = i < nq ? a.dout[(int64_t)b * a.do_bs + r * a.do_ls + h * DH + d] : 0.f;
+    }
+    if (threadIdx.x < SQ) {
+      const int i = threadIdx.x;
+      float D = 0.f, l = INFINITY;    // padding rows: p = 0
+      if (i < nq) {
+        float x[DH], y[DH];
+        ldr<DH>(a.dout + (int64_t)b * a.do_bs + (int64_t)(q0 + i) * a.do_ls + h * DH, x);
+        ldr<DH>(a.o + (int64_t)b * a.o_bs + (int64_t)(q0 + i) * a.o_ls + h * DH, y);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) D = fmaf(x[d], y[d], D);
+        l = a.lse[(int64_t)bh * a.Lq + q0 + i];
+      }
+      Dsh[i] = D;
+      lsh[i] = l;
+    }
+    __syncthreads();
+    // q / dO rows are re-read per key as LDS broadcasts (keeps dh=16 in registers)
+    float dq[SQ * DH], lse[SQ], D[SQ];
+    uint32_t rk[SQ];
+#pragma unroll
+    for (int i = 0; i < SQ; ++i) {
+      lse[i] = lsh[i];
+      D[i] = Dsh[i];
+      if (DROP) rk[i] = attn_row_key(skey, (uint32_t)((int64_t)bh * a.Lq + q0 + min(i, nq - 1)));
+    }
+#pragma unroll
+    for (int i = 0; i < SQ * DH; ++i) dq[i] = 0.f;
+    for (int j = threadIdx.x; j < a.Lk; j += SNT) {
+      float kr[DH], vr[DH], dk[DH], dv[DH];
+      ldr<DH>(kg + (int64_t)j * a.k_ls, kr);
+      ldr<DH>(vg + (int64_t)j * a.v_ls, vr);
+      const float kb = kbg ? kbg[j] : 0.f;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
+#pragma unroll
+      for (int i = 0; i < SQ; ++i) {
+        float qi[DH], gi[DH];
+        lrow<DH>(qs + i * DH, qi);
+        lrow<DH>(gs + i * DH, gi);
+        float sc = kb, dp = 0.f;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+          sc = fmaf(qi[d], kr[d], sc);
+          dp = fmaf(gi[d], vr[d], dp);
+        }
+        const float p = ex2(sc - lse[i]);
+        float aP = p * ik, dP = dp * ik;
+        if (DROP && !keep_of(rk[i], j, a.thr)) { aP = 0.f; dP = 0.f; }
+        const float dS = p * (dP - D[i]);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+          dv[d] = fmaf(aP, gi[d], dv[d]);
+          dk[d] = fmaf(dS, qi[d], dk[d]);
+          dq[i * DH + d] = fmaf(dS, kr[d], dq[i * DH + d]);
+        }
+      }
+      float* dkp = a.dk + (int64_t)b * a.dk_bs + (int64_t)j * a.dk_ls + h * DH;
+      float* dvp = a.dv + (int64_t)b * a.dv_bs + (int64_t)j * a.dv_ls + h * DH;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) dk[d] *= kf;
+      if (q0 > 0) {   // this thread owns key j in every query group: plain RMW
+        float ok[DH], ov[DH];
+        ldr<DH>(dkp, ok);
+        ldr<DH>(dvp, ov);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) { dk[d] += ok[d]; dv[d] += ov[d]; }
+      }
+      str<DH>(dkp, dk);
+      str<DH>(dvp, dv);
+    }
+    block_reduce<SQ * DH, false>(dq, red, res);
+    if (threadIdx.x < nq * DH) {
+      const int i = threadIdx.x / DH, d = threadIdx.x - i * DH;
+      a.dq[(int64_t)b * a.dq_bs + (int64_t)(q0 + i) * a.dq_ls + h * DH + d] = res[threadIdx.x] * a.scale;
+    }
+  }
 }
 
 __global__ void mask_bias_kernel(const uint8_t* __restrict__ m, int64_t n, float* __restrict__ out) {
@@ -504,58 +726,99 @@ void fill_common(AttnArgs& a, int B, int H, int Lq, int Lk, int dh, float p_drop
   a.rng_state = rng_state; a.call_id = call_id;
 }
 
-// threads per workgroup: the largest of {256, 128, 64} that still gives
-// >= 1024 workgroups (fill 256 CUs x 4), else 64
-int pick_nt(int64_t bh, int L) {
-  for (int nt = 256; nt > 64; nt >>= 1)
-    if (bh * ((L + 4 * nt - 1) / (4 * nt)) >= 1024) return nt;
-  return 64;
+// Geometry: rows per lane R = 2*NP (NP = 2 amortises each LDS read over four
+// rows) and workgroup size NTT in {256, 128, 64}.  Take the first of
+// (NP=2: 256,128,64; NP=1: 256,128,64) that yields >= 1024 workgroups (4 per
+// CU); the small encoder grids (B*H = 64) fall through to NP=1 / 64 threads.
+struct Geo { int nt, np; };
+Geo pick_geo(int64_t bh, int L) {
+  const int nts[3] = {256, 128, 64};
+  for (int np = 2; np >= 1; --np)
+    for (int i = 0; i < 3; ++i) {
+      const int nt = nts[i];
+      if (bh * ((L + 2 * np * nt - 1) / (2 * np * nt)) >= 1024) return {nt, np};
+    }
+  return {64, 1};
 }
 
-#define VAESNE_NT_SWITCH(NTV, CALL) \
-  switch (NTV) {                    \
-    case 256: { constexpr int NTT = 256; CALL; break; } \
-    case 128: { constexpr int NTT = 128; CALL; break; } \
-    default: { constexpr int NTT = 64; CALL; break; }   \
+#define VAESNE_GEO_SWITCH(G, CALL)                                                     \
+  if (G.np == 2) {                                                                     \
+    constexpr int NP = 2;                                                              \
+    switch (G.nt) {                                                                    \
+      case 256: { constexpr int NTT = 256; CALL; break; }                              \
+      case 128: { constexpr int NTT = 128; CALL; break; }                              \
+      default: { constexpr int NTT = 64; CALL; break; }                                \
+    }                                                                                  \
+  } else {                                                                             \
+    constexpr int NP = 1;                                                              \
+    switch (G.nt) {                                                                    \
+      case 256: { constexpr int NTT = 256; CALL; break; }                              \
+      case 128: { constexpr int NTT = 128; CALL; break; }                              \
+      default: { constexpr int NTT = 64; CALL; break; }                                \
+    }                                                                                  \
   }
 
 template <int DHV>
 int launch_fwd(const AttnArgs& a, float p_drop, hipStream_t s) {
-  const int nt = pick_nt((int64_t)a.B * a.H, a.Lq);
-  VAESNE_NT_SWITCH(nt, {
-    const int nqb = (a.Lq + 4 * NTT - 1) / (4 * NTT);
+  if (a.Lq <= 2 * SQ) {
+    dim3 grid((unsigned)((int64_t)a.B * a.H), (unsigned)((a.Lq + SQ - 1) / SQ));
+    if (p_drop > 0.f)
+      hipLaunchKernelGGL((attn_fwd_smallq_kernel<DHV, true>), grid, dim3(SNT), 0, s, a);
+    else
+      hipLaunchKernelGGL((attn_fwd_smallq_kernel<DHV, false>), grid, dim3(SNT), 0, s, a);
+    VAESNE_CHECK_LAUNCH();
+    return 0;
+  }
+  const Geo g = pick_geo((int64_t)a.B * a.H, a.Lq);
+  VAESNE_GEO_SWITCH(g, {
+    const int nqb = (a.Lq + 2 * NP * NTT - 1) / (2 * NP * NTT);
     dim3 grid((unsigned)((int64_t)a.B * a.H * nqb));
     if (p_drop > 0.f)
-      hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, true>), grid, dim3(NTT), 0, s, a);
+      hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, true>), grid, dim3(NTT), 0, s, a);
     else
-      hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, false>), grid, dim3(NTT), 0, s, a);
+      hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, a);
   })
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
 
+// part: 1 = dK/dV kernel, 2 = dQ kernel, 3 = both (the few-query path is one
+// fused kernel and runs for any nonzero part)
 template <int DHV>
-int launch_bwd(const AttnArgs& a, float p_drop, hipStream_t s) {
-  const int ntk = pick_nt((int64_t)a.B * a.H, a.Lk);
-  VAESNE_NT_SWITCH(ntk, {
-    const int nkb = (a.Lk + 4 * NTT - 1) / (4 * NTT);
-    dim3 g((unsigned)((int64_t)a.B * a.H * nkb));
+int launch_bwd(const AttnArgs& a, float p_drop, int part, hipStream_t s) {
+  if (a.Lq <= 2 * SQ) {
+    dim3 grid((unsigned)((int64_t)a.B * a.H));
     if (p_drop > 0.f)
-      hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, true>), g, dim3(NTT), 0, s, a);
+      hipLaunchKernelGGL((attn_bwd_smallq_kernel<DHV, true>), grid, dim3(SNT), 0, s, a);
     else
-      hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, false>), g, dim3(NTT), 0, s, a);
-  })
-  VAESNE_CHECK_LAUNCH();
-  const int ntq = pick_nt((int64_t)a.B * a.H, a.Lq);
-  VAESNE_NT_SWITCH(ntq, {
-    const int nqb = (a.Lq + 4 * NTT - 1) / (4 * NTT);
-    dim3 g((unsigned)((int64_t)a.B * a.H * nqb));
-    if (p_drop > 0.f)
-      hipLaunchKernelGGL((attn_bwd_q_kernel<DHV, NTT, true>), g, dim3(NTT), 0, s, a);
-    else
-      hipLaunchKernelGGL((attn_bwd_q_kernel<DHV, NTT, false>), g, dim3(NTT), 0, s, a);
-  })
-  VAESNE_CHECK_LAUNCH();
+      hipLaunchKernelGGL((attn_bwd_smallq_kernel<DHV, false>), grid, dim3(SNT), 0, s, a);
+    VAESNE_CHECK_LAUNCH();
+    return 0;
+  }
+  if (part & 1) {
+    const Geo gk = pick_geo((int64_t)a.B * a.H, a.Lk);
+    VAESNE_GEO_SWITCH(gk, {
+      const int nkb = (a.Lk + 2 * NP * NTT - 1) / (2 * NP * NTT);
+      dim3 grid((unsigned)((int64_t)a.B * a.H * nkb));
+      if (p_drop > 0.f)
+        hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, NP, true>), grid, dim3(NTT), 0, s, a);
+      else
+        hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, a);
+    })
+    VAESNE_CHECK_LAUNCH();
+  }
+  if (part & 2) {
+    const Geo gq = pick_geo((int64_t)a.B * a.H, a.Lq);
+    VAESNE_GEO_SWITCH(gq, {
+      const int nqb = (a.Lq + 2 * NP * NTT - 1) / (2 * NP * NTT);
+      dim3 grid((unsigned)((int64_t)a.B * a.H * nqb));
+      if (p_drop > 0.f)
+        hipLaunchKernelGGL((attn_bwd_q_kernel<DHV, NTT, NP, true>), grid, dim3(NTT), 0, s, a);
+      else
+        hipLaunchKernelGGL((attn_bwd_q_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, a);
+    })
+    VAESNE_CHECK_LAUNCH();
+  }
   return 0;
 }
 
@@ -598,17 +861,20 @@ VAESNE_API int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const
   return launch_fwd<16>(a, p_drop, s);
 }
 
-VAESNE_API int vaesne_attn_bwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k,
-                               int64_t k_bs, int64_t k_ls, const float* v, int64_t v_bs,
-                               int64_t v_ls, const float* kbias, int64_t kb_bs, const float* o,
-                               int64_t o_bs, int64_t o_ls, const float* lse, const float* dout,
-                               int64_t do_bs, int64_t do_ls, float* dq, int64_t dq_bs,
-                               int64_t dq_ls, float* dk, int64_t dk_bs, int64_t dk_ls, float* dv,
-                               int64_t dv_bs, int64_t dv_ls, int B, int H, int Lq, int Lk, int dh,
-                               float p_drop, const uint32_t* keep_bits, void* stream) {
+namespace {
+int attn_bwd_impl(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
+                  int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls, const float* kbias,
+                  int64_t kb_bs, const float* o, int64_t o_bs, int64_t o_ls, const float* lse,
+                  const float* dout, int64_t do_bs, int64_t do_ls, float* dq, int64_t dq_bs,
+                  int64_t dq_ls, float* dk, int64_t dk_bs, int64_t dk_ls, float* dv,
+                  int64_t dv_bs, int64_t dv_ls, int B, int H, int Lq, int Lk, int dh,
+                  float p_drop, const int64_t* rng_state, uint32_t call_id,
+                  const uint32_t* keep_bits, int part, void* stream) {
   if (B <= 0 || Lq <= 0) return 0;
   if (Lk <= 0 || (dh != 8 && dh != 16)) return (int)hipErrorInvalidValue;
-  if (p_drop > 0.f && !keep_bits) return (int)hipErrorInvalidValue;
+  // query-tiled kernels read the forward's keep bitmap; the few-query kernel
+  // re-derives the decisions from rng_state / call_id
+  if (p_drop > 0.f && (Lq > 2 * SQ ? !keep_bits : !rng_state)) return (int)hipErrorInvalidValue;
   if (!aligned16(q, q_ls) || !aligned16(k, k_ls) || !aligned16(v, v_ls) || !aligned16(o, o_ls) ||
       !aligned16(dout, do_ls) || !aligned16(dq, dq_ls) || !aligned16(dk, dk_ls) ||
       !aligned16(dv, dv_ls))
@@ -625,8 +891,32 @@ VAESNE_API int vaesne_attn_bwd(const float* q, int64_t q_bs, int64_t q_ls, const
   a.dk = dk; a.dk_bs = dk_bs; a.dk_ls = dk_ls;
   a.dv = dv; a.dv_bs = dv_bs; a.dv_ls = dv_ls;
   a.bits = const_cast<uint32_t*>(keep_bits);
-  fill_common(a, B, H, Lq, Lk, dh, p_drop, nullptr, 0);
+  fill_common(a, B, H, Lq, Lk, dh, p_drop, rng_state, call_id);
   hipStream_t s = (hipStream_t)stream;
-  if (dh == 8) return launch_bwd<8>(a, p_drop, s);
-  return launch_bwd<16>(a, p_drop, s);
+  if (dh == 8) return launch_bwd<8>(a, p_drop, part, s);
+  return launch_bwd<16>(a, p_drop, part, s);
+}
+}  // namespace
+
+#define VAESNE_ATTN_BWD_PARAMS                                                                  \
+  const float *q, int64_t q_bs, int64_t q_ls, const float *k, int64_t k_bs, int64_t k_ls,      \
+      const float *v, int64_t v_bs, int64_t v_ls, const float *kbias, int64_t kb_bs,          \
+      const float *o, int64_t o_bs, int64_t o_ls, const float *lse, const float *dout,        \
+      int64_t do_bs, int64_t do_ls, float *dq, int64_t dq_bs, int64_t dq_ls, float *dk,       \
+      int64_t dk_bs, int64_t dk_ls, float *dv, int64_t dv_bs, int64_t dv_ls, int B, int H,    \
+      int Lq, int Lk, int dh, float p_drop, const int64_t *rng_state, uint32_t call_id,       \
+      const uint32_t *keep_bits
+#define VAESNE_ATTN_BWD_ARGS                                                                    \
+  q, q_bs, q_ls, k, k_bs, k_ls, v, v_bs, v_ls, kbias, kb_bs, o, o_bs, o_ls, lse, dout, do_bs,  \
+      do_ls, dq, dq_bs, dq_ls, dk, dk_bs, dk_ls, dv, dv_bs, dv_ls, B, H, Lq, Lk, dh, p_drop,   \
+      rng_state, call_id, keep_bits
+
+VAESNE_API int vaesne_attn_bwd(VAESNE_ATTN_BWD_PARAMS, void* stream) {
+  return attn_bwd_impl(VAESNE_ATTN_BWD_ARGS, 3, stream);
+}
+VAESNE_API int vaesne_attn_bwd_kv(VAESNE_ATTN_BWD_PARAMS, void* stream) {
+  return attn_bwd_impl(VAESNE_ATTN_BWD_ARGS, 1, stream);
+}
+VAESNE_API int vaesne_attn_bwd_q(VAESNE_ATTN_BWD_PARAMS, void* stream) {
+  return attn_bwd_impl(VAESNE_ATTN_BWD_ARGS, 2, stream);
 }
