@@ -155,8 +155,9 @@ def time_kernel(fn, iters, device):
 
 
 def roofline(device, B):
-    """Spectra-decoder masked self-attention at its step shape (N = K*B
-    sequences x 982 tokens, 4 heads x dh 8, dropout 0.1, 5 % key padding),
+    """Spectra-decoder masked self-attention at its step shape (N = 2*K*B
+    sequences x 982 tokens: the decoder runs once over both modalities'
+    latents; 4 heads x dh 8, dropout 0.1, 5 % key padding),
     the dominant op of the step.  The roofline kernel is
     attn_bwd_kv_kernel, the most expensive single kernel of the step; the
     forward and the dQ kernel are reported beside it.  Algorithmic FLOPs per
@@ -164,7 +165,7 @@ def roofline(device, B):
     (S, dP, dQ) -- the flash backward's recomputation of S counts, as the
     kernels must do it."""
     from VAESNe import _lib, rng
-    N, L, E, H, dh = CFG["K"] * B, CFG["Ls"], CFG["model_dim"], CFG["num_heads"], 8
+    N, L, E, H, dh = 2 * CFG["K"] * B, CFG["Ls"], CFG["model_dim"], CFG["num_heads"], 8
     qkv = torch.randn(N, L, 3 * E, device=device)
     mask = (torch.rand(N, L, device=device) < 0.05)
     mask[:, 0] = False
@@ -207,7 +208,7 @@ def roofline(device, B):
                 detail={k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                             for kk, vv in v.items()} for k, v in res.items()},
                 note="fp32 packed-VALU kernel; peak = FP32 157.3 TF (vector = f32-MFMA rate on "
-                     "gfx950); scores per launch = K*B*H*982^2 = %d" % scores)
+                     "gfx950); scores per launch = 2*K*B*H*982^2 = %d" % scores)
 
 
 def cpu_baseline(sample_B=2, steps=2):

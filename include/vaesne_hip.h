@@ -191,16 +191,20 @@ int vaesne_mask_scale(const uint8_t* mask, int64_t n, int K, float big, float* o
  * Array arguments are HOST arrays of device pointers: x[2] ([B,L_d] flux),
  * llik[2], L[2], loc[4]/scale[4] (index 2r+d, [K,B,L_d]), zs[2] ([K,B,n]),
  * mu[2]/sc[2] ([B,n], the two posteriors), n = latent_len*latent_dim.
- * _bwd takes dL/dlw [2K,B] and writes dloc[4], dzs[2], dmu[2], dsc[2]
- * (null entries are skipped). */
+ * kstride[4] (host, may be null): element stride between consecutive k of
+ * cell 2r+d (null = B*L_d, contiguous cells).  photospecMMVAE decodes both
+ * modalities' latents in ONE decoder call per modality (loc [K, 2B, L_d],
+ * cell (r, d) = batch rows [rB, (r+1)B)): kstride 2B*L_d, loc[2r+d] offset r*B*L_d.
+ * _bwd takes dL/dlw [2K,B] and writes dloc[4] (same strides), dzs[2], dmu[2],
+ * dsc[2] (null entries are skipped). */
 int vaesne_iwae_lw_fwd(const float* const* x, const float* llik, const int* L,
                        const float* const* loc, const float* const* scale,
-                       const float* const* zs, const float* const* mu, const float* const* sc,
+                       const int64_t* kstride, const float* const* zs, const float* const* mu, const float* const* sc,
                        const float* pz_loc, const float* pz_scale, int K, int B, int n,
                        float* lw, void* stream);
 int vaesne_iwae_lw_bwd(const float* const* x, const float* llik, const int* L,
                        const float* const* loc, const float* const* scale,
-                       const float* const* zs, const float* const* mu, const float* const* sc,
+                       const int64_t* kstride, const float* const* zs, const float* const* mu, const float* const* sc,
                        const float* pz_loc, const float* pz_scale, int K, int B, int n,
                        const float* dlw, float* const* dloc, float* const* dzs,
                        float* const* dmu, float* const* dsc, void* stream);

@@ -77,12 +77,17 @@ class PhotometricVAE(VAE):
 
     def forward(self, x, K=1):
         """PhotometricVAE.py:157-176 -> (qz_x, px_z, zs)."""
+        qz_x, zs = self.posterior(x, K)
+        px_z = self.decode(zs, x)
+        return qz_x, px_z, zs
+
+    def posterior(self, x, K=1):
+        """Encoder -> q(z|x) and K reparameterised draws (PhotometricVAE.py:158-163)."""
         flux, time, band, mask = x
         self._qz_x_params = self.enc(flux, time, band, mask)
         qz_x = self._dist(self.qz_x, *self._qz_x_params)
         zs = _ops.laplace_rsample(*self._qz_x_params, K)
-        px_z = self.decode(zs, x)
-        return qz_x, px_z, zs
+        return qz_x, zs
 
     def encode(self, x, mean=True):
         flux, time, band, mask = x
@@ -96,13 +101,18 @@ class PhotometricVAE(VAE):
     def decode(self, zs, x):
         """PhotometricVAE.py:188-199: expand time/band/mask K times, decode,
         wrap in the likelihood distribution [K, B, L]."""
+        return self._dist(self.px_z, *self.decode_params(zs, x))
+
+    def decode_params(self, zs, x, groups=1):
+        """(loc, scale) [K, groups*B, L] for latents zs [K, groups*B, Lz, Dz]
+        decoded at x's grid, x's batch repeated `groups` times (group-major)."""
         _, time, band, mask = x
         K = zs.shape[0]
-        L = time.shape[-1]
-        rep = lambda t: t.unsqueeze(0).expand(K, -1, -1).reshape(-1, L)
+        B, L = time.shape
+        rep = lambda t: t.unsqueeze(0).unsqueeze(0).expand(K, groups, B, L).reshape(-1, L)
         loc, scale = self.dec(rep(time), rep(band), zs.reshape(-1, zs.shape[-2], zs.shape[-1]),
                               None if mask is None else rep(mask))
-        return self._dist(self.px_z, loc.reshape(K, -1, L), scale.reshape(K, -1, L))
+        return loc.reshape(K, groups * B, L), scale.reshape(K, groups * B, L)
 
     def reconstruct(self, x, K=1):
         self.eval()

@@ -75,12 +75,17 @@ class SpectraVAE(VAE):
 
     def forward(self, x, K=1):
         """SpectraVAE.py:148-165 -> (qz_x, px_z, zs)."""
+        qz_x, zs = self.posterior(x, K)
+        px_z = self.decode(zs, x)
+        return qz_x, px_z, zs
+
+    def posterior(self, x, K=1):
+        """Encoder -> q(z|x) and K reparameterised draws (SpectraVAE.py:149-152)."""
         flux, wavelength, phase, mask = x
         self._qz_x_params = self.enc(flux, wavelength, phase, mask)
         qz_x = self._dist(self.qz_x, *self._qz_x_params)
         zs = _ops.laplace_rsample(*self._qz_x_params, K)
-        px_z = self.decode(zs, x)
-        return qz_x, px_z, zs
+        return qz_x, zs
 
     def reconstruct(self, x, K=1):
         self.eval()
@@ -100,14 +105,20 @@ class SpectraVAE(VAE):
 
     def decode(self, zs, x):
         """SpectraVAE.py:186-196."""
+        return self._dist(self.px_z, *self.decode_params(zs, x))
+
+    def decode_params(self, zs, x, groups=1):
+        """(loc, scale) [K, groups*B, L] for latents zs [K, groups*B, Lz, Dz]
+        decoded at x's grid, x's batch repeated `groups` times (group-major)."""
         _, wavelength, phase, mask = x
         K = zs.shape[0]
-        L = wavelength.shape[-1]
-        rep = lambda t: t.unsqueeze(0).expand(K, -1, -1).reshape(-1, L)
-        loc, scale = self.dec(rep(wavelength), phase.unsqueeze(0).expand(K, -1).reshape(-1),
+        B, L = wavelength.shape
+        rep = lambda t: t.unsqueeze(0).unsqueeze(0).expand(K, groups, B, L).reshape(-1, L)
+        loc, scale = self.dec(rep(wavelength),
+                              phase.unsqueeze(0).unsqueeze(0).expand(K, groups, B).reshape(-1),
                               zs.reshape(-1, zs.shape[-2], zs.shape[-1]),
                               None if mask is None else rep(mask))
-        return self._dist(self.px_z, loc.reshape(K, -1, L), scale.reshape(K, -1, L))
+        return loc.reshape(K, groups * B, L), scale.reshape(K, groups * B, L)
 
     def generate(self, N, x):
         """SpectraVAE.py:198-206: N prior draws decoded at x's grids."""

@@ -63,10 +63,10 @@ SIGNATURES = {
     "vaesne_rsample_fwd": (I32, [P, P, P, I32, I64, P, P]),
     "vaesne_rsample_bwd": (I32, [P, P, I32, I64, P, P, P]),
     "vaesne_mask_scale": (I32, [P, I64, I32, F32, P, P]),
-    "vaesne_iwae_lw_fwd": (I32, [PP, C.POINTER(F32), C.POINTER(I32), PP, PP, PP, PP, PP, P, P,
-                                 I32, I32, I32, P, P]),
-    "vaesne_iwae_lw_bwd": (I32, [PP, C.POINTER(F32), C.POINTER(I32), PP, PP, PP, PP, PP, P, P,
-                                 I32, I32, I32, P, PP, PP, PP, PP, P]),
+    "vaesne_iwae_lw_fwd": (I32, [PP, C.POINTER(F32), C.POINTER(I32), PP, PP, C.POINTER(I64), PP,
+                                 PP, PP, P, P, I32, I32, I32, P, P]),
+    "vaesne_iwae_lw_bwd": (I32, [PP, C.POINTER(F32), C.POINTER(I32), PP, PP, C.POINTER(I64), PP,
+                                 PP, PP, P, P, I32, I32, I32, P, PP, PP, PP, PP, P]),
     "vaesne_lme_sum_fwd": (I32, [P, I32, I32, P, P]),
     "vaesne_lme_sum_bwd": (I32, [P, I32, I32, P, P, P]),
     "vaesne_elbo_fwd": (I32, [P, I32, F32, P, P, P, P, P, P, I32, I32, I32, P, P, P]),

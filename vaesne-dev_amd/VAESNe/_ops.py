@@ -451,7 +451,7 @@ class IwaeLwFn(torch.autograd.Function):
         K, B, n, llik, L = meta
         x0, x1, l00, l01, l10, l11, s00, s01, s10, s11, z0, z1, mu0, sc0, mu1, sc1 = ts[:16]
         return (_lib.ptr_array([x0, x1]), (C.c_float * 2)(*llik), (C.c_int * 2)(*L),
-                _lib.ptr_array([l00, l01, l10, l11]), _lib.ptr_array([s00, s01, s10, s11]),
+                _lib.ptr_array([l00, l01, l10, l11]), _lib.ptr_array([s00, s01, s10, s11]), None,
                 _lib.ptr_array([z0, z1]), _lib.ptr_array([mu0, mu1]), _lib.ptr_array([sc0, sc1]))
 
     @staticmethod
@@ -472,6 +472,67 @@ class IwaeLwFn(torch.autograd.Function):
                         _lib.ptr_array(dsc), stream())
         return (None, None, None, *dloc, None, None, None, None, dz[0], dz[1], dmu[0], dsc[0],
                 dmu[1], dsc[1], None, None)
+
+
+class IwaeLwMergedFn(torch.autograd.Function):
+    """_m_iwae's lw [2K, B] when photospecMMVAE decoded both modalities' latents
+    in one call per decoder: loc_d / scale_d [K, 2B, L_d] hold cell (r, d) in
+    batch rows [rB, (r+1)B) (kstride 2B*L_d), and the backward writes dloc_d
+    whole (both halves), so no slice-gradient scatter is needed."""
+
+    @staticmethod
+    def forward(ctx, x0, x1, llik, loc0, loc1, scl0, scl1, z0, z1, mu0, sc0, mu1, sc1, pzl, pzs):
+        ts = [x0, x1, loc0, loc1, scl0, scl1, z0, z1, mu0, sc0, mu1, sc1, pzl, pzs]
+        _lib.require_device(*ts)
+        ts = [t.contiguous() for t in ts]
+        x0, x1, loc0, loc1, scl0, scl1, z0, z1, mu0, sc0, mu1, sc1, pzl, pzs = ts
+        K, B2 = loc0.shape[0], loc0.shape[1]
+        B = B2 // 2
+        if B2 != 2 * B or loc1.shape[:2] != loc0.shape[:2] or z0.shape[1] != B:
+            raise RuntimeError("IwaeLwMergedFn: loc_d must be [K, 2B, L_d]")
+        n = mu0[0].numel()
+        lw = torch.empty((2 * K, B), dtype=torch.float32, device=x0.device)
+        ctx.meta = (K, B, n, [float(v) for v in llik], [x0.shape[-1], x1.shape[-1]])
+        lib.iwae_lw_fwd(*IwaeLwMergedFn._arrays(ctx.meta, ts), pzl.data_ptr(), pzs.data_ptr(), K,
+                        B, n, lw.data_ptr(), stream())
+        ctx.save_for_backward(*ts)
+        return lw
+
+    @staticmethod
+    def _cells(meta, t0, t1):
+        """pointer array of the 4 cells (index 2r+d) inside the per-decoder tensors."""
+        K, B, n, llik, L = meta
+        arr = (C.c_void_p * 4)()
+        for r in range(2):
+            for d, t in enumerate((t0, t1)):
+                arr[2 * r + d] = None if t is None else t.data_ptr() + 4 * r * B * L[d]
+        return arr
+
+    @staticmethod
+    def _arrays(meta, ts):
+        K, B, n, llik, L = meta
+        x0, x1, loc0, loc1, scl0, scl1, z0, z1, mu0, sc0, mu1, sc1 = ts[:12]
+        ks = (C.c_int64 * 4)(2 * B * L[0], 2 * B * L[1], 2 * B * L[0], 2 * B * L[1])
+        return (_lib.ptr_array([x0, x1]), (C.c_float * 2)(*llik), (C.c_int * 2)(*L),
+                IwaeLwMergedFn._cells(meta, loc0, loc1), IwaeLwMergedFn._cells(meta, scl0, scl1), ks,
+                _lib.ptr_array([z0, z1]), _lib.ptr_array([mu0, mu1]), _lib.ptr_array([sc0, sc1]))
+
+    @staticmethod
+    def backward(ctx, dlw):
+        ts = ctx.saved_tensors
+        dlw = dlw.contiguous()
+        ng = ctx.needs_input_grad
+        K, B, n, llik, L = ctx.meta
+        # input index: 3, 4 loc_d; 7, 8 zs; 9..12 mu0 sc0 mu1 sc1
+        dl = [torch.empty_like(ts[2 + d]) if ng[3 + d] else None for d in range(2)]
+        dz = [torch.empty_like(ts[6 + i]) if ng[7 + i] else None for i in range(2)]
+        dmu = [torch.empty_like(ts[8]) if ng[9] else None, torch.empty_like(ts[10]) if ng[11] else None]
+        dsc = [torch.empty_like(ts[9]) if ng[10] else None, torch.empty_like(ts[11]) if ng[12] else None]
+        lib.iwae_lw_bwd(*IwaeLwMergedFn._arrays(ctx.meta, ts), ts[12].data_ptr(), ts[13].data_ptr(),
+                        K, B, n, dlw.data_ptr(), IwaeLwMergedFn._cells(ctx.meta, dl[0], dl[1]),
+                        _lib.ptr_array(dz), _lib.ptr_array(dmu), _lib.ptr_array(dsc), stream())
+        return (None, None, None, dl[0], dl[1], None, None, dz[0], dz[1], dmu[0], dsc[0], dmu[1],
+                dsc[1], None, None)
 
 
 class LmeSumFn(torch.autograd.Function):

@@ -43,12 +43,33 @@ def _m_iwae(model, x, K=1):
     qz_xs, px_zs, zss = model(x, K)
     pz_loc, pz_scale = _pz(model)
     llik = [float(model.vaes[0].llik_scaling), float(model.vaes[1].llik_scaling)]
+    merged = getattr(px_zs, "merged", None)
+    if merged and _cells_are_views(px_zs, merged):
+        (l0, s0), (l1, s1) = merged
+        return _ops.IwaeLwMergedFn.apply(
+            x[0][0], x[1][0], llik, l0, l1, s0, s1, zss[0], zss[1],
+            qz_xs[0].loc, qz_xs[0].scale, qz_xs[1].loc, qz_xs[1].scale, pz_loc, pz_scale)
     return _ops.IwaeLwFn.apply(
         x[0][0], x[1][0], llik,
         px_zs[0][0].loc, px_zs[0][1].loc, px_zs[1][0].loc, px_zs[1][1].loc,
         px_zs[0][0].scale, px_zs[0][1].scale, px_zs[1][0].scale, px_zs[1][1].scale,
         zss[0], zss[1], qz_xs[0].loc, qz_xs[0].scale, qz_xs[1].loc, qz_xs[1].scale,
         pz_loc, pz_scale)
+
+
+def _cells_are_views(px_zs, merged):
+    """True iff every cell px_zs[e][d] still is the batch slice [eB, (e+1)B)
+    of decoder d's merged (loc, scale) (a caller may have replaced cells)."""
+    for d, (loc, scale) in enumerate(merged):
+        B = loc.shape[1] // 2
+        for e in range(2):
+            c = px_zs[e][d]
+            for t, full in ((c.loc, loc), (c.scale, scale)):
+                if (t.data_ptr() != full.data_ptr() + e * B * full.stride(1) * full.element_size()
+                        or t.shape != (full.shape[0], B, full.shape[2])
+                        or t.stride() != full.stride()):
+                    return False
+    return True
 
 
 def is_multidata(dataB):

@@ -7,6 +7,15 @@ import torch.nn as nn
 from . import _ops
 
 
+class _CellMatrix(list):
+    """The 2x2 px_zs list of lists; `merged` holds the per-decoder (loc, scale)
+    [K, 2B, L_d] tensors its cells are views of (empty if decoded per cell)."""
+
+    def __init__(self, rows):
+        super().__init__(rows)
+        self.merged = []
+
+
 class photospecMMVAE(nn.Module):
     def __init__(self, vaes, prior_dist=dist.Laplace, beta=1., length_ratio=982 / 60):
         super().__init__()
@@ -27,18 +36,35 @@ class photospecMMVAE(nn.Module):
         return self._pz_params
 
     def forward(self, x, K=1):
-        """mmVAE.py:91-106: diagonal cells from each VAE's forward, off-diagonal
-        px_zs[e][d] = vaes[d].decode(zs_e, x[d])."""
+        """mmVAE.py:91-106: px_zs[e][d] = vaes[d].decode(zs_e, x[d]) for every
+        (encoder e, decoder d) pair; the diagonal is each VAE's own forward.
+
+        The posteriors are drawn in the reference's order (photometry first,
+        so injected / seeded noise lines up).  Then each decoder runs ONCE over
+        both modalities' latents, batch-concatenated ([K, 2B]): per-sample the
+        arithmetic is the reference's, and the step launches every decoder
+        kernel once instead of twice (and needs no gradient sums over two
+        decoder calls).  px_zs cells are views of those [K, 2B, L] tensors;
+        `px_zs.merged` lets the fused m_iwae read them in place."""
+        n = len(self.vaes)
         qz_xs, zss = [], []
-        px_zs = [[None for _ in range(len(self.vaes))] for _ in range(len(self.vaes))]
         for m, vae in enumerate(self.vaes):
-            qz_x, px_z, zs = vae(x[m], K=K)
+            qz_x, zs = vae.posterior(x[m], K=K)
             qz_xs.append(qz_x)
             zss.append(zs)
-            px_zs[m][m] = px_z
-        for e, zs in enumerate(zss):
+        px_zs = _CellMatrix([[None for _ in range(n)] for _ in range(n)])
+        if all(z.shape == zss[0].shape for z in zss):
+            B = zss[0].shape[1]
+            zcat = torch.cat(zss, dim=1)
             for d, vae in enumerate(self.vaes):
-                if e != d:
+                loc, scale = vae.decode_params(zcat, x[d], groups=n)
+                px_zs.merged.append((loc, scale))
+                for e in range(n):
+                    px_zs[e][d] = vae._dist(vae.px_z, loc[:, e * B:(e + 1) * B],
+                                            scale[:, e * B:(e + 1) * B])
+        else:   # latent shapes differ per modality: one decoder call per cell
+            for e, zs in enumerate(zss):
+                for d, vae in enumerate(self.vaes):
                     px_zs[e][d] = vae.decode(zs, x[d])
         return qz_xs, px_zs, zss
 

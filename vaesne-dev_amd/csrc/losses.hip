@@ -28,6 +28,7 @@ struct IwaeArgs {
   int L[2];
   const float* loc[2][2];   // [r][d] -> [K, B, L_d]
   const float* scl[2][2];   // [r][d] -> [K, B, L_d]
+  int64_t ks[2][2];         // [r][d] element stride between consecutive k of a cell
   const float* zs[2];       // [K, B, n]
   const float* mu[2];       // [B, n]
   const float* sc[2];       // [B, n]
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(NT) void iwae_lw_kernel(IwaeArgs a, float* __restri
   for (int d = 0; d < 2; ++d) {
     const int L = a.L[d];
     const float* xp = a.x[d] + (int64_t)b * L;
-    const int64_t off = ((int64_t)k * a.B + b) * L;
+    const int64_t off = (int64_t)k * a.ks[r][d] + (int64_t)b * L;
     const float* lp = a.loc[r][d] + off;
     const float* sp = a.scl[r][d] + off;
     float s = 0.f;
@@ -132,11 +133,12 @@ __global__ void iwae_dloc_kernel(IwaeArgs a, const float* __restrict__ dlw, floa
     int l = (int)(e - kb * L);
     int b = (int)(kb % a.B);
     int k = (int)(kb / a.B);
+    const int64_t idx = (int64_t)k * a.ks[r][d] + (int64_t)b * L + l;
     float x = a.x[d][(int64_t)b * L + l];
-    float loc = a.loc[r][d][e];
-    float gr = dlw[(int64_t)(r * a.K + k) * a.B + b] * a.llik[d] * sgnf(x - loc) / a.scl[r][d][e];
+    float loc = a.loc[r][d][idx];
+    float gr = dlw[(int64_t)(r * a.K + k) * a.B + b] * a.llik[d] * sgnf(x - loc) / a.scl[r][d][idx];
     float* out = r == 0 ? (d == 0 ? dl00 : dl01) : (d == 0 ? dl10 : dl11);
-    if (out) out[e] = gr;
+    if (out) out[idx] = gr;
   }
 }
 
@@ -261,7 +263,8 @@ inline unsigned nblk(int64_t n, int64_t cap = 65536) {
 }
 
 IwaeArgs make_iwae(const float* const* xs, const float* llik, const int* L,
-                   const float* const* locs, const float* const* scls, const float* const* zs,
+                   const float* const* locs, const float* const* scls, const int64_t* kstride,
+                   const float* const* zs,
                    const float* const* mus, const float* const* scs, const float* pz_loc,
                    const float* pz_scale, int K, int B, int n) {
   IwaeArgs a{};
@@ -277,6 +280,7 @@ IwaeArgs make_iwae(const float* const* xs, const float* llik, const int* L,
     for (int d = 0; d < 2; ++d) {
       a.loc[r][d] = locs[2 * r + d];
       a.scl[r][d] = scls[2 * r + d];
+      a.ks[r][d] = kstride ? kstride[2 * r + d] : (int64_t)B * L[d];
     }
   a.pz_loc = pz_loc; a.pz_scale = pz_scale;
   a.K = K; a.B = B; a.n = n;
@@ -287,12 +291,13 @@ IwaeArgs make_iwae(const float* const* xs, const float* llik, const int* L,
 
 VAESNE_API int vaesne_iwae_lw_fwd(const float* const* x, const float* llik, const int* L,
                                   const float* const* loc, const float* const* scale,
+                                  const int64_t* kstride,
                                   const float* const* zs, const float* const* mu,
                                   const float* const* sc, const float* pz_loc,
                                   const float* pz_scale, int K, int B, int n, float* lw,
                                   void* stream) {
   if (B <= 0 || K <= 0) return (int)hipErrorInvalidValue;
-  IwaeArgs a = make_iwae(x, llik, L, loc, scale, zs, mu, sc, pz_loc, pz_scale, K, B, n);
+  IwaeArgs a = make_iwae(x, llik, L, loc, scale, kstride, zs, mu, sc, pz_loc, pz_scale, K, B, n);
   hipLaunchKernelGGL(iwae_lw_kernel, dim3((unsigned)(2 * K * B)), dim3(NT), 0,
                      (hipStream_t)stream, a, lw);
   VAESNE_CHECK_LAUNCH();
@@ -301,13 +306,14 @@ VAESNE_API int vaesne_iwae_lw_fwd(const float* const* x, const float* llik, cons
 
 VAESNE_API int vaesne_iwae_lw_bwd(const float* const* x, const float* llik, const int* L,
                                   const float* const* loc, const float* const* scale,
+                                  const int64_t* kstride,
                                   const float* const* zs, const float* const* mu,
                                   const float* const* sc, const float* pz_loc,
                                   const float* pz_scale, int K, int B, int n, const float* dlw,
                                   float* const* dloc, float* const* dzs, float* const* dmu,
                                   float* const* dsc, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  IwaeArgs a = make_iwae(x, llik, L, loc, scale, zs, mu, sc, pz_loc, pz_scale, K, B, n);
+  IwaeArgs a = make_iwae(x, llik, L, loc, scale, kstride, zs, mu, sc, pz_loc, pz_scale, K, B, n);
   int64_t tot = 2 * (int64_t)K * B * (L[0] + L[1]);
   hipLaunchKernelGGL(iwae_dloc_kernel, dim3(nblk(tot)), dim3(NT), 0, s, a, dlw, dloc[0], dloc[1],
                      dloc[2], dloc[3]);
