@@ -12,8 +12,8 @@ in HBM (weak scaling).  The step is captured once as a hipGraph and replayed.
 
 Rank 0 prints ONE JSON line (value = whole-job SN pairs/s).  Beside it:
   roofline     : the dominant kernel (spectra-decoder masked self-attention
-                 backward) timed with HIP events on its own stream, its
-                 algorithmic FLOPs / average launch time vs the FP32 peak;
+                 backward, dK/dV) timed with HIP events on its own stream,
+                 its algorithmic FLOPs / average launch time vs the FP32 peak;
   cpu_baseline : the CPU oracle (pure-PyTorch restatement of the reference,
                  oracle/vaesne_oracle.py) timed on the host cores on a bounded
                  sample (rank 0, N=1 only);
@@ -202,13 +202,22 @@ def roofline(device, B):
                          flops_per_launch=scores * fl)
     r = res["bwd_kv"]
     a = r["tflops"]
+    traffic, tsrc = None, None
+    try:   # HBM bytes per launch from the committed rocprofv3 --pmc passes (gpu_run.sh pmc)
+        t = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+        traffic = t["kernels"][r["kernel"]]["hbm_bytes_per_launch"]
+        tsrc = t["source"] + "; " + t["correction"]
+    except (OSError, KeyError, ValueError):
+        pass
     return dict(bound="mfma", kernel=r["kernel"], achieved=round(a, 3), peak=FP32_PEAK_TFLOPS,
-                unit="TFLOP/s", frac=round(a / FP32_PEAK_TFLOPS, 4), traffic=None,
+                unit="TFLOP/s", frac=round(a / FP32_PEAK_TFLOPS, 4), traffic=traffic,
+                traffic_source=tsrc,
                 launch_ms=round(r["ms"], 4), flops_per_launch=r["flops_per_launch"],
                 detail={k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                             for kk, vv in v.items()} for k, v in res.items()},
-                note="fp32 packed-VALU kernel; peak = FP32 157.3 TF (vector = f32-MFMA rate on "
-                     "gfx950); scores per launch = 2*K*B*H*982^2 = %d" % scores)
+                note="fp32 packed-VALU kernel (v_pk_fma_f32); peak = FP32 157.3 TF (vector = "
+                     "f32-MFMA rate on gfx950); "
+                     "scores per launch = 2*K*B*H*982^2 = %d" % scores)
 
 
 def cpu_baseline(sample_B=2, steps=2):
@@ -283,7 +292,17 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the roofline kernel launches (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
+    if args.roofline_only:
+        device = torch.device("cuda", 0)
+        torch.cuda.set_device(device)
+        from VAESNe import _lib, rng
+        _lib.load()
+        rng.manual_seed(1234)
+        print(json.dumps(roofline(device, args.batch)), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -9,13 +9,14 @@
 //   in[r, k]  = (a[r, k] + a2[r, k]) * (act_in_grad ? act'(zin[r, k]) : 1)
 //   optional activation on the way out (relu / exact-erf gelu), pre-activation
 //   optionally stored for the backward.
-// Geometry: 256-thread workgroup = 4 waves; a 64-row tile puts one row on each
-// lane; wave w owns the contiguous output columns [w*C, (w+1)*C).  The weight
-// (<= 128 x 128 fp32) sits in LDS once per workgroup and is read as broadcast
-// float4s; workgroups walk row tiles with a grid stride.
+// Geometry: MFMA v_mfma_f32_32x32x2_f32 (exact f32) in the feature layout of
+// decoder_block.hip: a wave owns 32 rows (lane = row, 16 features per lane and
+// 32-block as 4 float4s), y^T = W x^T is 16 MFMAs per 32x32 block with the
+// weight in LDS (staged once per workgroup, odd row stride).
 //
 // Backward-weight kernel: dW[o, i] = sum_r dz[r, o] x[r, i], db[o] = sum_r dz[r, o]
-// with dz = dy * act'(z) recomputed on the fly; per-workgroup partial sums in a
+// with dz = dy * act'(z) recomputed on the fly, as MFMAs contracting over rows
+// (both operands coalesced row segments); per-workgroup partial sums in a
 // workspace, then a fixed-order reduction (bitwise reproducible).
 #include "common.h"
 
@@ -46,124 +47,181 @@ __device__ __forceinline__ float act_grad(int act, float z) {
   return 1.f;
 }
 
-constexpr int ROWS = 64;
 constexpr int NT = 256;
 constexpr int MAXK = 128;
 constexpr int MAXN = 128;
+constexpr int MAXB = MAXK / 32;   // 32-feature blocks
 
-template <int C, bool VEC>
-__global__ __launch_bounds__(NT) void linear_kernel(LinArgs p) {
-  __shared__ float4 Ws4[MAXN * (MAXK / 4)];
-  const int KP = (p.K + 3) & ~3;
-  const int KP4 = KP >> 2;
-  float* Ws = reinterpret_cast<float*>(Ws4);
-  // stage Wt[n][k] (zero padded in k)
-  for (int idx = threadIdx.x; idx < p.N * KP; idx += NT) {
-    int n = idx / KP, k = idx - n * KP;
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f16v mfma(float a, float b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+// feature layout of v_mfma_f32_32x32x2_f32 (as decoder_block.hip): lane l holds
+// row t = l & 31 and, per 32-feature block, features F(s, h), h = l >> 5
+__device__ __forceinline__ int F(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// x[s] = (a + a2)[row][kb*32 + F(s,h)] * (act_in_grad ? act'(zin) : 1), 0 past K
+template <bool VIN>
+__device__ __forceinline__ void load_feat(const LinArgs& p, int64_t row, int kb, int h,
+                                          float (&x)[16]) {
+  const float* ar = p.a + row * p.lda;
+  const float* a2r = p.a2 ? p.a2 + row * p.lda2 : nullptr;
+  const float* zr = p.act_in_grad ? p.zin + row * p.ldzin : nullptr;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k0 = kb * 32 + 8 * j + 4 * h;
+    if (VIN) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k0 < p.K) {
+        v = *reinterpret_cast<const float4*>(ar + k0);
+        if (a2r) {
+          const float4 w = *reinterpret_cast<const float4*>(a2r + k0);
+          v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+        }
+        if (zr) {
+          const float4 z = *reinterpret_cast<const float4*>(zr + k0);
+          v.x *= act_grad(p.act_in_grad, z.x); v.y *= act_grad(p.act_in_grad, z.y);
+          v.z *= act_grad(p.act_in_grad, z.z); v.w *= act_grad(p.act_in_grad, z.w);
+        }
+      }
+      x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + i;
+        float v = 0.f;
+        if (k < p.K) {
+          v = ar[k];
+          if (a2r) v += a2r[k];
+          if (zr) v *= act_grad(p.act_in_grad, zr[k]);
+        }
+        x[4 * j + i] = v;
+      }
+    }
+  }
+}
+
+// out[row][nb*32 + F(i,h)] = act((accum ? out : 0) + acc[i]), pre-activation to zout
+template <bool VOUT>
+__device__ __forceinline__ void store_feat(const LinArgs& p, int64_t row, int nb, int h,
+                                           const f16v& acc) {
+  float* orow = p.out + row * p.ldo;
+  float* zrow = p.zout ? p.zout + row * p.ldzo : nullptr;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n0 = nb * 32 + 8 * j + 4 * h;
+    if (VOUT) {
+      if (n0 < p.N) {
+        float4 v = make_float4(acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]);
+        if (p.accum) {
+          const float4 o = *reinterpret_cast<const float4*>(orow + n0);
+          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        }
+        if (zrow) *reinterpret_cast<float4*>(zrow + n0) = v;
+        v.x = act_fwd(p.act_out, v.x); v.y = act_fwd(p.act_out, v.y);
+        v.z = act_fwd(p.act_out, v.z); v.w = act_fwd(p.act_out, v.w);
+        *reinterpret_cast<float4*>(orow + n0) = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + i;
+        if (n < p.N) {
+          float v = acc[4 * j + i];
+          if (p.accum) v += orow[n];
+          if (zrow) zrow[n] = v;
+          orow[n] = act_fwd(p.act_out, v);
+        }
+      }
+    }
+  }
+}
+
+// y^T = W x^T on v_mfma_f32_32x32x2_f32: a wave owns 32 rows; A = W from LDS
+// (row n = lane & 31, k = F(s, h)), B = the row's own features: 16 MFMAs per
+// 32x32 block, output straight in the feature layout (no shuffles).  The
+// weight (zero padded to kbn x nbn blocks of 32) is staged once per workgroup.
+template <bool VIN, bool VOUT>
+__global__ __launch_bounds__(NT) void linear_kernel(LinArgs p, int kbn, int nbn) {
+  extern __shared__ float smem[];
+  const int LDW = kbn * 32 + 1;             // odd row stride: conflict-free A reads
+  float* Ws = smem;                         // [nbn*32][LDW]: Ws[n][k] = W(n, k)
+  float* bs = smem + nbn * 32 * LDW;        // [nbn*32]
+  for (int idx = threadIdx.x; idx < nbn * 32 * kbn * 32; idx += NT) {
+    const int n = idx / (kbn * 32), k = idx - n * (kbn * 32);
     float w = 0.f;
-    if (k < p.K) w = p.w_trans ? p.W[(int64_t)k * p.N + n] : p.W[(int64_t)n * p.K + k];
-    Ws[idx] = w;
+    if (n < p.N && k < p.K) w = p.w_trans ? p.W[(int64_t)k * p.N + n] : p.W[(int64_t)n * p.K + k];
+    Ws[n * LDW + k] = w;
   }
+  for (int n = threadIdx.x; n < nbn * 32; n += NT) bs[n] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int n0 = wave * C;
-  if (n0 >= p.N) return;  // no barrier after this point
-  const int nc = min(C, p.N - n0);
-  float bias[C];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int t = lane & 31, h = lane >> 5;
+  const int64_t tiles = (p.M + 31) / 32;
+  for (int64_t tile = (int64_t)blockIdx.x * (NT / 64) + wave; tile < tiles;
+       tile += (int64_t)gridDim.x * (NT / 64)) {
+    const int64_t r = tile * 32 + t;
+    const bool valid = r < p.M;
+    const int64_t rr = valid ? r : p.M - 1;
+    float x[MAXB][16];
 #pragma unroll
-  for (int c = 0; c < C; ++c) bias[c] = (p.bias && c < nc) ? p.bias[n0 + c] : 0.f;
-
-  const int64_t tiles = (p.M + ROWS - 1) / ROWS;
-  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
-    const int64_t r = t * ROWS + lane;
-    if (r >= p.M) continue;
-    float acc[C];
+    for (int kb = 0; kb < MAXB; ++kb)
+      if (kb < kbn) load_feat<VIN>(p, rr, kb, h, x[kb]);
+    for (int nb = 0; nb < nbn; ++nb) {
+      f16v acc;
 #pragma unroll
-    for (int c = 0; c < C; ++c) acc[c] = bias[c];
-    const float* arow = p.a + r * p.lda;
-    const float* a2row = p.a2 ? p.a2 + r * p.lda2 : nullptr;
-    const float* zrow = p.act_in_grad ? p.zin + r * p.ldzin : nullptr;
-    for (int k4 = 0; k4 < KP4; ++k4) {
-      float4 xv;
-      if (VEC) {
-        xv = *reinterpret_cast<const float4*>(arow + 4 * k4);
-        if (a2row) {
-          float4 x2 = *reinterpret_cast<const float4*>(a2row + 4 * k4);
-          xv.x += x2.x; xv.y += x2.y; xv.z += x2.z; xv.w += x2.w;
-        }
-        if (zrow) {
-          float4 zv = *reinterpret_cast<const float4*>(zrow + 4 * k4);
-          xv.x *= act_grad(p.act_in_grad, zv.x); xv.y *= act_grad(p.act_in_grad, zv.y);
-          xv.z *= act_grad(p.act_in_grad, zv.z); xv.w *= act_grad(p.act_in_grad, zv.w);
-        }
-      } else {
-        float e[4];
+      for (int i = 0; i < 16; ++i) acc[i] = bs[nb * 32 + F(i, h)];
+      const float* wr = Ws + (nb * 32 + t) * LDW;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          int k = 4 * k4 + j;
-          float v = 0.f;
-          if (k < p.K) {
-            v = arow[k];
-            if (a2row) v += a2row[k];
-            if (zrow) v *= act_grad(p.act_in_grad, zrow[k]);
-          }
-          e[j] = v;
-        }
-        xv = make_float4(e[0], e[1], e[2], e[3]);
-      }
+      for (int kb = 0; kb < MAXB; ++kb) {
+        if (kb < kbn) {
 #pragma unroll
-      for (int c = 0; c < C; ++c) {
-        if (c < nc) {
-          float4 w = Ws4[(n0 + c) * KP4 + k4];
-          acc[c] = fmaf(xv.x, w.x, acc[c]);
-          acc[c] = fmaf(xv.y, w.y, acc[c]);
-          acc[c] = fmaf(xv.z, w.z, acc[c]);
-          acc[c] = fmaf(xv.w, w.w, acc[c]);
+          for (int s2 = 0; s2 < 16; ++s2) acc = mfma(wr[kb * 32 + F(s2, h)], x[kb][s2], acc);
         }
       }
-    }
-    float* orow = p.out + r * p.ldo + n0;
-    float* zorow = p.zout ? p.zout + r * p.ldzo + n0 : nullptr;
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      if (c < nc) {
-        float v = acc[c];
-        if (p.accum) v += orow[c];
-        if (zorow) zorow[c] = v;
-        orow[c] = act_fwd(p.act_out, v);
-      }
+      if (valid) store_feat<VOUT>(p, r, nb, h, acc);
     }
   }
 }
 
-template <int C>
-int launch_linear_c(const LinArgs& p, hipStream_t s) {
-  int64_t tiles = (p.M + ROWS - 1) / ROWS;
-  int grid = (int)(tiles < 2048 ? tiles : 2048);
-  if (grid < 1) return 0;
-  bool vec = (p.K % 4 == 0) && (p.lda % 4 == 0) && ((uintptr_t)p.a % 16 == 0) &&
-             (!p.a2 || ((p.lda2 % 4 == 0) && ((uintptr_t)p.a2 % 16 == 0))) &&
-             (!p.act_in_grad || ((p.ldzin % 4 == 0) && ((uintptr_t)p.zin % 16 == 0)));
-  if (vec)
-    hipLaunchKernelGGL((linear_kernel<C, true>), dim3(grid), dim3(NT), 0, s, p);
-  else
-    hipLaunchKernelGGL((linear_kernel<C, false>), dim3(grid), dim3(NT), 0, s, p);
-  VAESNE_CHECK_LAUNCH();
-  return 0;
-}
+bool al16(const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && (ld % 4 == 0); }
 
 int launch_linear(const LinArgs& p, hipStream_t s) {
   if (p.K < 1 || p.K > MAXK || p.N < 1 || p.N > MAXN) return (int)hipErrorInvalidValue;
   if (p.M <= 0) return 0;
-  int c = (p.N + 3) / 4;
-  if (c <= 1) return launch_linear_c<1>(p, s);
-  if (c <= 2) return launch_linear_c<2>(p, s);
-  if (c <= 4) return launch_linear_c<4>(p, s);
-  if (c <= 8) return launch_linear_c<8>(p, s);
-  if (c <= 16) return launch_linear_c<16>(p, s);
-  if (c <= 24) return launch_linear_c<24>(p, s);
-  return launch_linear_c<32>(p, s);
+  const int kbn = (p.K + 31) / 32, nbn = (p.N + 31) / 32;
+  const int64_t tiles = (p.M + 31) / 32;
+  const int64_t wg = (tiles + NT / 64 - 1) / (NT / 64);
+  const int grid = (int)(wg < 2048 ? wg : 2048);
+  const size_t shmem = sizeof(float) * ((size_t)nbn * 32 * (kbn * 32 + 1) + nbn * 32);
+  const bool vin = (p.K % 4 == 0) && al16(p.a, p.lda) && (!p.a2 || al16(p.a2, p.lda2)) &&
+                   (!p.act_in_grad || al16(p.zin, p.ldzin));
+  const bool vout = (p.N % 4 == 0) && al16(p.out, p.ldo) && (!p.zout || al16(p.zout, p.ldzo));
+  if (shmem > 65536) {   // > 64 KB of LDS (K, N up to 128): opt in once per instantiation
+    static bool opted = false;
+    if (!opted) {
+      const void* fns[4] = {(const void*)linear_kernel<true, true>,
+                            (const void*)linear_kernel<true, false>,
+                            (const void*)linear_kernel<false, true>,
+                            (const void*)linear_kernel<false, false>};
+      for (const void* f : fns) {
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return (int)e;
+      }
+      opted = true;
+    }
+  }
+  if (vin && vout)
+    hipLaunchKernelGGL((linear_kernel<true, true>), dim3(grid), dim3(NT), shmem, s, p, kbn, nbn);
+  else if (vin)
+    hipLaunchKernelGGL((linear_kernel<true, false>), dim3(grid), dim3(NT), shmem, s, p, kbn, nbn);
+  else if (vout)
+    hipLaunchKernelGGL((linear_kernel<false, true>), dim3(grid), dim3(NT), shmem, s, p, kbn, nbn);
+  else
+    hipLaunchKernelGGL((linear_kernel<false, false>), dim3(grid), dim3(NT), shmem, s, p, kbn, nbn);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -175,67 +233,75 @@ struct WgtArgs {
   const float* x; int64_t ldx;
   const float* x2; int64_t ldx2;         // x := x + x2
   int64_t M; int O; int I;
-  float* partial;                        // [gridDim][O*(I+1)]
+  float* partial;                        // [gridDim.x][O*I + O]
 };
 
-constexpr int WROWS = 64;
+// One workgroup per (row range, 32 x 32 block of dW).  dW^T is never formed:
+// v_mfma_f32_32x32x2_f32 with A[o][kk] = dz[r + kk][o] and B[kk][i] = x[r + kk][i]
+// (lane l: column l & 31 of row r + (l >> 5)) contracts over rows, so both
+// operands are plain coalesced 128-byte row segments straight from HBM / L2.
+// db rides along as the column sum of the dz values the o-block lanes load.
+constexpr int WG_MAX = 256;
 
-template <int E>
-__global__ __launch_bounds__(NT) void linear_wgrad_kernel(WgtArgs p) {
-  __shared__ float Dz[WROWS * MAXN];
-  __shared__ float Xs[WROWS * (MAXK + 1)];
-  const int I1 = p.I + 1;
-  const int F = p.O * I1;
-  float acc[E];
-  int fo[E], fi[E];
+int64_t wgrad_groups(int64_t M) {
+  const int64_t chunks = (M + 31) / 32;                 // 32 rows per wave iteration
+  int64_t g = (chunks + NT / 64 - 1) / (NT / 64);
+  if (g > WG_MAX) g = WG_MAX;
+  return g < 1 ? 1 : g;
+}
+
+__global__ __launch_bounds__(NT) void linear_wgrad_kernel(WgtArgs p, int nib) {
+  __shared__ float red[NT / 64][1024 + 32];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 31, hh = lane >> 5;
+  const int ob = blockIdx.y / nib, ib = blockIdx.y - ob * nib;
+  const int o = ob * 32 + col, i = ib * 32 + col;
+  const bool oin = o < p.O, iin = i < p.I;
+  f16v acc = {};
+  float cs = 0.f;
+  const int64_t chunks = (p.M + 31) / 32;
+  for (int64_t ch = (int64_t)blockIdx.x * (NT / 64) + wave; ch < chunks;
+       ch += (int64_t)gridDim.x * (NT / 64)) {
+    float gv[16], xv[16];
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    acc[e] = 0.f;
-    int f = threadIdx.x + NT * e;
-    fo[e] = f < F ? f / I1 : 0;
-    fi[e] = f < F ? f - fo[e] * I1 : 0;
-  }
-  const int64_t tiles = (p.M + WROWS - 1) / WROWS;
-  for (int64_t t = blockIdx.x; t < tiles; t += gridDim.x) {
-    const int64_t r0 = t * WROWS;
-    const int nr = (int)min((int64_t)WROWS, p.M - r0);
-    __syncthreads();
-    for (int idx = threadIdx.x; idx < WROWS * p.O; idx += NT) {
-      int rr = idx / p.O, o = idx - rr * p.O;
-      float v = 0.f;
-      if (rr < nr) {
-        int64_t r = r0 + rr;
-        v = p.dy[r * p.lddy + o];
-        if (p.act) v *= act_grad(p.act, p.z[r * p.ldz + o]);
-      }
-      Dz[rr * p.O + o] = v;
-    }
-    for (int idx = threadIdx.x; idx < WROWS * I1; idx += NT) {
-      int rr = idx / I1, i = idx - rr * I1;
-      float v = 0.f;
-      if (rr < nr) {
-        int64_t r = r0 + rr;
-        if (i < p.I) {
-          v = p.x[r * p.ldx + i];
-          if (p.x2) v += p.x2[r * p.ldx2 + i];
-        } else {
-          v = 1.f;
+    for (int s2 = 0; s2 < 16; ++s2) {
+      const int64_t r = ch * 32 + 2 * s2 + hh;
+      float gg = 0.f, xx = 0.f;
+      if (r < p.M) {
+        if (oin) {
+          gg = p.dy[r * p.lddy + o];
+          if (p.act) gg *= act_grad(p.act, p.z[r * p.ldz + o]);
+        }
+        if (iin) {
+          xx = p.x[r * p.ldx + i];
+          if (p.x2) xx += p.x2[r * p.ldx2 + i];
         }
       }
-      Xs[rr * I1 + i] = v;
+      gv[s2] = gg;
+      xv[s2] = xx;
+      cs += gg;
     }
-    __syncthreads();
-    for (int rr = 0; rr < nr; ++rr) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) acc[e] = fmaf(Dz[rr * p.O + fo[e]], Xs[rr * I1 + fi[e]], acc[e]);
-    }
+    for (int s2 = 0; s2 < 16; ++s2) acc = mfma(gv[s2], xv[s2], acc);
   }
-  // partial layout [G][O*I (dW) | O (db)] so one column-sum splits at O*I
-  float* out = p.partial + (int64_t)blockIdx.x * F;
+  cs += __shfl_xor(cs, 32, 64);
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    int f = threadIdx.x + NT * e;
-    if (f < F) out[fi[e] < p.I ? fo[e] * p.I + fi[e] : p.O * p.I + fo[e]] = acc[e];
+  for (int rg = 0; rg < 16; ++rg) red[wave][F(rg, hh) * 32 + col] = acc[rg];
+  if (hh == 0) red[wave][1024 + col] = cs;
+  __syncthreads();
+  // partial layout [G][O*I (dW) | O (db)] so one column-sum splits at O*I
+  float* out = p.partial + (int64_t)blockIdx.x * ((int64_t)p.O * p.I + p.O);
+  for (int e = threadIdx.x; e < 1024 + 32; e += NT) {
+    float v = red[0][e];
+#pragma unroll
+    for (int w = 1; w < NT / 64; ++w) v += red[w][e];
+    if (e < 1024) {
+      const int oo = ob * 32 + (e >> 5), ii = ib * 32 + (e & 31);
+      if (oo < p.O && ii < p.I) out[(int64_t)oo * p.I + ii] = v;
+    } else if (ib == 0) {
+      const int oo = ob * 32 + (e - 1024);
+      if (oo < p.O) out[(int64_t)p.O * p.I + oo] = v;
+    }
   }
 }
 
@@ -273,10 +339,7 @@ VAESNE_API int vaesne_linear_bwd_data(const float* dy, int64_t lddy, const float
 }
 
 VAESNE_API int64_t vaesne_linear_bwd_weight_workspace(int64_t M, int O, int I) {
-  int64_t tiles = (M + WROWS - 1) / WROWS;
-  int64_t g = tiles < 512 ? tiles : 512;
-  if (g < 1) g = 1;
-  return g * (int64_t)O * (I + 1) * (int64_t)sizeof(float);
+  return wgrad_groups(M) * ((int64_t)O * I + O) * (int64_t)sizeof(float);
 }
 
 VAESNE_API int vaesne_linear_bwd_weight(const float* dy, int64_t lddy, const float* z, int64_t ldz,
@@ -285,27 +348,17 @@ VAESNE_API int vaesne_linear_bwd_weight(const float* dy, int64_t lddy, const flo
                                         float* db, int accum, float* workspace, void* stream) {
   if (O < 1 || O > MAXN || I < 1 || I > MAXK) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  int64_t tiles = (M + WROWS - 1) / WROWS;
-  int G = (int)(tiles < 512 ? tiles : 512);
-  const int F = O * (I + 1);
-  if (G < 1) {
+  const int F = O * I + O;
+  int G = 1;
+  if (M <= 0) {
     // empty batch: gradient is zero
-    G = 1;
     hipError_t me = hipMemsetAsync(workspace, 0, sizeof(float) * F, s);
     if (me != hipSuccess) return (int)me;
   } else {
+    G = (int)wgrad_groups(M);
     WgtArgs p{dy, lddy, z, ldz, act, x, ldx, x2, ldx2, M, O, I, workspace};
-    int e = (F + NT - 1) / NT;
-    if (e <= 4)
-      hipLaunchKernelGGL(linear_wgrad_kernel<4>, dim3(G), dim3(NT), 0, s, p);
-    else if (e <= 8)
-      hipLaunchKernelGGL(linear_wgrad_kernel<8>, dim3(G), dim3(NT), 0, s, p);
-    else if (e <= 16)
-      hipLaunchKernelGGL(linear_wgrad_kernel<16>, dim3(G), dim3(NT), 0, s, p);
-    else if (e <= 40)
-      hipLaunchKernelGGL(linear_wgrad_kernel<40>, dim3(G), dim3(NT), 0, s, p);
-    else
-      return (int)hipErrorInvalidValue;
+    const int nob = (O + 31) / 32, nib = (I + 31) / 32;
+    hipLaunchKernelGGL(linear_wgrad_kernel, dim3(G, nob * nib), dim3(NT), 0, s, p, nib);
     VAESNE_CHECK_LAUNCH();
   }
   return launch_colsum(workspace, G, F, dW, db, O * I, accum, s);
