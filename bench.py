@@ -182,14 +182,14 @@ def roofline(device, B):
     def fwd():
         lib.attn_fwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E, kbias.data_ptr(), L,
                      o.data_ptr(), L * E, E, lse.data_ptr(), N, H, L, L, dh, 0.1, st.data_ptr(), 7,
-                     bits.data_ptr(), _lib.stream())
+                     bits.data_ptr(), None, _lib.stream())
 
     def bwd(fn):
         return lambda: fn(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E,
                           kbias.data_ptr(), L, o.data_ptr(), L * E, E, lse.data_ptr(),
                           do.data_ptr(), L * E, E, d, s3, 3 * E, d + 4 * E, s3, 3 * E, d + 8 * E,
                           s3, 3 * E, N, H, L, L, dh, 0.1, st.data_ptr(), 7, bits.data_ptr(),
-                          _lib.stream())
+                          None, _lib.stream())
 
     fwd()
     scores = N * H * L * L

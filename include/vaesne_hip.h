@@ -80,15 +80,19 @@ int vaesne_reduce_partials(const float* partial, int G, int F, float* out0, floa
  * lse [B,H,Lq] (log2 domain) is saved for the backward.  dh in {8, 16}.
  * Dropout (p_drop > 0): the forward draws the keep mask from the counter RNG
  * and stores it in keep_bits (1 bit per score, vaesne_attn_keep_bits_size
- * bytes); the backward reads it. */
+ * bytes); the backward reads it.
+ * workspace (may be null): vaesne_attn_workspace(..., bwd) bytes.  Shapes whose
+ * grid cannot fill the chip (the encoder's 983-token context self-attention,
+ * B*H = 64) then run as key / query chunks with a fixed-order combine. */
 int vaesne_mask_bias(const uint8_t* mask, int64_t n, float* out, void* stream);
 int64_t vaesne_attn_keep_bits_size(int B, int H, int Lq, int Lk);
+int64_t vaesne_attn_workspace(int B, int H, int Lq, int Lk, int dh, int bwd);
 int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
                     int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls,
                     const float* kbias, int64_t kb_bs, float* o, int64_t o_bs, int64_t o_ls,
                     float* lse, int B, int H, int Lq, int Lk, int dh, float p_drop,
                     const int64_t* rng_state, uint32_t call_id, uint32_t* keep_bits,
-                    void* stream);
+                    float* workspace, void* stream);
 /* Backward.  Query-tiled shapes read the forward's keep_bits; the few-query
  * path (Lq <= 16: the encoders' latent tokens, one fused key-parallel kernel)
  * re-derives the keep decisions from (rng_state, call_id), which must be the
@@ -102,7 +106,7 @@ int vaesne_attn_bwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, 
                     int64_t dq_ls, float* dk, int64_t dk_bs, int64_t dk_ls, float* dv, int64_t dv_bs,
                     int64_t dv_ls, int B, int H, int Lq, int Lk, int dh, float p_drop,
                     const int64_t* rng_state, uint32_t call_id, const uint32_t* keep_bits,
-                    void* stream);
+                    float* workspace, void* stream);
 int vaesne_attn_bwd_kv(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
                        int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls, const float* kbias,
                        int64_t kb_bs, const float* o, int64_t o_bs, int64_t o_ls, const float* lse,
@@ -110,7 +114,7 @@ int vaesne_attn_bwd_kv(const float* q, int64_t q_bs, int64_t q_ls, const float* 
                        int64_t dq_ls, float* dk, int64_t dk_bs, int64_t dk_ls, float* dv, int64_t dv_bs,
                        int64_t dv_ls, int B, int H, int Lq, int Lk, int dh, float p_drop,
                        const int64_t* rng_state, uint32_t call_id, const uint32_t* keep_bits,
-                       void* stream);
+                       float* workspace, void* stream);
 int vaesne_attn_bwd_q(const float* q, int64_t q_bs, int64_t q_ls, const float* k, int64_t k_bs,
                       int64_t k_ls, const float* v, int64_t v_bs, int64_t v_ls, const float* kbias,
                       int64_t kb_bs, const float* o, int64_t o_bs, int64_t o_ls, const float* lse,
@@ -118,7 +122,7 @@ int vaesne_attn_bwd_q(const float* q, int64_t q_bs, int64_t q_ls, const float* k
                       int64_t dq_ls, float* dk, int64_t dk_bs, int64_t dk_ls, float* dv, int64_t dv_bs,
                       int64_t dv_ls, int B, int H, int Lq, int Lk, int dh, float p_drop,
                       const int64_t* rng_state, uint32_t call_id, const uint32_t* keep_bits,
-                      void* stream);
+                      float* workspace, void* stream);
 
 /* ---- fused decoder-block tail --------------------------------------------------
  * Everything of a decoder TransformerBlock after its masked self-attention core

@@ -153,7 +153,7 @@ def test_attention_dropout_statistics_and_backward_mask(B, Lq, Lk):
     assert _rel(dv, expect) < 1e-5
 
 
-@pytest.mark.parametrize("B,Lq,Lk", [(2, 200, 40), (3, 37, 70)])
+@pytest.mark.parametrize("B,Lq,Lk", [(2, 200, 40), (3, 37, 70), (2, 300, 300)])
 def test_attention_dropout_outputs_and_all_gradients_vs_dense(B, Lq, Lk):
     """With dropout on, out / dQ / dK / dV of the query-tiled kernels equal a
     dense fp64 attention that applies the kernel's own keep mask (probed 8

@@ -27,7 +27,7 @@ PP = C.POINTER(C.c_void_p)
 # name -> (restype, argtypes).  Mirrors include/vaesne_hip.h one to one.
 _ATTN_BWD = (I32, [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, P, I64, I64, P, P, I64, I64, P,
                    I64, I64, P, I64, I64, P, I64, I64, I32, I32, I32, I32, I32, F32, P, U32, P,
-                   P])
+                   P, P])
 
 SIGNATURES = {
     "vaesne_linear_fwd": (I32, [P, I64, P, I64, I64, I32, P, P, I32, P, I64, P, I64, I32, I32, P]),
@@ -42,8 +42,9 @@ SIGNATURES = {
     "vaesne_reduce_partials": (I32, [P, I32, I32, P, P, I32, I32, P]),
     "vaesne_mask_bias": (I32, [P, I64, P, P]),
     "vaesne_attn_keep_bits_size": (I64, [I32, I32, I32, I32]),
+    "vaesne_attn_workspace": (I64, [I32, I32, I32, I32, I32, I32]),
     "vaesne_attn_fwd": (I32, [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, P, I64, I64, P, I32,
-                              I32, I32, I32, I32, F32, P, U32, P, P]),
+                              I32, I32, I32, I32, F32, P, U32, P, P, P]),
     "vaesne_attn_bwd": _ATTN_BWD,
     "vaesne_attn_bwd_kv": _ATTN_BWD,
     "vaesne_attn_bwd_q": _ATTN_BWD,

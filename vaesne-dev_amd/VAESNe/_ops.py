@@ -182,6 +182,12 @@ def _bias_of(mask, kbias):
     return key_bias(mask)
 
 
+def _attn_ws(B, H, Lq, Lk, dh, bwd, dev):
+    """Workspace of a chunked (split) attention launch, or None (not needed)."""
+    n = lib.attn_workspace(B, H, Lq, Lk, dh, bwd)
+    return _ws(n, dev) if n > 0 else None
+
+
 def _attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, kbias, B, H, Lq, Lk, dh, p, dev):
     E = H * dh
     o = torch.empty((B, Lq, E), dtype=torch.float32, device=dev)
@@ -192,8 +198,10 @@ def _attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, kbias, B, H, Lq, Lk, dh, p, dev):
     if p > 0:
         n = lib.attn_keep_bits_size(B, H, Lq, Lk)
         bits = torch.empty((n + 3) // 4, dtype=torch.int32, device=dev)
+    ws = _attn_ws(B, H, Lq, Lk, dh, 0, dev)
     lib.attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, ptr(kbias), Lk, o.data_ptr(), Lq * E, E,
-                 lse.data_ptr(), B, H, Lq, Lk, dh, float(p), ptr(st), cid, ptr(bits), stream())
+                 lse.data_ptr(), B, H, Lq, Lk, dh, float(p), ptr(st), cid, ptr(bits), ptr(ws),
+                 stream())
     return o, lse, bits, st, cid
 
 
@@ -226,7 +234,8 @@ class SelfAttnFn(torch.autograd.Function):
         lib.attn_bwd(b, L * E3, E3, b + 4 * E, L * E3, E3, b + 8 * E, L * E3, E3, ptr(kbias), L,
                      o.data_ptr(), L * E, E, lse.data_ptr(), do.data_ptr(), L * E, E,
                      d, L * E3, E3, d + 4 * E, L * E3, E3, d + 8 * E, L * E3, E3,
-                     B, H, L, L, dh, p, ptr(st), cid, ptr(bits), stream())
+                     B, H, L, L, dh, p, ptr(st), cid, ptr(bits),
+                     ptr(_attn_ws(B, H, L, L, dh, 1, qkv.device)), stream())
         return dqkv, None, None, None
 
 
@@ -260,7 +269,8 @@ class CrossAttnFn(torch.autograd.Function):
         lib.attn_bwd(q.data_ptr(), Lq * E, E, kb, Lk * 2 * E, 2 * E, kb + 4 * E, Lk * 2 * E,
                      2 * E, ptr(kbias), Lk, o.data_ptr(), Lq * E, E, lse.data_ptr(), do.data_ptr(),
                      Lq * E, E, dq.data_ptr(), Lq * E, E, dkb, Lk * 2 * E, 2 * E, dkb + 4 * E,
-                     Lk * 2 * E, 2 * E, B, H, Lq, Lk, dh, p, ptr(st), cid, ptr(bits), stream())
+                     Lk * 2 * E, 2 * E, B, H, Lq, Lk, dh, p, ptr(st), cid, ptr(bits),
+                     ptr(_attn_ws(B, H, Lq, Lk, dh, 1, q.device)), stream())
         return dq, dkv, None, None, None
 
 

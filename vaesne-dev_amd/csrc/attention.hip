@@ -19,6 +19,8 @@
 //     62 MB per 128x4x982^2 layer) so both backward kernels read bits instead
 //     of re-hashing;
 //   * D = rowsum(dO * O) is computed by the query-tile loaders (no pre-pass).
+#include <algorithm>
+
 #include "common.h"
 
 using namespace vaesne;
@@ -47,6 +49,13 @@ struct AttnArgs {
   float scale_log2;   // log2(e)/sqrt(dh)
   uint32_t thr; float inv_keep;
   const int64_t* rng_state; uint32_t call_id;
+  // split launches (gridDim.y chunks, small grids only): chunk y covers keys
+  // [y*kchunk, ..) (forward, dQ) or queries [y*qchunk, ..) (dK/dV) and writes
+  // partial results at +y*(o_ss | dq_ss | dk_ss); the forward's partial o is
+  // un-normalised, with (m, l) per query in ml.  Unsplit: chunk = whole axis.
+  int kchunk, qchunk;
+  int64_t o_ss, dq_ss, dk_ss;
+  float* ml;                                // [split][B*H*Lq][2] or null
 };
 
 __device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -144,15 +153,16 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   const float* vg = a.v + (int64_t)b * a.v_bs + h * DH;
   const float* kbg = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
   uint32_t* bitp = DROP ? a.bits + (int64_t)bh * a.nw * a.Lq : nullptr;
+  const int kbeg = blockIdx.y * a.kchunk, klim = min(a.Lk, kbeg + a.kchunk);
 
-  for (int kt = 0; kt < a.Lk; kt += TK) {
+  for (int kt = kbeg; kt < klim; kt += TK) {
     __syncthreads();
-    stage<DH, NTT>(Ks, kg, a.k_ls, kt, a.Lk, 1.f);
-    stage<DH, NTT>(Vs, vg, a.v_ls, kt, a.Lk, 1.f);
+    stage<DH, NTT>(Ks, kg, a.k_ls, kt, klim, 1.f);
+    stage<DH, NTT>(Vs, vg, a.v_ls, kt, klim, 1.f);
     for (int i = threadIdx.x; i < TK; i += NTT)
-      Kb[i] = kt + i < a.Lk ? (kbg ? kbg[kt + i] : 0.f) : -INFINITY;
+      Kb[i] = kt + i < klim ? (kbg ? kbg[kt + i] : 0.f) : -INFINITY;
     __syncthreads();
-    const int kend = min(TK, a.Lk - kt);
+    const int kend = min(TK, klim - kt);
     uint32_t w[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) w[u] = 0u;
@@ -233,6 +243,26 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
       }
     }
   }
+  if (a.ml) {   // split launch: un-normalised partial o and (m, l) of this key chunk
+    float* ob = a.o_out + blockIdx.y * a.o_ss + (int64_t)b * a.o_bs + h * DH;
+    float* mlp = a.ml + ((int64_t)blockIdx.y * a.B * a.H + bh) * a.Lq * 2;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      float r0[DH], r1[DH];
+#pragma unroll
+      for (int d = 0; d < DH; ++d) { r0[d] = o[p][d].x; r1[d] = o[p][d].y; }
+      const int i0 = qi[2 * p], i1 = qi[2 * p + 1];
+      if (i0 < a.Lq) {
+        str<DH>(ob + (int64_t)i0 * a.o_ls, r0);
+        *reinterpret_cast<float2*>(mlp + 2 * i0) = make_float2(m[p].x, l[p].x);
+      }
+      if (i1 < a.Lq) {
+        str<DH>(ob + (int64_t)i1 * a.o_ls, r1);
+        *reinterpret_cast<float2*>(mlp + 2 * i1) = make_float2(m[p].y, l[p].y);
+      }
+    }
+    return;
+  }
   // l == 0 (every key masked) -> 0/0 = NaN, as the reference's -inf softmax
   const float ik = DROP ? a.inv_keep : 1.f;
 #pragma unroll
@@ -305,14 +335,15 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
   const uint32_t* bitp = DROP ? a.bits + (int64_t)bh * a.nw * a.Lq : nullptr;
   const int wfirst = (kb * KB) >> 5;
   const f2 ik = bc(a.inv_keep);
-  for (int qt = 0; qt < a.Lq; qt += TK) {
+  const int qbeg = blockIdx.y * a.qchunk, qlim = min(a.Lq, qbeg + a.qchunk);
+  for (int qt = qbeg; qt < qlim; qt += TK) {
     __syncthreads();
-    stage<DH, NTT>(Qs, qg, a.q_ls, qt, a.Lq, a.scale_log2);
-    stage<DH, NTT>(Ds_, dg, a.do_ls, qt, a.Lq, 1.f);
+    stage<DH, NTT>(Qs, qg, a.q_ls, qt, qlim, a.scale_log2);
+    stage<DH, NTT>(Ds_, dg, a.do_ls, qt, qlim, 1.f);
     for (int i = threadIdx.x; i < TK; i += NTT) {
       const int qi = qt + i;
       float Di = 0.f, li = INFINITY;
-      if (qi < a.Lq) {
+      if (qi < qlim) {
         float x[DH], y[DH];
         ldr<DH>(dg + (int64_t)qi * a.do_ls, x);
         ldr<DH>(og + (int64_t)qi * a.o_ls, y);
@@ -327,11 +358,11 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
       for (int idx = threadIdx.x; idx < TK * NWB; idx += NTT) {
         const int i = idx / NWB, wv = idx - i * NWB;
         const int qi = qt + i, word = wfirst + wv;
-        Ws[idx] = (qi < a.Lq && word < a.nw) ? bitp[(int64_t)word * a.Lq + qi] : 0u;
+        Ws[idx] = (qi < qlim && word < a.nw) ? bitp[(int64_t)word * a.Lq + qi] : 0u;
       }
     }
     __syncthreads();
-    const int qend = min(TK, a.Lq - qt);
+    const int qend = min(TK, qlim - qt);
     for (int i = 0; i < qend; ++i) {
       float qr[DH], dr[DH];
       lrow<DH>(Qs + i * DH, qr);
@@ -370,12 +401,14 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
     float r0[DH], r1[DH];
 #pragma unroll
     for (int d = 0; d < DH; ++d) { r0[d] = dk[p][d].x * kf; r1[d] = dk[p][d].y * kf; }
-    if (j0 < a.Lk) str<DH>(a.dk + (int64_t)b * a.dk_bs + (int64_t)j0 * a.dk_ls + h * DH, r0);
-    if (j1 < a.Lk) str<DH>(a.dk + (int64_t)b * a.dk_bs + (int64_t)j1 * a.dk_ls + h * DH, r1);
+    float* dkb = a.dk + blockIdx.y * a.dk_ss + (int64_t)b * a.dk_bs + h * DH;
+    float* dvb = a.dv + blockIdx.y * a.dk_ss + (int64_t)b * a.dv_bs + h * DH;
+    if (j0 < a.Lk) str<DH>(dkb + (int64_t)j0 * a.dk_ls, r0);
+    if (j1 < a.Lk) str<DH>(dkb + (int64_t)j1 * a.dk_ls, r1);
 #pragma unroll
     for (int d = 0; d < DH; ++d) { r0[d] = dv[p][d].x; r1[d] = dv[p][d].y; }
-    if (j0 < a.Lk) str<DH>(a.dv + (int64_t)b * a.dv_bs + (int64_t)j0 * a.dv_ls + h * DH, r0);
-    if (j1 < a.Lk) str<DH>(a.dv + (int64_t)b * a.dv_bs + (int64_t)j1 * a.dv_ls + h * DH, r1);
+    if (j0 < a.Lk) str<DH>(dvb + (int64_t)j0 * a.dv_ls, r0);
+    if (j1 < a.Lk) str<DH>(dvb + (int64_t)j1 * a.dv_ls, r1);
   }
 }
 
@@ -432,14 +465,15 @@ __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
   const float* kbg = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
   const uint32_t* bitp = DROP ? a.bits + (int64_t)bh * a.nw * a.Lq : nullptr;
   const f2 ik = bc(DROP ? a.inv_keep : 1.f);
-  for (int kt = 0; kt < a.Lk; kt += TK) {
+  const int kbeg = blockIdx.y * a.kchunk, klim = min(a.Lk, kbeg + a.kchunk);
+  for (int kt = kbeg; kt < klim; kt += TK) {
     __syncthreads();
-    stage<DH, NTT>(Ks, kg, a.k_ls, kt, a.Lk, 1.f);
-    stage<DH, NTT>(Vs, vg, a.v_ls, kt, a.Lk, 1.f);
+    stage<DH, NTT>(Ks, kg, a.k_ls, kt, klim, 1.f);
+    stage<DH, NTT>(Vs, vg, a.v_ls, kt, klim, 1.f);
     for (int i = threadIdx.x; i < TK; i += NTT)
-      Kb[i] = kt + i < a.Lk ? (kbg ? kbg[kt + i] : 0.f) : -INFINITY;
+      Kb[i] = kt + i < klim ? (kbg ? kbg[kt + i] : 0.f) : -INFINITY;
     __syncthreads();
-    const int kend = min(TK, a.Lk - kt);
+    const int kend = min(TK, klim - kt);
     uint32_t w[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) w[u] = 0xffffffffu;
@@ -477,8 +511,9 @@ __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
 #pragma unroll
     for (int d = 0; d < DH; ++d) { r0[d] = dq[p][d].x * a.scale; r1[d] = dq[p][d].y * a.scale; }
     const int i0 = qi[2 * p], i1 = qi[2 * p + 1];
-    if (i0 < a.Lq) str<DH>(a.dq + (int64_t)b * a.dq_bs + (int64_t)i0 * a.dq_ls + h * DH, r0);
-    if (i1 < a.Lq) str<DH>(a.dq + (int64_t)b * a.dq_bs + (int64_t)i1 * a.dq_ls + h * DH, r1);
+    float* dqb = a.dq + blockIdx.y * a.dq_ss + (int64_t)b * a.dq_bs + h * DH;
+    if (i0 < a.Lq) str<DH>(dqb + (int64_t)i0 * a.dq_ls, r0);
+    if (i1 < a.Lq) str<DH>(dqb + (int64_t)i1 * a.dq_ls, r1);
   }
 }
 
@@ -724,6 +759,7 @@ void fill_common(AttnArgs& a, int B, int H, int Lq, int Lk, int dh, float p_drop
   a.thr = drop_thr16(p_drop);
   a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   a.rng_state = rng_state; a.call_id = call_id;
+  a.kchunk = Lk; a.qchunk = Lq;
 }
 
 // Geometry: rows per lane R = 2*NP (NP = 2 amortises each LDS read over four
@@ -739,6 +775,93 @@ Geo pick_geo(int64_t bh, int L) {
       if (bh * ((L + 2 * np * nt - 1) / (2 * np * nt)) >= 1024) return {nt, np};
     }
   return {64, 1};
+}
+
+// Split launches for grids too small to fill the chip (the encoder's 983-token
+// context self-attention: B*H = 64 sequences -> 512 one-wave workgroups): the
+// streamed axis (keys for the forward / dQ, queries for dK / dV) is cut into
+// `n` chunks of a multiple of 64 (= TK and two keep-bitmap words), each chunk a
+// grid row; partial results go to the workspace and a fixed-order combine
+// kernel finishes them (bitwise reproducible).
+struct Split { int n, chunk; };
+Split pick_split(int64_t waves, int L) {
+  Split sp{1, L};
+  if (waves >= 2048 || L < 256) return sp;
+  int n = (int)std::min<int64_t>(16, (4096 + waves - 1) / waves);
+  n = std::min(n, L / 128);
+  if (n <= 1) return sp;
+  sp.chunk = ((L + n - 1) / n + 63) / 64 * 64;
+  sp.n = (L + sp.chunk - 1) / sp.chunk;
+  return sp;
+}
+int64_t waves_of(int64_t bh, int L) {
+  const Geo g = pick_geo(bh, L);
+  return bh * ((L + 2 * g.np * g.nt - 1) / (2 * g.np * g.nt)) * (g.nt / 64);
+}
+
+// o = sum_c o_c 2^(m_c - M) * ik / L,  L = sum_c l_c 2^(m_c - M),  lse = M + log2 L
+template <int DH>
+__global__ void attn_fwd_combine_kernel(const float* __restrict__ po, int64_t o_ss,
+                                        const float* __restrict__ ml, int n, int B, int H, int Lq,
+                                        float ik, float* __restrict__ o, int64_t o_bs,
+                                        int64_t o_ls, float* __restrict__ lse) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t BHL = (int64_t)B * H * Lq;
+  if (t >= BHL) return;
+  const int q = (int)(t % Lq);
+  const int64_t bh = t / Lq;
+  const int h = (int)(bh % H), b = (int)(bh / H);
+  float M = -INFINITY;
+  for (int c = 0; c < n; ++c) M = fmaxf(M, ml[(c * BHL + t) * 2]);
+  const float Mu = M == -INFINITY ? 0.f : M;
+  float L = 0.f, acc[DH];
+#pragma unroll
+  for (int d = 0; d < DH; ++d) acc[d] = 0.f;
+  for (int c = 0; c < n; ++c) {
+    const float w = ex2(ml[(c * BHL + t) * 2] - Mu);
+    L = fmaf(ml[(c * BHL + t) * 2 + 1], w, L);
+    float r[DH];
+    ldr<DH>(po + c * o_ss + ((int64_t)b * Lq + q) * (H * DH) + h * DH, r);
+#pragma unroll
+    for (int d = 0; d < DH; ++d) acc[d] = fmaf(w, r[d], acc[d]);
+  }
+  const float sc = ik / L;   // L == 0 (every key masked): NaN, as the reference
+#pragma unroll
+  for (int d = 0; d < DH; ++d) acc[d] *= sc;
+  str<DH>(o + (int64_t)b * o_bs + (int64_t)q * o_ls + h * DH, acc);
+  lse[t] = M + __log2f(L);
+}
+
+// out[b, l, e] = sum_c ws[c][b, l, e]  (dense [B, L, E] chunks, stride ss)
+__global__ void attn_sum_chunks_kernel(const float* __restrict__ ws, int64_t ss, int n, int B,
+                                       int L, int E, float* __restrict__ out, int64_t bs,
+                                       int64_t ls) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)B * L * E) return;
+  const int e = (int)(t % E);
+  const int64_t bl = t / E;
+  const int l = (int)(bl % L), b = (int)(bl / L);
+  float v = 0.f;
+  for (int c = 0; c < n; ++c) v += ws[c * ss + t];
+  out[(int64_t)b * bs + (int64_t)l * ls + e] = v;
+}
+
+// workspace of a split launch (bytes; 0 = no split for this shape)
+int64_t fwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sp) {
+  sp = {1, Lk};
+  if (Lq <= 2 * SQ) return 0;
+  sp = pick_split(waves_of((int64_t)B * H, Lq), Lk);
+  if (sp.n <= 1) return 0;
+  return (int64_t)sp.n * B * Lq * H * dh + (int64_t)sp.n * B * H * Lq * 2;
+}
+int64_t bwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sq, Split& sk) {
+  sq = {1, Lk};   // dQ: key chunks
+  sk = {1, Lq};   // dK/dV: query chunks
+  if (Lq <= 2 * SQ) return 0;
+  sq = pick_split(waves_of((int64_t)B * H, Lq), Lk);
+  sk = pick_split(waves_of((int64_t)B * H, Lk), Lq);
+  return (int64_t)(sq.n > 1 ? sq.n : 0) * B * Lq * H * dh +
+         (int64_t)(sk.n > 1 ? sk.n : 0) * B * Lk * H * dh * 2;
 }
 
 #define VAESNE_GEO_SWITCH(G, CALL)                                                     \
@@ -759,7 +882,7 @@ Geo pick_geo(int64_t bh, int L) {
   }
 
 template <int DHV>
-int launch_fwd(const AttnArgs& a, float p_drop, hipStream_t s) {
+int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s) {
   if (a.Lq <= 2 * SQ) {
     dim3 grid((unsigned)((int64_t)a.B * a.H), (unsigned)((a.Lq + SQ - 1) / SQ));
     if (p_drop > 0.f)
@@ -769,23 +892,41 @@ int launch_fwd(const AttnArgs& a, float p_drop, hipStream_t s) {
     VAESNE_CHECK_LAUNCH();
     return 0;
   }
+  Split sp;
+  const int64_t wsf = fwd_ws_floats(a.B, a.H, a.Lq, a.Lk, DHV, sp);
+  AttnArgs c = a;
+  if (wsf > 0 && ws) {   // chunked keys: partial o / (m, l) into the workspace
+    c.kchunk = sp.chunk;
+    c.o_out = ws; c.o_bs = (int64_t)a.Lq * a.H * DHV; c.o_ls = (int64_t)a.H * DHV;
+    c.o_ss = (int64_t)a.B * a.Lq * a.H * DHV;
+    c.ml = ws + sp.n * c.o_ss;
+  } else {
+    sp = {1, a.Lk};
+  }
   const Geo g = pick_geo((int64_t)a.B * a.H, a.Lq);
   VAESNE_GEO_SWITCH(g, {
     const int nqb = (a.Lq + 2 * NP * NTT - 1) / (2 * NP * NTT);
-    dim3 grid((unsigned)((int64_t)a.B * a.H * nqb));
+    dim3 grid((unsigned)((int64_t)a.B * a.H * nqb), (unsigned)sp.n);
     if (p_drop > 0.f)
-      hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, true>), grid, dim3(NTT), 0, s, a);
+      hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, true>), grid, dim3(NTT), 0, s, c);
     else
-      hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, a);
+      hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, c);
   })
   VAESNE_CHECK_LAUNCH();
+  if (sp.n > 1) {
+    const int64_t n = (int64_t)a.B * a.H * a.Lq;
+    hipLaunchKernelGGL((attn_fwd_combine_kernel<DHV>), dim3((unsigned)((n + 255) / 256)), dim3(256),
+                       0, s, c.o_out, c.o_ss, c.ml, sp.n, a.B, a.H, a.Lq,
+                       p_drop > 0.f ? a.inv_keep : 1.f, a.o_out, a.o_bs, a.o_ls, a.lse);
+    VAESNE_CHECK_LAUNCH();
+  }
   return 0;
 }
 
 // part: 1 = dK/dV kernel, 2 = dQ kernel, 3 = both (the few-query path is one
 // fused kernel and runs for any nonzero part)
 template <int DHV>
-int launch_bwd(const AttnArgs& a, float p_drop, int part, hipStream_t s) {
+int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t s) {
   if (a.Lq <= 2 * SQ) {
     dim3 grid((unsigned)((int64_t)a.B * a.H));
     if (p_drop > 0.f)
@@ -795,29 +936,64 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, hipStream_t s) {
     VAESNE_CHECK_LAUNCH();
     return 0;
   }
+  Split sq, sk;
+  const int64_t wsf = bwd_ws_floats(a.B, a.H, a.Lq, a.Lk, DHV, sq, sk);
+  if (wsf == 0 || !ws) { sq = {1, a.Lk}; sk = {1, a.Lq}; }
+  const int E = a.H * DHV;
+  float* ws_dq = ws;
+  float* ws_dkv = ws ? ws + (int64_t)(sq.n > 1 ? sq.n : 0) * a.B * a.Lq * E : nullptr;
   if (part & 1) {
+    AttnArgs c = a;
+    if (sk.n > 1) {   // chunked queries: partial dK / dV per chunk
+      c.qchunk = sk.chunk;
+      c.dk = ws_dkv; c.dk_bs = (int64_t)a.Lk * E; c.dk_ls = E;
+      c.dv = ws_dkv + (int64_t)sk.n * a.B * a.Lk * E; c.dv_bs = c.dk_bs; c.dv_ls = E;
+      c.dk_ss = (int64_t)a.B * a.Lk * E;
+    }
     const Geo gk = pick_geo((int64_t)a.B * a.H, a.Lk);
     VAESNE_GEO_SWITCH(gk, {
       const int nkb = (a.Lk + 2 * NP * NTT - 1) / (2 * NP * NTT);
-      dim3 grid((unsigned)((int64_t)a.B * a.H * nkb));
+      dim3 grid((unsigned)((int64_t)a.B * a.H * nkb), (unsigned)sk.n);
       if (p_drop > 0.f)
-        hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, NP, true>), grid, dim3(NTT), 0, s, a);
+        hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, NP, true>), grid, dim3(NTT), 0, s, c);
       else
-        hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, a);
+        hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, c);
     })
     VAESNE_CHECK_LAUNCH();
+    if (sk.n > 1) {
+      const int64_t n = (int64_t)a.B * a.Lk * E;
+      const unsigned nb = (unsigned)((n + 255) / 256);
+      hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3(nb), dim3(256), 0, s, c.dk, c.dk_ss, sk.n,
+                         a.B, a.Lk, E, a.dk, a.dk_bs, a.dk_ls);
+      VAESNE_CHECK_LAUNCH();
+      hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3(nb), dim3(256), 0, s, c.dv, c.dk_ss, sk.n,
+                         a.B, a.Lk, E, a.dv, a.dv_bs, a.dv_ls);
+      VAESNE_CHECK_LAUNCH();
+    }
   }
   if (part & 2) {
+    AttnArgs c = a;
+    if (sq.n > 1) {   // chunked keys: partial dQ per chunk
+      c.kchunk = sq.chunk;
+      c.dq = ws_dq; c.dq_bs = (int64_t)a.Lq * E; c.dq_ls = E;
+      c.dq_ss = (int64_t)a.B * a.Lq * E;
+    }
     const Geo gq = pick_geo((int64_t)a.B * a.H, a.Lq);
     VAESNE_GEO_SWITCH(gq, {
       const int nqb = (a.Lq + 2 * NP * NTT - 1) / (2 * NP * NTT);
-      dim3 grid((unsigned)((int64_t)a.B * a.H * nqb));
+      dim3 grid((unsigned)((int64_t)a.B * a.H * nqb), (unsigned)sq.n);
       if (p_drop > 0.f)
-        hipLaunchKernelGGL((attn_bwd_q_kernel<DHV, NTT, NP, true>), grid, dim3(NTT), 0, s, a);
+        hipLaunchKernelGGL((attn_bwd_q_kernel<DHV, NTT, NP, true>), grid, dim3(NTT), 0, s, c);
       else
-        hipLaunchKernelGGL((attn_bwd_q_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, a);
+        hipLaunchKernelGGL((attn_bwd_q_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, c);
     })
     VAESNE_CHECK_LAUNCH();
+    if (sq.n > 1) {
+      const int64_t n = (int64_t)a.B * a.Lq * E;
+      hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                         c.dq, c.dq_ss, sq.n, a.B, a.Lq, E, a.dq, a.dq_bs, a.dq_ls);
+      VAESNE_CHECK_LAUNCH();
+    }
   }
   return 0;
 }
@@ -836,12 +1012,20 @@ VAESNE_API int64_t vaesne_attn_keep_bits_size(int B, int H, int Lq, int Lk) {
   return (int64_t)B * H * ((Lk + 31) / 32) * Lq * (int64_t)sizeof(uint32_t);
 }
 
+VAESNE_API int64_t vaesne_attn_workspace(int B, int H, int Lq, int Lk, int dh, int bwd) {
+  if (B <= 0 || Lq <= 0 || Lk <= 0) return 0;
+  Split a, b;
+  const int64_t f = bwd ? bwd_ws_floats(B, H, Lq, Lk, dh, a, b) : fwd_ws_floats(B, H, Lq, Lk, dh, a);
+  return f * (int64_t)sizeof(float);
+}
+
 VAESNE_API int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k,
                                int64_t k_bs, int64_t k_ls, const float* v, int64_t v_bs,
                                int64_t v_ls, const float* kbias, int64_t kb_bs, float* o,
                                int64_t o_bs, int64_t o_ls, float* lse, int B, int H, int Lq,
                                int Lk, int dh, float p_drop, const int64_t* rng_state,
-                               uint32_t call_id, uint32_t* keep_bits, void* stream) {
+                               uint32_t call_id, uint32_t* keep_bits, float* workspace,
+                               void* stream) {
   if (B <= 0 || Lq <= 0) return 0;
   if (Lk <= 0 || (dh != 8 && dh != 16)) return (int)hipErrorInvalidValue;
   if (p_drop > 0.f && (!keep_bits || !rng_state)) return (int)hipErrorInvalidValue;
@@ -857,8 +1041,8 @@ VAESNE_API int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const
   a.bits = keep_bits;
   fill_common(a, B, H, Lq, Lk, dh, p_drop, rng_state, call_id);
   hipStream_t s = (hipStream_t)stream;
-  if (dh == 8) return launch_fwd<8>(a, p_drop, s);
-  return launch_fwd<16>(a, p_drop, s);
+  if (dh == 8) return launch_fwd<8>(a, p_drop, workspace, s);
+  return launch_fwd<16>(a, p_drop, workspace, s);
 }
 
 namespace {
@@ -869,7 +1053,7 @@ int attn_bwd_impl(const float* q, int64_t q_bs, int64_t q_ls, const float* k, in
                   int64_t dq_ls, float* dk, int64_t dk_bs, int64_t dk_ls, float* dv,
                   int64_t dv_bs, int64_t dv_ls, int B, int H, int Lq, int Lk, int dh,
                   float p_drop, const int64_t* rng_state, uint32_t call_id,
-                  const uint32_t* keep_bits, int part, void* stream) {
+                  const uint32_t* keep_bits, float* workspace, int part, void* stream) {
   if (B <= 0 || Lq <= 0) return 0;
   if (Lk <= 0 || (dh != 8 && dh != 16)) return (int)hipErrorInvalidValue;
   // query-tiled kernels read the forward's keep bitmap; the few-query kernel
@@ -893,8 +1077,8 @@ int attn_bwd_impl(const float* q, int64_t q_bs, int64_t q_ls, const float* k, in
   a.bits = const_cast<uint32_t*>(keep_bits);
   fill_common(a, B, H, Lq, Lk, dh, p_drop, rng_state, call_id);
   hipStream_t s = (hipStream_t)stream;
-  if (dh == 8) return launch_bwd<8>(a, p_drop, part, s);
-  return launch_bwd<16>(a, p_drop, part, s);
+  if (dh == 8) return launch_bwd<8>(a, p_drop, part, workspace, s);
+  return launch_bwd<16>(a, p_drop, part, workspace, s);
 }
 }  // namespace
 
@@ -905,11 +1089,11 @@ int attn_bwd_impl(const float* q, int64_t q_bs, int64_t q_ls, const float* k, in
       int64_t do_bs, int64_t do_ls, float *dq, int64_t dq_bs, int64_t dq_ls, float *dk,       \
       int64_t dk_bs, int64_t dk_ls, float *dv, int64_t dv_bs, int64_t dv_ls, int B, int H,    \
       int Lq, int Lk, int dh, float p_drop, const int64_t *rng_state, uint32_t call_id,       \
-      const uint32_t *keep_bits
+      const uint32_t *keep_bits, float *workspace
 #define VAESNE_ATTN_BWD_ARGS                                                                    \
   q, q_bs, q_ls, k, k_bs, k_ls, v, v_bs, v_ls, kbias, kb_bs, o, o_bs, o_ls, lse, dout, do_bs,  \
       do_ls, dq, dq_bs, dq_ls, dk, dk_bs, dk_ls, dv, dv_bs, dv_ls, B, H, Lq, Lk, dh, p_drop,   \
-      rng_state, call_id, keep_bits
+      rng_state, call_id, keep_bits, workspace
 
 VAESNE_API int vaesne_attn_bwd(VAESNE_ATTN_BWD_PARAMS, void* stream) {
   return attn_bwd_impl(VAESNE_ATTN_BWD_ARGS, 3, stream);
