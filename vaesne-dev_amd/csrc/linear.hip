@@ -250,39 +250,45 @@ int64_t wgrad_groups(int64_t M) {
   return g < 1 ? 1 : g;
 }
 
-__global__ __launch_bounds__(NT) void linear_wgrad_kernel(WgtArgs p, int nib) {
+// ACT: activation whose derivative scales dy (0 none, 1 relu, 2 gelu); X2: x := x + x2.
+// Loads are unconditional (rows / columns clamped) so all 16 x 2 of a chunk are
+// in flight at once; out-of-range terms are zeroed afterwards.  With G == 1
+// (gridDim.x) the workgroup writes dW / db directly (no column-sum pass).
+template <int ACT, bool X2>
+__global__ __launch_bounds__(NT) void linear_wgrad_kernel(WgtArgs p, int nib, float* dW, float* db,
+                                                          int accum) {
   __shared__ float red[NT / 64][1024 + 32];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 31, hh = lane >> 5;
   const int ob = blockIdx.y / nib, ib = blockIdx.y - ob * nib;
   const int o = ob * 32 + col, i = ib * 32 + col;
   const bool oin = o < p.O, iin = i < p.I;
+  const int oc = min(o, p.O - 1), ic = min(i, p.I - 1);
   f16v acc = {};
   float cs = 0.f;
   const int64_t chunks = (p.M + 31) / 32;
   for (int64_t ch = (int64_t)blockIdx.x * (NT / 64) + wave; ch < chunks;
        ch += (int64_t)gridDim.x * (NT / 64)) {
-    float gv[16], xv[16];
+    float gv[16], zv[16], xv[16], x2v[16];
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2) {
-      const int64_t r = ch * 32 + 2 * s2 + hh;
-      float gg = 0.f, xx = 0.f;
-      if (r < p.M) {
-        if (oin) {
-          gg = p.dy[r * p.lddy + o];
-          if (p.act) gg *= act_grad(p.act, p.z[r * p.ldz + o]);
-        }
-        if (iin) {
-          xx = p.x[r * p.ldx + i];
-          if (p.x2) xx += p.x2[r * p.ldx2 + i];
-        }
-      }
-      gv[s2] = gg;
-      xv[s2] = xx;
-      cs += gg;
+      const int64_t r = min(ch * 32 + 2 * s2 + hh, p.M - 1);
+      gv[s2] = p.dy[r * p.lddy + oc];
+      if (ACT) zv[s2] = p.z[r * p.ldz + oc];
+      xv[s2] = p.x[r * p.ldx + ic];
+      if (X2) x2v[s2] = p.x2[r * p.ldx2 + ic];
     }
 #pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2) acc = mfma(gv[s2], xv[s2], acc);
+    for (int s2 = 0; s2 < 16; ++s2) {
+      const bool ok = ch * 32 + 2 * s2 + hh < p.M;
+      float gg = gv[s2], xx = xv[s2];
+      if (ACT) gg *= act_grad(ACT, zv[s2]);
+      if (X2) xx += x2v[s2];
+      gg = (ok && oin) ? gg : 0.f;
+      xx = (ok && iin) ? xx : 0.f;
+      cs += gg;
+      acc = mfma(gg, xx, acc);
+    }
   }
   cs += __shfl_xor(cs, 32, 64);
 #pragma unroll
@@ -290,6 +296,7 @@ __global__ __launch_bounds__(NT) void linear_wgrad_kernel(WgtArgs p, int nib) {
   if (hh == 0) red[wave][1024 + col] = cs;
   __syncthreads();
   // partial layout [G][O*I (dW) | O (db)] so one column-sum splits at O*I
+  const bool direct = gridDim.x == 1;
   float* out = p.partial + (int64_t)blockIdx.x * ((int64_t)p.O * p.I + p.O);
   for (int e = threadIdx.x; e < 1024 + 32; e += NT) {
     float v = red[0][e];
@@ -297,10 +304,17 @@ __global__ __launch_bounds__(NT) void linear_wgrad_kernel(WgtArgs p, int nib) {
     for (int w = 1; w < NT / 64; ++w) v += red[w][e];
     if (e < 1024) {
       const int oo = ob * 32 + (e >> 5), ii = ib * 32 + (e & 31);
-      if (oo < p.O && ii < p.I) out[(int64_t)oo * p.I + ii] = v;
+      if (oo < p.O && ii < p.I) {
+        const int64_t f = (int64_t)oo * p.I + ii;
+        if (!direct) out[f] = v;
+        else if (dW) dW[f] = accum ? dW[f] + v : v;
+      }
     } else if (ib == 0) {
       const int oo = ob * 32 + (e - 1024);
-      if (oo < p.O) out[(int64_t)p.O * p.I + oo] = v;
+      if (oo < p.O) {
+        if (!direct) out[(int64_t)p.O * p.I + oo] = v;
+        else if (db) db[oo] = accum ? db[oo] + v : v;
+      }
     }
   }
 }
@@ -358,8 +372,15 @@ VAESNE_API int vaesne_linear_bwd_weight(const float* dy, int64_t lddy, const flo
     G = (int)wgrad_groups(M);
     WgtArgs p{dy, lddy, z, ldz, act, x, ldx, x2, ldx2, M, O, I, workspace};
     const int nob = (O + 31) / 32, nib = (I + 31) / 32;
-    hipLaunchKernelGGL(linear_wgrad_kernel, dim3(G, nob * nib), dim3(NT), 0, s, p, nib);
+    const dim3 grid(G, nob * nib);
+#define VAESNE_WG(A, X)                                                                           \
+  hipLaunchKernelGGL((linear_wgrad_kernel<A, X>), grid, dim3(NT), 0, s, p, nib, dW, db, accum)
+    if (act == ACT_RELU) { if (x2) VAESNE_WG(ACT_RELU, true); else VAESNE_WG(ACT_RELU, false); }
+    else if (act == ACT_GELU) { if (x2) VAESNE_WG(ACT_GELU, true); else VAESNE_WG(ACT_GELU, false); }
+    else { if (x2) VAESNE_WG(ACT_NONE, true); else VAESNE_WG(ACT_NONE, false); }
+#undef VAESNE_WG
     VAESNE_CHECK_LAUNCH();
+    if (G == 1) return 0;   // written directly
   }
   return launch_colsum(workspace, G, F, dW, db, O * I, accum, s);
 }
