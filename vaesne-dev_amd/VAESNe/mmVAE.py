@@ -1,10 +1,54 @@
 """Mixture-of-experts multimodal VAE over (light curve, spectrum) pairs,
 MI355X build (reference: mmVAE.py:71-132, photospecMMVAE)."""
+import contextlib
+import os
+
 import torch
 import torch.distributions as dist
 import torch.nn as nn
 
 from . import _ops
+
+
+_SIDE = {}
+
+
+def _side_stream(t):
+    """A second HIP stream for the photometry branch (VAESNE_STREAMS=0 turns it off)."""
+    if not t.is_cuda or os.environ.get("VAESNE_STREAMS", "1") == "0":
+        return None
+    dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
+    st = _SIDE.get(dev)
+    if st is None:
+        st = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return st
+
+
+class _Branches:
+    """Run branch 0 (photometry) on a side stream and branch 1 (spectra) on the
+    current stream, then join.  The photometry encoder / decoder are chains of
+    small latency-bound kernels; beside the spectra work they cost ~nothing.
+    Host order (and so RNG call ids / injected noise order) is unchanged, and
+    autograd replays each branch's backward on the stream its forward used."""
+
+    def __init__(self, side):
+        self.side = side
+        self.main = torch.cuda.current_stream() if side is not None else None
+
+    def __enter__(self):
+        if self.side is not None:
+            self.side.wait_stream(self.main)
+        return self
+
+    def on(self, branch):
+        if self.side is None or branch != 0:
+            return contextlib.nullcontext()
+        return torch.cuda.stream(self.side)
+
+    def __exit__(self, *exc):
+        if self.side is not None:
+            self.main.wait_stream(self.side)
+        return False
 
 
 class _CellMatrix(list):
@@ -47,18 +91,23 @@ class photospecMMVAE(nn.Module):
         decoder calls).  px_zs cells are views of those [K, 2B, L] tensors;
         `px_zs.merged` lets the fused m_iwae read them in place."""
         n = len(self.vaes)
-        qz_xs, zss = [], []
-        for m, vae in enumerate(self.vaes):
-            qz_x, zs = vae.posterior(x[m], K=K)
-            qz_xs.append(qz_x)
-            zss.append(zs)
+        side = _side_stream(x[0][0]) if n == 2 else None
+        qz_xs, zss = [None] * n, [None] * n
+        with _Branches(side) as br:
+            for m, vae in enumerate(self.vaes):
+                with br.on(m):
+                    qz_xs[m], zss[m] = vae.posterior(x[m], K=K)
         px_zs = _CellMatrix([[None for _ in range(n)] for _ in range(n)])
         if all(z.shape == zss[0].shape for z in zss):
             B = zss[0].shape[1]
             zcat = torch.cat(zss, dim=1)
+            px_zs.merged = [None] * n
+            with _Branches(side) as br:
+                for d, vae in enumerate(self.vaes):
+                    with br.on(d):
+                        px_zs.merged[d] = vae.decode_params(zcat, x[d], groups=n)
             for d, vae in enumerate(self.vaes):
-                loc, scale = vae.decode_params(zcat, x[d], groups=n)
-                px_zs.merged.append((loc, scale))
+                loc, scale = px_zs.merged[d]
                 for e in range(n):
                     px_zs[e][d] = vae._dist(vae.px_z, loc[:, e * B:(e + 1) * B],
                                             scale[:, e * B:(e + 1) * B])
