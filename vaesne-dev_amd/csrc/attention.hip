@@ -20,6 +20,8 @@
 //     of re-hashing;
 //   * D = rowsum(dO * O) is computed by the query-tile loaders (no pre-pass).
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -768,6 +770,12 @@ void fill_common(AttnArgs& a, int B, int H, int Lq, int Lk, int dh, float p_drop
 // CU); the small encoder grids (B*H = 64) fall through to NP=1 / 64 threads.
 struct Geo { int nt, np; };
 Geo pick_geo(int64_t bh, int L) {
+  static const Geo forced = [] {   // tuning hook: VAESNE_ATTN_GEO="nt,np" (np in 1, 2)
+    Geo f{0, 0};
+    if (const char* e = getenv("VAESNE_ATTN_GEO")) sscanf(e, "%d,%d", &f.nt, &f.np);
+    return f;
+  }();
+  if (forced.nt > 0) return forced;
   const int nts[3] = {256, 128, 64};
   for (int np = 2; np >= 1; --np)
     for (int i = 0; i < 3; ++i) {
