@@ -336,12 +336,13 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
   const float* lg = a.lse + (int64_t)bh * a.Lq;
   const uint32_t* bitp = DROP ? a.bits + (int64_t)bh * a.nw * a.Lq : nullptr;
   const int wfirst = (kb * KB) >> 5;
-  const f2 ik = bc(a.inv_keep);
+  // dO is staged pre-multiplied by 1/(1-p): dV = sum keep*P*dO/(1-p) and
+  // dP = keep * (V . dO)/(1-p) come out scaled; D = rowsum(dO*O) uses the raw dO.
   const int qbeg = blockIdx.y * a.qchunk, qlim = min(a.Lq, qbeg + a.qchunk);
   for (int qt = qbeg; qt < qlim; qt += TK) {
     __syncthreads();
     stage<DH, NTT>(Qs, qg, a.q_ls, qt, qlim, a.scale_log2);
-    stage<DH, NTT>(Ds_, dg, a.do_ls, qt, qlim, 1.f);
+    stage<DH, NTT>(Ds_, dg, a.do_ls, qt, qlim, a.inv_keep);
     for (int i = threadIdx.x; i < TK; i += NTT) {
       const int qi = qt + i;
       float Di = 0.f, li = INFINITY;
@@ -365,6 +366,7 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
     }
     __syncthreads();
     const int qend = min(TK, qlim - qt);
+#pragma unroll 2
     for (int i = 0; i < qend; ++i) {
       float qr[DH], dr[DH];
       lrow<DH>(Qs + i * DH, qr);
@@ -383,8 +385,8 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
         f2 aP = pr, dP = g;
         if (DROP) {
           const uint32_t m0 = (kw >> (2 * p)) & 1u, m1 = (kw >> (2 * p + 1)) & 1u;
-          aP = sel2(m0, m1, pr * ik);
-          dP = sel2(m0, m1, g * ik);
+          aP = sel2(m0, m1, pr);
+          dP = sel2(m0, m1, g);
         }
         const f2 dS = pr * (dP - Di);
 #pragma unroll
@@ -466,12 +468,12 @@ __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
   const float* vg = a.v + (int64_t)b * a.v_bs + h * DH;
   const float* kbg = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
   const uint32_t* bitp = DROP ? a.bits + (int64_t)bh * a.nw * a.Lq : nullptr;
-  const f2 ik = bc(DROP ? a.inv_keep : 1.f);
+  // V staged pre-multiplied by 1/(1-p): t = dO . V/(1-p) is the kept-score dP
   const int kbeg = blockIdx.y * a.kchunk, klim = min(a.Lk, kbeg + a.kchunk);
   for (int kt = kbeg; kt < klim; kt += TK) {
     __syncthreads();
     stage<DH, NTT>(Ks, kg, a.k_ls, kt, klim, 1.f);
-    stage<DH, NTT>(Vs, vg, a.v_ls, kt, klim, 1.f);
+    stage<DH, NTT>(Vs, vg, a.v_ls, kt, klim, DROP ? a.inv_keep : 1.f);
     for (int i = threadIdx.x; i < TK; i += NTT)
       Kb[i] = kt + i < klim ? (kbg ? kbg[kt + i] : 0.f) : -INFINITY;
     __syncthreads();
@@ -499,7 +501,7 @@ __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
           t = fma2(g[p][d], bc(vr[d]), t);
         }
         const f2 pr = ex2(sc - lse[p]);
-        f2 dP = t * ik;
+        f2 dP = t;
         if (DROP) dP = sel2((w[2 * p] >> s) & 1u, (w[2 * p + 1] >> s) & 1u, dP);
         const f2 dS = pr * (dP - D[p]);
 #pragma unroll
