@@ -139,6 +139,30 @@ class Step:
             g2.replay()
 
 
+def throughput_point(device, B, use_graph, steps=10, warmup=3):
+    """The same cfg-5 step at a larger per-GPU batch (a capacity point beside
+    the reference-batch `value`; not the headline metric)."""
+    torch.manual_seed(1)
+    model = make_model(device, CFG["dropout"])
+    x = synthetic_batch(B, 4321, device)
+    step = Step(model, x, device, 1, use_graph=use_graph)
+    if use_graph:
+        step.capture()
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(device)
+    dt = (time.perf_counter() - t0) / steps
+    loss = step.loss.item()
+    del step, model, x
+    torch.cuda.empty_cache()
+    return dict(per_gpu_batch=B, value=round(B / dt, 2), unit="SN pairs/s", ms_per_step=round(dt * 1e3, 3),
+                steps=steps, finite_loss=math.isfinite(loss))
+
+
 def time_kernel(fn, iters, device):
     """Average duration of fn's launches, HIP events on the stream they run on."""
     s = torch.cuda.Stream(device)
@@ -166,6 +190,7 @@ def roofline(device, B):
     kernels must do it."""
     from VAESNe import _lib, rng
     N, L, E, H, dh = 2 * CFG["K"] * B, CFG["Ls"], CFG["model_dim"], CFG["num_heads"], 8
+    pd = float(os.environ.get("VAESNE_ROOFLINE_PDROP", CFG["dropout"]))   # A/B studies only
     qkv = torch.randn(N, L, 3 * E, device=device)
     mask = (torch.rand(N, L, device=device) < 0.05)
     mask[:, 0] = False
@@ -181,14 +206,14 @@ def roofline(device, B):
 
     def fwd():
         lib.attn_fwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E, kbias.data_ptr(), L,
-                     o.data_ptr(), L * E, E, lse.data_ptr(), N, H, L, L, dh, 0.1, st.data_ptr(), 7,
+                     o.data_ptr(), L * E, E, lse.data_ptr(), N, H, L, L, dh, pd, st.data_ptr(), 7,
                      bits.data_ptr(), None, _lib.stream())
 
     def bwd(fn):
         return lambda: fn(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E,
                           kbias.data_ptr(), L, o.data_ptr(), L * E, E, lse.data_ptr(),
                           do.data_ptr(), L * E, E, d, s3, 3 * E, d + 4 * E, s3, 3 * E, d + 8 * E,
-                          s3, 3 * E, N, H, L, L, dh, 0.1, st.data_ptr(), 7, bits.data_ptr(),
+                          s3, 3 * E, N, H, L, L, dh, pd, st.data_ptr(), 7, bits.data_ptr(),
                           None, _lib.stream())
 
     fwd()
@@ -292,6 +317,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--throughput-batch", type=int, default=64,
+                    help="also time the same step at this per-GPU batch (N=1 only; 0 = skip)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the roofline kernel launches (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
@@ -371,6 +398,8 @@ def main():
             log(f"[bench] elbo_rel_err failed: {e!r}")
         if not args.no_roofline:
             out["roofline"] = roofline(device, args.batch)
+        if world == 1 and args.throughput_batch > 0:
+            out["throughput_batch"] = throughput_point(device, args.throughput_batch, not args.no_graph)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
