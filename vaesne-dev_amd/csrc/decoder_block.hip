@@ -554,28 +554,38 @@ constexpr int OFF_WO1 = 0, OFF_WQ = 1024, OFF_WO2 = 2048, OFF_W1 = 3072, OFF_W2 
               OFF_BE2 = 8544, OFF_G3 = 8576, OFF_BE3 = 8608, WPART = 8640;
 
 // acc[o][k] += sum_t G[t][o] X[t][k] over the wave's 32 tokens (rows r0..r0+31,
-// rows >= rmax contribute 0); operands read straight from L2 / HBM
-__device__ __forceinline__ void wg_tile(const float* G, int ldg, const float* X, int ldx,
-                                        int64_t r0, int64_t rmax, f16v& acc, int lane) {
+// rows >= rmax contribute 0); operands read straight from L2 / HBM, all 32 loads
+// issued before the MFMAs; returns this lane's share of the column sum of G
+// (rows of parity h; the caller adds the other half-wave)
+__device__ __forceinline__ float wg_tile(const float* G, int ldg, const float* X, int ldx,
+                                         int64_t r0, int64_t rmax, f16v& acc, int lane) {
   const int c = lane & 31, h = lane >> 5;
+  float g[16], x[16];
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
-    const int64_t t = r0 + 2 * s + h;
-    const bool ok = t < rmax;
-    const float g = ok ? G[t * ldg + c] : 0.f;
-    const float x = ok ? X[t * ldx + c] : 0.f;
-    acc = mfma(g, x, acc);
+    const int64_t t = min(r0 + 2 * s + h, rmax - 1);
+    g[s] = G[t * ldg + c];
+    x[s] = X[t * ldx + c];
   }
+  float cs = 0.f;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const bool ok = r0 + 2 * s + h < rmax;
+    const float gg = ok ? g[s] : 0.f;
+    cs += gg;
+    acc = mfma(gg, ok ? x[s] : 0.f, acc);
+  }
+  return cs;
 }
 __device__ __forceinline__ float cs_tile(const float* G, int ldg, int64_t r0, int64_t rmax,
                                          int lane) {
   const int c = lane & 31, h = lane >> 5;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = G[min(r0 + 16 * h + i, rmax - 1) * ldg + c];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int64_t t = r0 + 16 * h + i;
-    s += t < rmax ? G[t * ldg + c] : 0.f;
-  }
+  for (int i = 0; i < 16; ++i) s += r0 + 16 * h + i < rmax ? v[i] : 0.f;
   return s;
 }
 
@@ -636,10 +646,9 @@ __global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __rest
   }
   f16v acc = {};
   float cs = 0.f;
-  for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32) {
-    wg_tile(G, ldg, X, E, base + tt, rmax, acc, lane);
-    if (boff >= 0) cs += cs_tile(G, ldg, base + tt, rmax, lane);
-  }
+#pragma unroll 2
+  for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32)
+    cs += wg_tile(G, ldg, X, E, base + tt, rmax, acc, lane);
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[wave * 1024 + F(r, h) * 32 + (lane & 31)] = acc[r];
   __syncthreads();
