@@ -28,7 +28,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(ROOT, "vaesne-dev_amd"))
+sys.path.insert(0, os.environ.get("VAESNE_PKG_DIR", os.path.join(ROOT, "vaesne-dev_amd")))   # A/B
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402

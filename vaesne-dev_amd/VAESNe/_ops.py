@@ -615,37 +615,49 @@ def _tail_layout():
 
 
 class DecTailFn(torch.autograd.Function):
-    """(x, O, kvc, 16-18 weights) -> (y [, qkv_next]) for one decoder block."""
+    """(x, O, context, cross in_proj Wc [96, 32] / bc [96], 16 more block tensors)
+    -> (y [, qkv_next]) for one decoder block.  The context's k|v projection
+    (rows [E, 3E) of Wc) runs inside, and the whole in_proj gradient is returned
+    as one tensor: no slice-gradient zero-fill / copy / add glue per block."""
 
     @staticmethod
-    def forward(ctx, L, p, x, O, kvc, *w):
-        _lib.require_device(x, O, kvc)
-        x, O, kvc = x.contiguous(), O.contiguous(), kvc.contiguous()
-        M = x.numel() // 32
-        Lc = kvc.shape[1]
-        w = [None if t is None else t.contiguous() for t in w]
+    def forward(ctx, L, p, x, O, context, Wc, bc, *w16):
+        _lib.require_device(x, O, context, Wc, bc)
+        x, O, context = x.contiguous(), O.contiguous(), context.contiguous()
+        Wc, bc = Wc.contiguous(), bc.contiguous()
+        E = 32
+        M = x.numel() // E
+        Nseq, Lc = context.shape[0], context.shape[1]
+        dev = x.device
+        # kvc = context @ Wc[E:]^T + bc[E:]   ([Nseq, Lc, 64]; the reference's cross k/v proj)
+        kvc = torch.empty((Nseq, Lc, 2 * E), dtype=torch.float32, device=dev)
+        lib.linear_fwd(context.data_ptr(), E, None, 0, Nseq * Lc, E, Wc.data_ptr() + 4 * E * E,
+                       bc.data_ptr() + 4 * E, 2 * E, kvc.data_ptr(), 2 * E, None, 0, 0, 0, stream())
+        w16 = [None if t is None else t.contiguous() for t in w16]
+        w = w16[:4] + [Wc, bc] + w16[4:]          # C-ABI order: Wq/bq = rows [0, E) of Wc/bc
         nxt = w[16] is not None
-        y = torch.empty((M, 32), dtype=torch.float32, device=x.device)
-        qkv = torch.empty((M, 96), dtype=torch.float32, device=x.device) if nxt else None
-        st = rng.state(x.device) if p > 0 else None
+        y = torch.empty((M, E), dtype=torch.float32, device=dev)
+        qkv = torch.empty((M, 3 * E), dtype=torch.float32, device=dev) if nxt else None
+        st = rng.state(dev) if p > 0 else None
         cid = rng.next_call_id() if p > 0 else 0
         lib.dec_tail_fwd(x.data_ptr(), O.data_ptr(), kvc.data_ptr(), M, L, Lc, _lib.ptr_array(w),
                          float(p), ptr(st), cid, y.data_ptr(), ptr(qkv), stream())
         ctx.meta = (M, L, Lc, float(p), cid, nxt, x.shape)
-        ctx.save_for_backward(x, O, kvc, y, st, *w)
+        ctx.save_for_backward(x, O, context, kvc, y, st, *w)
         y = y.view(x.shape)
         if nxt:
-            return y, qkv.view(*x.shape[:-1], 96)
+            return y, qkv.view(*x.shape[:-1], 3 * E)
         return y, None
 
     @staticmethod
     def backward(ctx, dy, dqkv):
-        x, O, kvc, y, st, *w = ctx.saved_tensors
+        x, O, context, kvc, y, st, *w = ctx.saved_tensors
         M, L, Lc, p, cid, nxt, xshape = ctx.meta
+        E = 32
         dev = x.device
         dy = torch.zeros_like(y) if dy is None else dy.contiguous()
         if nxt:
-            dqkv = torch.zeros((M, 96), dtype=torch.float32, device=dev) if dqkv is None \
+            dqkv = torch.zeros((M, 3 * E), dtype=torch.float32, device=dev) if dqkv is None \
                 else dqkv.contiguous()
         else:
             dqkv = None
@@ -655,10 +667,26 @@ class DecTailFn(torch.autograd.Function):
         offs, total = _tail_layout()
         gflat = torch.empty(total, dtype=torch.float32, device=dev)
         ws = _ws(lib.dec_tail_workspace(M, L, Lc), dev)
+        s = stream()
         lib.dec_tail_bwd(x.data_ptr(), O.data_ptr(), kvc.data_ptr(), M, L, Lc, _lib.ptr_array(w),
                          p, ptr(st), cid, y.data_ptr(), dy.data_ptr(), ptr(dqkv), dx.data_ptr(),
-                         dO.data_ptr(), dkvc.data_ptr(), gflat.data_ptr(), ws.data_ptr(), stream())
-        ng = ctx.needs_input_grad[5:]
-        gw = [gflat[o:o + t.numel()].view_as(t) if (t is not None and ng[i]) else None
-              for i, (t, o) in enumerate(zip(w, offs))]
-        return (None, None, dx.view(xshape), dO, dkvc, *gw)
+                         dO.data_ptr(), dkvc.data_ptr(), gflat.data_ptr(), ws.data_ptr(), s)
+        Wc = w[4]
+        Mc = context.shape[0] * Lc
+        # full in_proj gradient: rows [0, E) from the tail, rows [E, 3E) from the k|v proj
+        dWc = torch.empty_like(Wc)
+        dbc = torch.empty_like(w[5])
+        lib.pack(_lib.ptr_array([dWc, dbc]), (C.c_int64 * 2)(offs[4], offs[5]),
+                 (C.c_int64 * 2)(E * E, E), 2, gflat.data_ptr(), 1, s)
+        wsk = _ws(lib.linear_bwd_weight_workspace(Mc, 2 * E, E), dev)
+        lib.linear_bwd_weight(dkvc.data_ptr(), 2 * E, None, 0, 0, context.data_ptr(), E, None, 0,
+                              Mc, 2 * E, E, dWc.data_ptr() + 4 * E * E, dbc.data_ptr() + 4 * E, 0,
+                              wsk.data_ptr(), s)
+        dctx = torch.empty_like(context)
+        lib.linear_bwd_data(dkvc.data_ptr(), 2 * E, None, 0, 0, Mc, 2 * E,
+                            Wc.data_ptr() + 4 * E * E, E, dctx.data_ptr(), E, 0, s)
+        ng = ctx.needs_input_grad
+        gw = [gflat[o:o + t.numel()].view_as(t) if (t is not None and ng[7 + j]) else None
+              for j, (t, o) in enumerate(zip(w[:4] + w[6:], offs[:4] + offs[6:]))]
+        return (None, None, dx.view(xshape), dO, dctx, dWc if ng[5] else None,
+                dbc if ng[6] else None, *gw)

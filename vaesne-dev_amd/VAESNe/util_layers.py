@@ -218,13 +218,11 @@ def decoder_stack(blocks, x, context, mask=None):
         p_attn = blk.self_attn.dropout if blk.training else 0.0
         p = blk.dropout.p if blk.training else 0.0
         O = _ops.self_attention(qkv, None, blk.self_attn.num_heads, p_attn, kbias=kbias)
-        Wc, bc = blk.cross_attn.in_proj_weight, blk.cross_attn.in_proj_bias
-        kvc = _ops.linear(context, Wc[E:], bc[E:])
         nxt = blocks[i + 1].self_attn if i + 1 < len(blocks) else None
         x, qkv = _ops.DecTailFn.apply(
-            L, p, x, O, kvc,
+            L, p, x, O, context, blk.cross_attn.in_proj_weight, blk.cross_attn.in_proj_bias,
             blk.self_attn.out_proj.weight, blk.self_attn.out_proj.bias,
-            blk.layernorm1.weight, blk.layernorm1.bias, Wc[:E], bc[:E],
+            blk.layernorm1.weight, blk.layernorm1.bias,
             blk.cross_attn.out_proj.weight, blk.cross_attn.out_proj.bias,
             blk.layernorm2.weight, blk.layernorm2.bias,
             blk.ffn[0].weight, blk.ffn[0].bias, blk.ffn[2].weight, blk.ffn[2].bias,
