@@ -717,7 +717,7 @@ Tail make(const float* x, const float* O, const float* kvc, int M, int L, int Lc
   a.p_drop = p_drop; a.thr = drop_thr16(p_drop);
   a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   a.rng = rng; a.call_id = call_id;
-  a.chunk = L <= 256 ? ((L + 127) / 128) * 128 : 256;
+  a.chunk = L <= 256 ? ((L + 127) / 128) * 128 : 512;
   return a;
 }
 
@@ -729,7 +729,7 @@ bool shapes_ok(int M, int L, int Lc) {
 
 VAESNE_API int64_t vaesne_dec_tail_workspace(int M, int L, int Lc) {
   if (!shapes_ok(M, L, Lc)) return 0;
-  const int chunk = L <= 256 ? ((L + 127) / 128) * 128 : 256;
+  const int chunk = L <= 256 ? ((L + 127) / 128) * 128 : 512;
   const int chunks = (L + chunk - 1) / chunk;
   const int64_t G = (int64_t)(M / L) * chunks;
   return (G * WPART + (int64_t)chunks * (M / L) * Lc * 2 * E + (int64_t)NVEC * M * E) *
