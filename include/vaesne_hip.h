@@ -137,16 +137,20 @@ int vaesne_attn_bwd_q(const float* q, int64_t q_bs, int64_t q_ls, const float* k
  * bwd: gflat = ONE device buffer receiving every parameter gradient of the
  * block at the offsets vaesne_dec_tail_grad_layout() reports (same order as w;
  * returns the buffer length, 8640 floats); y = the forward output; dqkv
- * required iff Wn; workspace sized by vaesne_dec_tail_workspace. */
+ * required iff Wn; workspace sized by vaesne_dec_tail_workspace.
+ * drop_masks (nullable, p_drop > 0): uint32 [M][4] keep masks of the block's four
+ * dropout sites, written by the forward and read by the backward instead of
+ * re-hashing (16 bytes per token). */
 int64_t vaesne_dec_tail_workspace(int M, int L, int Lc);
 int vaesne_dec_tail_fwd(const float* x, const float* O, const float* kvc, int M, int L, int Lc,
                         const float* const* w, float p_drop, const int64_t* rng_state,
-                        uint32_t call_id, float* y, float* qkv, void* stream);
+                        uint32_t call_id, float* y, float* qkv, uint32_t* drop_masks,
+                        void* stream);
 int vaesne_dec_tail_bwd(const float* x, const float* O, const float* kvc, int M, int L, int Lc,
                         const float* const* w, float p_drop, const int64_t* rng_state,
                         uint32_t call_id, const float* y, const float* dy, const float* dqkv,
-                        float* dx, float* dO, float* dkvc, float* gflat, float* workspace,
-                        void* stream);
+                        const uint32_t* drop_masks, float* dx, float* dO, float* dkvc,
+                        float* gflat, float* workspace, void* stream);
 int vaesne_dec_tail_grad_layout(int* offsets);
 
 /* ---- embeddings ------------------------------------------------------------

@@ -383,3 +383,36 @@ def test_fused_decoder_tail_dropout_fwd_bwd_consistent():
         rng._call = 500
         o1 = decoder_stack(blocks, x, ctx, None)
     assert (o1 - o2).abs().max().item() > 1e-3
+
+
+def test_fused_decoder_tail_stored_masks_match_rehash():
+    """The tail backward reading the forward's stored dropout masks gives the
+    same gradients, bit for bit, as re-hashing them from the counter RNG."""
+    from VAESNe import _ops, rng
+    from VAESNe.util_layers import decoder_stack
+    blocks = _decoder_blocks(2, 5).to(DEV)
+    for b in blocks:
+        b.dropout.p = 0.2
+        b.self_attn.dropout = 0.2
+        b.cross_attn.dropout = 0.2
+    blocks.train()
+    g = torch.Generator().manual_seed(12)
+    N, L, Lc = 3, 333, 7                      # ragged chunk tail, Lc < LCMAX
+    x = torch.randn(N, L, 32, generator=g).to(DEV)
+    ctx = torch.randn(N, Lc, 32, generator=g).to(DEV)
+    go = torch.randn(N, L, 32, generator=g).to(DEV)
+    res = []
+    for store in (True, False):
+        _ops.STORE_TAIL_MASKS = store
+        try:
+            rng._call = 700
+            blocks.zero_grad(set_to_none=True)
+            xx = x.clone().requires_grad_(True)
+            cc = ctx.clone().requires_grad_(True)
+            out = decoder_stack(blocks, xx, cc, None)
+            (out * go).sum().backward()
+            res.append([out, xx.grad, cc.grad] + [p.grad.clone() for p in blocks.parameters()])
+        finally:
+            _ops.STORE_TAIL_MASKS = True
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

@@ -49,9 +49,9 @@ SIGNATURES = {
     "vaesne_attn_bwd_kv": _ATTN_BWD,
     "vaesne_attn_bwd_q": _ATTN_BWD,
     "vaesne_dec_tail_workspace": (I64, [I32, I32, I32]),
-    "vaesne_dec_tail_fwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P]),
+    "vaesne_dec_tail_fwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P, P]),
     "vaesne_dec_tail_bwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P, P, P, P, P,
-                                  P, P]),
+                                  P, P, P]),
     "vaesne_dec_tail_grad_layout": (I32, [C.POINTER(I32)]),
     "vaesne_sincos": (I32, [P, I64, I64, P, I32, P, I64, P]),
     "vaesne_embed_fwd": (I32, [P, I64, I64, P, I32, P, I64, P, I64, P]),

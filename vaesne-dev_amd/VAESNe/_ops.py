@@ -614,6 +614,11 @@ def _tail_layout():
     return _TAIL_LAYOUT
 
 
+# the tail forward stores its dropout keep masks (16 B/token) for the backward;
+# False makes the backward re-hash them (tests compare the two bit for bit)
+STORE_TAIL_MASKS = True
+
+
 class DecTailFn(torch.autograd.Function):
     """(x, O, context, cross in_proj Wc [96, 32] / bc [96], 16 more block tensors)
     -> (y [, qkv_next]) for one decoder block.  The context's k|v projection
@@ -640,10 +645,12 @@ class DecTailFn(torch.autograd.Function):
         qkv = torch.empty((M, 3 * E), dtype=torch.float32, device=dev) if nxt else None
         st = rng.state(dev) if p > 0 else None
         cid = rng.next_call_id() if p > 0 else 0
+        masks = torch.empty((M, 4), dtype=torch.int32, device=dev) \
+            if p > 0 and STORE_TAIL_MASKS else None
         lib.dec_tail_fwd(x.data_ptr(), O.data_ptr(), kvc.data_ptr(), M, L, Lc, _lib.ptr_array(w),
-                         float(p), ptr(st), cid, y.data_ptr(), ptr(qkv), stream())
+                         float(p), ptr(st), cid, y.data_ptr(), ptr(qkv), ptr(masks), stream())
         ctx.meta = (M, L, Lc, float(p), cid, nxt, x.shape)
-        ctx.save_for_backward(x, O, context, kvc, y, st, *w)
+        ctx.save_for_backward(x, O, context, kvc, y, st, masks, *w)
         y = y.view(x.shape)
         if nxt:
             return y, qkv.view(*x.shape[:-1], 3 * E)
@@ -651,7 +658,7 @@ class DecTailFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, dqkv):
-        x, O, context, kvc, y, st, *w = ctx.saved_tensors
+        x, O, context, kvc, y, st, masks, *w = ctx.saved_tensors
         M, L, Lc, p, cid, nxt, xshape = ctx.meta
         E = 32
         dev = x.device
@@ -669,8 +676,9 @@ class DecTailFn(torch.autograd.Function):
         ws = _ws(lib.dec_tail_workspace(M, L, Lc), dev)
         s = stream()
         lib.dec_tail_bwd(x.data_ptr(), O.data_ptr(), kvc.data_ptr(), M, L, Lc, _lib.ptr_array(w),
-                         p, ptr(st), cid, y.data_ptr(), dy.data_ptr(), ptr(dqkv), dx.data_ptr(),
-                         dO.data_ptr(), dkvc.data_ptr(), gflat.data_ptr(), ws.data_ptr(), s)
+                         p, ptr(st), cid, y.data_ptr(), dy.data_ptr(), ptr(dqkv), ptr(masks),
+                         dx.data_ptr(), dO.data_ptr(), dkvc.data_ptr(), gflat.data_ptr(),
+                         ws.data_ptr(), s)
         Wc = w[4]
         Mc = context.shape[0] * Lc
         # full in_proj gradient: rows [0, E) from the tail, rows [E, 3E) from the k|v proj

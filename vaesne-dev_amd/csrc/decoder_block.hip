@@ -59,6 +59,9 @@ struct Tail {
   uint32_t thr; float inv_keep;
   const int64_t* rng; uint32_t call_id;
   int chunk;           // tokens per workgroup (multiple of 128)
+  uint32_t* masks;     // [M][4] dropout keep masks written by fwd, read by bwd (or null:
+                       // bwd re-hashes): word s < 3 = residual site s, 16 bits per half
+                       // (half 0 low), word 3 = cross-attention keep bits
   // forward outputs
   float* y;            // [M, 32]
   float* qkv;          // [M, 96] (if Wn)
@@ -182,13 +185,14 @@ __device__ __forceinline__ float gelu(float x) { return gelu_erf(x); }
 
 // cross attention of one token over the Lc context tokens (all heads):
 // p[hd][j] (pre-dropout), keep bits, c (feature layout)
+// have_km: keepm already holds the keep bits (stored by the forward); else hash
 template <int LC>
 __device__ __forceinline__ void cross_fwd(const float* kv, int Lc, const float (&q)[16], int h,
                                           uint32_t akey, int64_t row, bool drop, uint32_t thr,
                                           float inv_keep, float (&p)[H][LC], uint32_t& keepm,
-                                          float (&c)[16]) {
+                                          float (&c)[16], bool have_km = false) {
   const float scale = 0.35355339059327373f;  // 1/sqrt(8)
-  keepm = 0u;
+  if (!have_km) keepm = 0u;
 #pragma unroll
   for (int hd = 0; hd < H; ++hd) {
     float s[LC];
@@ -221,11 +225,16 @@ __device__ __forceinline__ void cross_fwd(const float* kv, int Lc, const float (
       p[hd][j] = pj;
       float pd = pj;
       if (drop && j < Lc) {
-        uint32_t bits = rand_u32(akey, ((uint64_t)row * H + hd) * LCMAX + j);
-        bool kp = (bits & 0xffffu) >= thr;
-        keepm |= (kp ? 1u : 0u) << (hd * LCMAX + j);
+        bool kp;
+        if (have_km) {
+          kp = (keepm >> (hd * LCMAX + j)) & 1u;
+        } else {
+          uint32_t bits = rand_u32(akey, ((uint64_t)row * H + hd) * LCMAX + j);
+          kp = (bits & 0xffffu) >= thr;
+          keepm |= (kp ? 1u : 0u) << (hd * LCMAX + j);
+        }
         pd = kp ? pj * inv_keep : 0.f;
-      } else {
+      } else if (!have_km) {
         keepm |= 1u << (hd * LCMAX + j);
       }
       if (j < Lc) {
@@ -257,11 +266,15 @@ __global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
     load_row(a.O, row, h, v);
     mv(S.Wo1, S.bo1, v, v, lane);                          // a1
     load_row(a.x, row, h, xin);
+    uint16_t* m16 = reinterpret_cast<uint16_t*>(a.masks) + row * 8 + h;
+    const bool keep_masks = DROP && a.masks != nullptr && valid;
     if (DROP) {
       float sc[16];
       drop_res(site_key(key, 0), row, h, a.thr, a.inv_keep, sc);
+      uint32_t m = 0u;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] *= sc[r];
+      for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; m |= (sc[r] != 0.f ? 1u : 0u) << r; }
+      if (keep_masks) m16[0] = (uint16_t)m;
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] += xin[r];
@@ -276,8 +289,10 @@ __global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
     if (DROP) {
       float sc[16];
       drop_res(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
+      uint32_t m = 0u;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] *= sc[r];
+      for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; m |= (sc[r] != 0.f ? 1u : 0u) << r; }
+      if (keep_masks) { m16[2] = (uint16_t)m; if (h) a.masks[row * 4 + 3] = km; }
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] += xin[r];
@@ -291,8 +306,10 @@ __global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
     if (DROP) {
       float sc[16];
       drop_res(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
+      uint32_t m = 0u;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] *= sc[r];
+      for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; m |= (sc[r] != 0.f ? 1u : 0u) << r; }
+      if (keep_masks) m16[4] = (uint16_t)m;
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] += xin[r];
@@ -344,12 +361,24 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
     float xh1[16], xh2[16], xh3[16], q[16], c[16], f1[16];
     float rs1, rs2, rs3, p[H][LC];
     uint32_t km, k0 = 0xffffffffu, k1 = 0xffffffffu, k2 = 0xffffffffu;
+    const bool have = DROP && a.masks != nullptr;   // masks stored by the forward
+    if (have) {
+      const uint4 mw = *reinterpret_cast<const uint4*>(a.masks + row * 4);
+      const int sh = 16 * h;
+      k0 = (mw.x >> sh) & 0xffffu;
+      k1 = (mw.y >> sh) & 0xffffu;
+      k2 = (mw.z >> sh) & 0xffffu;
+      km = mw.w;
+    }
     {
       float v[16], t[16];
       load_row(a.O, row, h, t);
       mv(S.Wo1, S.bo1, t, v, lane);
       load_row(a.x, row, h, t);
-      if (DROP) {
+      if (DROP && have) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] *= ((k0 >> r) & 1u) ? a.inv_keep : 0.f;
+      } else if (DROP) {
         float sc[16];
         drop_res(site_key(key, 0), row, h, a.thr, a.inv_keep, sc);
         k0 = 0u;
@@ -362,9 +391,13 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
 #pragma unroll
       for (int r = 0; r < 16; ++r) t[r] = fmaf(xh1[r], S.g1[F(r, h)], S.be1[F(r, h)]);   // x1
       mv(S.Wq, S.bq, t, q, lane);
-      cross_fwd<LC>(S.kv, a.Lc, q, h, site_key(key, 3), row, DROP, a.thr, a.inv_keep, p, km, c);
+      cross_fwd<LC>(S.kv, a.Lc, q, h, site_key(key, 3), row, DROP, a.thr, a.inv_keep, p, km, c,
+                    have);
       mv(S.Wo2, S.bo2, c, v, lane);
-      if (DROP) {
+      if (DROP && have) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] *= ((k1 >> r) & 1u) ? a.inv_keep : 0.f;
+      } else if (DROP) {
         float sc[16];
         drop_res(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
         k1 = 0u;
@@ -380,7 +413,10 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = gelu(f1[r]);
       mv(S.W2, S.b2, v, v, lane);
-      if (DROP) {
+      if (DROP && have) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] *= ((k2 >> r) & 1u) ? a.inv_keep : 0.f;
+      } else if (DROP) {
         float sc[16];
         drop_res(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
         k2 = 0u;
@@ -739,9 +775,10 @@ VAESNE_API int64_t vaesne_dec_tail_workspace(int M, int L, int Lc) {
 VAESNE_API int vaesne_dec_tail_fwd(const float* x, const float* O, const float* kvc, int M, int L,
                                    int Lc, const float* const* w, float p_drop,
                                    const int64_t* rng, uint32_t call_id, float* y, float* qkv,
-                                   void* stream) {
+                                   uint32_t* drop_masks, void* stream) {
   if (!shapes_ok(M, L, Lc)) return (int)hipErrorInvalidValue;
   Tail a = make(x, O, kvc, M, L, Lc, w, p_drop, rng, call_id);
+  a.masks = p_drop > 0.f ? drop_masks : nullptr;
   a.y = y; a.qkv = qkv;
   if (a.Wn && !qkv) return (int)hipErrorInvalidValue;
   const int grid = (M / L) * ((L + a.chunk - 1) / a.chunk);
@@ -753,11 +790,13 @@ VAESNE_API int vaesne_dec_tail_fwd(const float* x, const float* O, const float* 
 VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* kvc, int M, int L,
                                    int Lc, const float* const* w, float p_drop,
                                    const int64_t* rng, uint32_t call_id, const float* y,
-                                   const float* dy, const float* dqkv, float* dx, float* dO,
-                                   float* dkvc, float* gflat, float* workspace, void* stream) {
+                                   const float* dy, const float* dqkv, const uint32_t* drop_masks,
+                                   float* dx, float* dO, float* dkvc, float* gflat,
+                                   float* workspace, void* stream) {
   if (!shapes_ok(M, L, Lc)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   Tail a = make(x, O, kvc, M, L, Lc, w, p_drop, rng, call_id);
+  a.masks = p_drop > 0.f ? const_cast<uint32_t*>(drop_masks) : nullptr;
   a.dy = dy; a.dqkv = dqkv; a.dx = dx; a.dO = dO;
   if (a.Wn && !dqkv) return (int)hipErrorInvalidValue;
   const int chunks = (L + a.chunk - 1) / a.chunk;
