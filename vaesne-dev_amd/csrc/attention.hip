@@ -285,18 +285,55 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+// sum of v[0..7] over the 64 lanes of a wave; lane l returns the total of
+// component (l >> 3) & 7.  Transposing butterfly: each permlane swap exchanges
+// half of the live components with the partner half-wave / half-row, so the
+// live set halves per level (4 + 2 swaps, one DPP exchange, 3 DPP adds).
+__device__ __forceinline__ float wave_sum8_spread(const float (&v)[8]) {
+  float u[4], w[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {   // lanes 0-31: components i, lanes 32-63: i + 4
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]),
+                                                    __float_as_uint(v[i + 4]), false, false);
+    u[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {   // lane bit 4 selects i / i + 2
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(u[i]),
+                                                    __float_as_uint(u[i + 2]), false, false);
+    w[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  // lane bit 3 selects w[0] / w[1]: keep mine, send the partner (l ^ 8 = row_ror 8) its half
+  const bool hi = (threadIdx.x >> 3) & 1;
+  const float keep = hi ? w[1] : w[0], send = hi ? w[0] : w[1];
+  float x = keep + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), 0x128,
+                                                              0xf, 0xf, false));
+  // reduce over lane bits 0..2: half-row mirror, then quad xor 2, xor 1
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xf, 0xf, false));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4e, 0xf, 0xf, false));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xb1, 0xf, 0xf, false));
+  return x;
+}
+
 // ============================== dK, dV =====================================
 // lane owns 2*NP adjacent keys key0 .. key0 + 2NP - 1 (pairs of adjacent keys);
-// queries stream through LDS tiles
-template <int DH, int NTT, int NP, bool DROP>
+// queries stream through LDS tiles.
+// DQ (head_dim 8, the whole key axis in this workgroup): dQ is fused in.  Per
+// query, each lane's dS-weighted key sum is reduced over the wave
+// (wave_sum8_spread) into LDS, and over the workgroup's waves per query tile:
+// the dQ kernel's recomputation of S, P and dP is saved.
+template <int DH, int NTT, int NP, bool DROP, bool DQ = false>
 __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
   constexpr int R = 2 * NP;
   constexpr int KB = R * NTT;
   constexpr int NWB = (KB + 31) / 32;       // bitmap words of this key block
+  constexpr int NWV = NTT / 64;             // waves
+  static_assert(!DQ || DH == 8, "fused dQ reduces 8 components");
   __shared__ __attribute__((aligned(16))) float Qs[TK * DH];
   __shared__ __attribute__((aligned(16))) float Ds_[TK * DH];   // dO tile
   __shared__ float Ls[TK], Dd[TK];
   __shared__ uint32_t Ws[TK * NWB];
+  __shared__ __attribute__((aligned(16))) float Qw[DQ ? NWV * TK * DH : 1];   // per-wave dQ
   const int nkb = (a.Lk + KB - 1) / KB;
   const int kb = blockIdx.x % nkb;
   const int bh = blockIdx.x / nkb;
@@ -373,6 +410,11 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
       lrow<DH>(Ds_ + i * DH, dr);
       const f2 li = bc(Ls[i]), Di = bc(Dd[i]);
       const uint32_t kw = DROP ? (Ws[i * NWB + wl] >> sh) : 0xffffffffu;
+      f2 dq2[DQ ? DH : 1];
+      if (DQ) {
+#pragma unroll
+        for (int d = 0; d < DH; ++d) dq2[d] = bc(0.f);
+      }
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         f2 s = kbias[p], g = bc(0.f);
@@ -393,7 +435,31 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
         for (int d = 0; d < DH; ++d) {
           dv[p][d] = fma2(aP, bc(dr[d]), dv[p][d]);
           dk[p][d] = fma2(dS, bc(qr[d]), dk[p][d]);
+          if (DQ) dq2[d] = fma2(dS, k[p][d], dq2[d]);
         }
+      }
+      if (DQ) {
+        float c[8];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) c[d] = dq2[d].x + dq2[d].y;
+        const float t = wave_sum8_spread(c);
+        if ((threadIdx.x & 7) == 0)
+          Qw[((threadIdx.x >> 6) * TK + i) * DH + ((threadIdx.x >> 3) & 7)] = t;
+      }
+    }
+    if (DQ) {   // dQ rows of this tile: sum over the waves (the whole key axis)
+      __syncthreads();
+      float* dqb = a.dq + (int64_t)b * a.dq_bs + h * DH;
+      for (int idx = threadIdx.x; idx < qend * (DH / 4); idx += NTT) {
+        const int i = idx / (DH / 4), c = (idx - i * (DH / 4)) * 4;
+        float4 acc = *reinterpret_cast<const float4*>(Qw + i * DH + c);
+#pragma unroll
+        for (int wv = 1; wv < NWV; ++wv) {
+          const float4 t = *reinterpret_cast<const float4*>(Qw + (wv * TK + i) * DH + c);
+          acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+        }
+        acc.x *= a.scale; acc.y *= a.scale; acc.z *= a.scale; acc.w *= a.scale;
+        *reinterpret_cast<float4*>(dqb + (int64_t)(qt + i) * a.dq_ls + c) = acc;
       }
     }
   }
@@ -787,6 +853,15 @@ Geo pick_geo(int64_t bh, int L) {
   return {64, 1};
 }
 
+// tuning / A/B hook: VAESNE_ATTN_FUSED_DQ=0 keeps dQ in its own kernel
+bool fused_dq_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("VAESNE_ATTN_FUSED_DQ");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Split launches for grids too small to fill the chip (the encoder's 983-token
 // context self-attention: B*H = 64 sequences -> 512 one-wave workgroups): the
 // streamed axis (keys for the forward / dQ, queries for dK / dV) is cut into
@@ -952,6 +1027,9 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
   const int E = a.H * DHV;
   float* ws_dq = ws;
   float* ws_dkv = ws ? ws + (int64_t)(sq.n > 1 ? sq.n : 0) * a.B * a.Lq * E : nullptr;
+  // fused dK/dV/dQ: head_dim 8 and the whole key axis in one workgroup
+  const Geo gk0 = pick_geo((int64_t)a.B * a.H, a.Lk);
+  const bool fuse = DHV == 8 && part == 3 && a.Lk <= 2 * gk0.np * gk0.nt && fused_dq_enabled();
   if (part & 1) {
     AttnArgs c = a;
     if (sk.n > 1) {   // chunked queries: partial dK / dV per chunk
@@ -964,10 +1042,18 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
     VAESNE_GEO_SWITCH(gk, {
       const int nkb = (a.Lk + 2 * NP * NTT - 1) / (2 * NP * NTT);
       dim3 grid((unsigned)((int64_t)a.B * a.H * nkb), (unsigned)sk.n);
-      if (p_drop > 0.f)
+      if (fuse) {
+        if (p_drop > 0.f)
+          hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, NP, true, DHV == 8>), grid, dim3(NTT),
+                             0, s, c);
+        else
+          hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, NP, false, DHV == 8>), grid,
+                             dim3(NTT), 0, s, c);
+      } else if (p_drop > 0.f) {
         hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, NP, true>), grid, dim3(NTT), 0, s, c);
-      else
+      } else {
         hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, c);
+      }
     })
     VAESNE_CHECK_LAUNCH();
     if (sk.n > 1) {
@@ -981,7 +1067,7 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
       VAESNE_CHECK_LAUNCH();
     }
   }
-  if (part & 2) {
+  if ((part & 2) && !fuse) {
     AttnArgs c = a;
     if (sq.n > 1) {   // chunked keys: partial dQ per chunk
       c.kchunk = sq.chunk;
