@@ -183,11 +183,11 @@ def roofline(device, B):
     sequences x 982 tokens: the decoder runs once over both modalities'
     latents; 4 heads x dh 8, dropout 0.1, 5 % key padding),
     the dominant op of the step.  The roofline kernel is
-    attn_bwd_kv_kernel, the most expensive single kernel of the step; the
-    forward and the dQ kernel are reported beside it.  Algorithmic FLOPs per
-    score: fwd 4*dh (QK^T, PV), bwd_kv 8*dh (S, dP, dV, dK), bwd_q 6*dh
-    (S, dP, dQ) -- the flash backward's recomputation of S counts, as the
-    kernels must do it."""
+    the fused attention backward (attn_bwd_kv_kernel<..., DQ=true>: dK, dV and
+    dQ in one pass), the most expensive single kernel of the step; the forward
+    is reported beside it.  Algorithmic FLOPs per score: fwd 4*dh (QK^T, PV),
+    bwd 10*dh (S, dP, dV, dK, dQ) -- the flash backward's recomputation of S
+    counts, as the kernel must do it."""
     from VAESNe import _lib, rng
     N, L, E, H, dh = 2 * CFG["K"] * B, CFG["Ls"], CFG["model_dim"], CFG["num_heads"], 8
     pd = float(os.environ.get("VAESNE_ROOFLINE_PDROP", CFG["dropout"]))   # A/B studies only
@@ -220,12 +220,11 @@ def roofline(device, B):
     scores = N * H * L * L
     res = {}
     for name, kern, fn, fl in [("fwd", "attn_fwd_kernel", fwd, 4 * dh),
-                               ("bwd_kv", "attn_bwd_kv_kernel", bwd(lib.attn_bwd_kv), 8 * dh),
-                               ("bwd_q", "attn_bwd_q_kernel", bwd(lib.attn_bwd_q), 6 * dh)]:
+                               ("bwd", "attn_bwd_kv_kernel", bwd(lib.attn_bwd), 10 * dh)]:
         t = time_kernel(fn, 20, device)
         res[name] = dict(kernel=kern, ms=t * 1e3, tflops=scores * fl / t / 1e12,
                          flops_per_launch=scores * fl)
-    r = res["bwd_kv"]
+    r = res["bwd"]
     a = r["tflops"]
     traffic, tsrc = None, None
     try:   # HBM bytes per launch from the committed rocprofv3 --pmc passes (gpu_run.sh pmc)

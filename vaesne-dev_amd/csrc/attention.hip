@@ -92,6 +92,33 @@ __device__ __forceinline__ void lrow(const float* s, float (&r)[DH]) {
   }
 }
 
+// broadcast-operand packed FMA: c + a * {r_d, r_d} with r_d one half of an LDS
+// row held as register pairs.  The op_sel / op_sel_hi forms read the scalar
+// straight out of the pair (the compiler otherwise copies it into a fresh pair
+// with up to two v_mov per use: ~30 % extra VALU in the inner loops).
+__device__ __forceinline__ f2 fma2_lo(f2 a, f2 b, f2 c) {
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(c) : "v"(a), "v"(b));
+  return c;
+}
+__device__ __forceinline__ f2 fma2_hi(f2 a, f2 b, f2 c) {
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(c) : "v"(a), "v"(b));
+  return c;
+}
+template <int DH>
+__device__ __forceinline__ f2 fma2r(f2 a, const f2 (&r)[DH / 2], int d, f2 c) {
+  return (d & 1) ? fma2_hi(a, r[d >> 1], c) : fma2_lo(a, r[d >> 1], c);
+}
+// broadcast read of one LDS row as register pairs
+template <int DH>
+__device__ __forceinline__ void lrow2(const float* s, f2 (&r)[DH / 2]) {
+#pragma unroll
+  for (int d = 0; d < DH; d += 4) {
+    float4 a = *reinterpret_cast<const float4*>(s + d);
+    r[d / 2] = (f2){a.x, a.y};
+    r[d / 2 + 1] = (f2){a.z, a.w};
+  }
+}
+
 // stage rows [r0, r0 + TK) of a (row-major, stride ls) matrix's head slice
 // into LDS [TK][DH] (zeros past `rows`)
 template <int DH, int NTT>
@@ -175,14 +202,14 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
       for (int p = 0; p < NP; ++p) x[p] = m[p];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        float kr[DH];
-        lrow<DH>(Ks + (g0 + u) * DH, kr);
+        f2 kr[DH / 2];
+        lrow2<DH>(Ks + (g0 + u) * DH, kr);
         const float kb = Kb[g0 + u];
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
           f2 acc = bc(kb);
 #pragma unroll
-          for (int d = 0; d < DH; ++d) acc = fma2(q[p][d], bc(kr[d]), acc);
+          for (int d = 0; d < DH; ++d) acc = fma2r<DH>(q[p][d], kr, d, acc);
           s[p][u] = acc;
           x[p] = __builtin_elementwise_max(x[p], acc);
         }
@@ -223,15 +250,15 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
             p1[p] = sel2(kk[2 * p] & 2u, kk[2 * p + 1] & 2u, p1[p]);
           }
         }
-        float v0[DH], v1[DH];
-        lrow<DH>(Vs + (g0 + u) * DH, v0);
-        lrow<DH>(Vs + (g0 + u + 1) * DH, v1);
+        f2 v0[DH / 2], v1[DH / 2];
+        lrow2<DH>(Vs + (g0 + u) * DH, v0);
+        lrow2<DH>(Vs + (g0 + u + 1) * DH, v1);
 #pragma unroll
         for (int d = 0; d < DH; ++d) {
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
-            o[p][d] = fma2(p0[p], bc(v0[d]), o[p][d]);
-            o[p][d] = fma2(p1[p], bc(v1[d]), o[p][d]);
+            o[p][d] = fma2r<DH>(p0[p], v0, d, o[p][d]);
+            o[p][d] = fma2r<DH>(p1[p], v1, d, o[p][d]);
           }
         }
       }
@@ -405,9 +432,9 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
     const int qend = min(TK, qlim - qt);
 #pragma unroll 2
     for (int i = 0; i < qend; ++i) {
-      float qr[DH], dr[DH];
-      lrow<DH>(Qs + i * DH, qr);
-      lrow<DH>(Ds_ + i * DH, dr);
+      f2 qr[DH / 2], dr[DH / 2];
+      lrow2<DH>(Qs + i * DH, qr);
+      lrow2<DH>(Ds_ + i * DH, dr);
       const f2 li = bc(Ls[i]), Di = bc(Dd[i]);
       const uint32_t kw = DROP ? (Ws[i * NWB + wl] >> sh) : 0xffffffffu;
       f2 dq2[DQ ? DH : 1];
@@ -420,8 +447,8 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
         f2 s = kbias[p], g = bc(0.f);
 #pragma unroll
         for (int d = 0; d < DH; ++d) {
-          s = fma2(k[p][d], bc(qr[d]), s);
-          g = fma2(v[p][d], bc(dr[d]), g);
+          s = fma2r<DH>(k[p][d], qr, d, s);
+          g = fma2r<DH>(v[p][d], dr, d, g);
         }
         const f2 pr = ex2(s - li);
         f2 aP = pr, dP = g;
@@ -433,8 +460,8 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
         const f2 dS = pr * (dP - Di);
 #pragma unroll
         for (int d = 0; d < DH; ++d) {
-          dv[p][d] = fma2(aP, bc(dr[d]), dv[p][d]);
-          dk[p][d] = fma2(dS, bc(qr[d]), dk[p][d]);
+          dv[p][d] = fma2r<DH>(aP, dr, d, dv[p][d]);
+          dk[p][d] = fma2r<DH>(dS, qr, d, dk[p][d]);
           if (DQ) dq2[d] = fma2(dS, k[p][d], dq2[d]);
         }
       }
@@ -553,9 +580,9 @@ __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
 #pragma unroll
         for (int u = 0; u < R; ++u) w[u] = bitp[(int64_t)word * a.Lq + qc[u]];
       }
-      float kr[DH], vr[DH];
-      lrow<DH>(Ks + j * DH, kr);
-      lrow<DH>(Vs + j * DH, vr);
+      f2 kr[DH / 2], vr[DH / 2];
+      lrow2<DH>(Ks + j * DH, kr);
+      lrow2<DH>(Vs + j * DH, vr);
       const float kb = Kb[j];
       const int s = j & 31;
 #pragma unroll
@@ -563,15 +590,15 @@ __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
         f2 sc = bc(kb), t = bc(0.f);
 #pragma unroll
         for (int d = 0; d < DH; ++d) {
-          sc = fma2(q[p][d], bc(kr[d]), sc);
-          t = fma2(g[p][d], bc(vr[d]), t);
+          sc = fma2r<DH>(q[p][d], kr, d, sc);
+          t = fma2r<DH>(g[p][d], vr, d, t);
         }
         const f2 pr = ex2(sc - lse[p]);
         f2 dP = t;
         if (DROP) dP = sel2((w[2 * p] >> s) & 1u, (w[2 * p + 1] >> s) & 1u, dP);
         const f2 dS = pr * (dP - D[p]);
 #pragma unroll
-        for (int d = 0; d < DH; ++d) dq[p][d] = fma2(dS, bc(kr[d]), dq[p][d]);
+        for (int d = 0; d < DH; ++d) dq[p][d] = fma2r<DH>(dS, kr, d, dq[p][d]);
       }
     }
   }
