@@ -860,9 +860,10 @@ void fill_common(AttnArgs& a, int B, int H, int Lq, int Lk, int dh, float p_drop
 }
 
 // Geometry: rows per lane R = 2*NP (NP = 2 amortises each LDS read over four
-// rows) and workgroup size NTT in {256, 128, 64}.  Take the first of
-// (NP=2: 256,128,64; NP=1: 256,128,64) that yields >= 1024 workgroups (4 per
-// CU); the small encoder grids (B*H = 64) fall through to NP=1 / 64 threads.
+// rows) and workgroup size NTT in {256, 128, 64}.  Of (NP=2: 256,128,64; NP=1:
+// 256,128,64), the geometries yielding >= 1024 workgroups (4 per CU) compete on
+// row-slot efficiency; the small encoder grids (B*H = 64) fall through to NP=1
+// / 64 threads.
 struct Geo { int nt, np; };
 Geo pick_geo(int64_t bh, int L) {
   static const Geo forced = [] {   // tuning hook: VAESNE_ATTN_GEO="nt,np" (np in 1, 2)
@@ -871,13 +872,20 @@ Geo pick_geo(int64_t bh, int L) {
     return f;
   }();
   if (forced.nt > 0) return forced;
+  // among geometries with >= 1024 workgroups, the one wasting the fewest row
+  // slots (short sequences: the photometry decoder's 60 tokens x 1024 (b, h)
+  // fill 60 of 1024 rows at 256x2 but 60 of 128 at 64x1); ties keep the order
   const int nts[3] = {256, 128, 64};
+  Geo best{64, 1};
+  double best_eff = -1.0;
   for (int np = 2; np >= 1; --np)
     for (int i = 0; i < 3; ++i) {
-      const int nt = nts[i];
-      if (bh * ((L + 2 * np * nt - 1) / (2 * np * nt)) >= 1024) return {nt, np};
+      const int nt = nts[i], rows = 2 * np * nt;
+      const int64_t nb = (L + rows - 1) / rows;
+      const double eff = (double)L / (double)(rows * nb);
+      if (bh * nb >= 1024 && eff > best_eff + 1e-9) { best = {nt, np}; best_eff = eff; }
     }
-  return {64, 1};
+  return best;
 }
 
 // tuning / A/B hook: VAESNE_ATTN_FUSED_DQ=0 keeps dQ in its own kernel
