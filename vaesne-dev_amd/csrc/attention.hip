@@ -430,8 +430,12 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
     }
     __syncthreads();
     const int qend = min(TK, qlim - qt);
-#pragma unroll 2
-    for (int i = 0; i < qend; ++i) {
+    // two queries per trip (a padding row past qend has Ls = +inf -> p = 0 and
+    // contributes nothing): explicit, as the wave reduction's cross-lane ops
+    // keep the compiler from unrolling a runtime-count loop
+    for (int i0 = 0; i0 < qend; i0 += 2)
+#pragma unroll
+    for (int i = i0; i < i0 + 2; ++i) {
       f2 qr[DH / 2], dr[DH / 2];
       lrow2<DH>(Qs + i * DH, qr);
       lrow2<DH>(Ds_ + i * DH, dr);
@@ -469,9 +473,9 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
         float c[8];
 #pragma unroll
         for (int d = 0; d < 8; ++d) c[d] = dq2[d].x + dq2[d].y;
-        const float t = wave_sum8_spread(c);
-        if ((threadIdx.x & 7) == 0)
-          Qw[((threadIdx.x >> 6) * TK + i) * DH + ((threadIdx.x >> 3) & 7)] = t;
+        // the 8 lanes of a group hold the same total: all store it (no branch)
+        Qw[((threadIdx.x >> 6) * TK + i) * DH + ((threadIdx.x >> 3) & 7)] =
+            wave_sum8_spread(c);
       }
     }
     if (DQ) {   // dQ rows of this tile: sum over the waves (the whole key axis)
