@@ -96,6 +96,9 @@ __device__ __forceinline__ void lrow(const float* s, float (&r)[DH]) {
 // row held as register pairs.  The op_sel / op_sel_hi forms read the scalar
 // straight out of the pair (the compiler otherwise copies it into a fresh pair
 // with up to two v_mov per use: ~30 % extra VALU in the inner loops).
+// Tied (in-place accumulator) forms for the forward / dQ kernels, where they
+// keep the register count down (forward 161 vs 189 VGPRs untied); untied forms
+// (_u) for the dK/dV kernel, whose accumulators start from live values.
 __device__ __forceinline__ f2 fma2_lo(f2 a, f2 b, f2 c) {
   asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(c) : "v"(a), "v"(b));
   return c;
@@ -104,9 +107,34 @@ __device__ __forceinline__ f2 fma2_hi(f2 a, f2 b, f2 c) {
   asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(c) : "v"(a), "v"(b));
   return c;
 }
+__device__ __forceinline__ f2 fma2_lo_u(f2 a, f2 b, f2 c) {
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ f2 fma2_hi_u(f2 a, f2 b, f2 c) {
+  f2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
+      : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ f2 mul2_lo(f2 a, f2 b) {
+  f2 r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ f2 mul2_hi(f2 a, f2 b) {
+  f2 r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 template <int DH>
 __device__ __forceinline__ f2 fma2r(f2 a, const f2 (&r)[DH / 2], int d, f2 c) {
   return (d & 1) ? fma2_hi(a, r[d >> 1], c) : fma2_lo(a, r[d >> 1], c);
+}
+template <int DH>
+__device__ __forceinline__ f2 fma2ru(f2 a, const f2 (&r)[DH / 2], int d, f2 c) {
+  return (d & 1) ? fma2_hi_u(a, r[d >> 1], c) : fma2_lo_u(a, r[d >> 1], c);
 }
 // broadcast read of one LDS row as register pairs
 template <int DH>
@@ -312,43 +340,48 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
-// sum of v[0..7] over the 64 lanes of a wave; lane l returns the total of
-// component (l >> 3) & 7.  Transposing butterfly: each permlane swap exchanges
-// half of the live components with the partner half-wave / half-row, so the
-// live set halves per level (4 + 2 swaps, one DPP exchange, 3 DPP adds).
-__device__ __forceinline__ float wave_sum8_spread(const float (&v)[8]) {
-  float u[4], w[2];
+// sum of v[0..15] over the 64 lanes of a wave; lane l returns the total of
+// component l >> 2.  Transposing butterfly: each exchange level sends half of
+// the live components to the partner lane group and keeps the other half, so
+// the live set halves per level: permlane32 swaps (8), permlane16 swaps (4),
+// DPP row_ror 8 (xor 8, 2) and half-row mirror (partner 7 - l, flips bit 2),
+// then two quad-permute adds over lane bits 0, 1.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_sum16_spread(const float (&v)[16]) {
+  float u[8], w[4], x[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {   // lanes 0-31: components i, lanes 32-63: i + 4
+  for (int i = 0; i < 8; ++i) {   // lanes 0-31 keep component i, lanes 32-63 i + 8
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]),
-                                                    __float_as_uint(v[i + 4]), false, false);
+                                                    __float_as_uint(v[i + 8]), false, false);
     u[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {   // lane bit 4 selects i / i + 2
+  for (int i = 0; i < 4; ++i) {   // lane bit 4 selects i / i + 4
     const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(u[i]),
-                                                    __float_as_uint(u[i + 2]), false, false);
+                                                    __float_as_uint(u[i + 4]), false, false);
     w[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
   }
-  // lane bit 3 selects w[0] / w[1]: keep mine, send the partner (l ^ 8 = row_ror 8) its half
-  const bool hi = (threadIdx.x >> 3) & 1;
-  const float keep = hi ? w[1] : w[0], send = hi ? w[0] : w[1];
-  float x = keep + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), 0x128,
-                                                              0xf, 0xf, false));
-  // reduce over lane bits 0..2: half-row mirror, then quad xor 2, xor 1
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xf, 0xf, false));
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4e, 0xf, 0xf, false));
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xb1, 0xf, 0xf, false));
-  return x;
+  const bool b3 = (threadIdx.x >> 3) & 1, b2 = (threadIdx.x >> 2) & 1;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)     // lane bit 3 selects i / i + 2 (partner l ^ 8 = row_ror 8)
+    x[i] = (b3 ? w[i + 2] : w[i]) + dpp<0x128>(b3 ? w[i] : w[i + 2]);
+  float y = (b2 ? x[1] : x[0]) + dpp<0x141>(b2 ? x[0] : x[1]);   // half-row mirror
+  y += dpp<0x4e>(y);              // quad xor 2
+  y += dpp<0xb1>(y);              // quad xor 1
+  return y;
 }
 
 // ============================== dK, dV =====================================
 // lane owns 2*NP adjacent keys key0 .. key0 + 2NP - 1 (pairs of adjacent keys);
 // queries stream through LDS tiles.
 // DQ (head_dim 8, the whole key axis in this workgroup): dQ is fused in.  Per
-// query, each lane's dS-weighted key sum is reduced over the wave
-// (wave_sum8_spread) into LDS, and over the workgroup's waves per query tile:
-// the dQ kernel's recomputation of S, P and dP is saved.
+// pair of queries, each lane's dS-weighted key sums (both queries packed in one
+// f2 per feature) are reduced over the wave (wave_sum16_spread) into LDS, and
+// over the workgroup's waves per query tile: the dQ kernel's recomputation of
+// S, P and dP is saved.
 template <int DH, int NTT, int NP, bool DROP, bool DQ = false>
 __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
   constexpr int R = 2 * NP;
@@ -433,49 +466,56 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
     // two queries per trip (a padding row past qend has Ls = +inf -> p = 0 and
     // contributes nothing): explicit, as the wave reduction's cross-lane ops
     // keep the compiler from unrolling a runtime-count loop
-    for (int i0 = 0; i0 < qend; i0 += 2)
+    for (int i0 = 0; i0 < qend; i0 += 2) {
+      f2 dSq[2][NP];
 #pragma unroll
-    for (int i = i0; i < i0 + 2; ++i) {
-      f2 qr[DH / 2], dr[DH / 2];
-      lrow2<DH>(Qs + i * DH, qr);
-      lrow2<DH>(Ds_ + i * DH, dr);
-      const f2 li = bc(Ls[i]), Di = bc(Dd[i]);
-      const uint32_t kw = DROP ? (Ws[i * NWB + wl] >> sh) : 0xffffffffu;
-      f2 dq2[DQ ? DH : 1];
-      if (DQ) {
+      for (int i = i0; i < i0 + 2; ++i) {
+        f2 qr[DH / 2], dr[DH / 2];
+        lrow2<DH>(Qs + i * DH, qr);
+        lrow2<DH>(Ds_ + i * DH, dr);
+        const f2 li = bc(Ls[i]), Di = bc(Dd[i]);
+        const uint32_t kw = DROP ? (Ws[i * NWB + wl] >> sh) : 0xffffffffu;
 #pragma unroll
-        for (int d = 0; d < DH; ++d) dq2[d] = bc(0.f);
-      }
+        for (int p = 0; p < NP; ++p) {
+          f2 s = kbias[p], g = mul2_lo(v[p][0], dr[0]);
 #pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        f2 s = kbias[p], g = bc(0.f);
+          for (int d = 0; d < DH; ++d) {
+            s = fma2ru<DH>(k[p][d], qr, d, s);
+            if (d > 0) g = fma2ru<DH>(v[p][d], dr, d, g);
+          }
+          const f2 pr = ex2(s - li);
+          f2 aP = pr, dP = g;
+          if (DROP) {
+            const uint32_t m0 = (kw >> (2 * p)) & 1u, m1 = (kw >> (2 * p + 1)) & 1u;
+            aP = sel2(m0, m1, pr);
+            dP = sel2(m0, m1, g);
+          }
+          const f2 dS = pr * (dP - Di);
+          dSq[i - i0][p] = dS;
 #pragma unroll
-        for (int d = 0; d < DH; ++d) {
-          s = fma2r<DH>(k[p][d], qr, d, s);
-          g = fma2r<DH>(v[p][d], dr, d, g);
-        }
-        const f2 pr = ex2(s - li);
-        f2 aP = pr, dP = g;
-        if (DROP) {
-          const uint32_t m0 = (kw >> (2 * p)) & 1u, m1 = (kw >> (2 * p + 1)) & 1u;
-          aP = sel2(m0, m1, pr);
-          dP = sel2(m0, m1, g);
-        }
-        const f2 dS = pr * (dP - Di);
-#pragma unroll
-        for (int d = 0; d < DH; ++d) {
-          dv[p][d] = fma2r<DH>(aP, dr, d, dv[p][d]);
-          dk[p][d] = fma2r<DH>(dS, qr, d, dk[p][d]);
-          if (DQ) dq2[d] = fma2(dS, k[p][d], dq2[d]);
+          for (int d = 0; d < DH; ++d) {
+            dv[p][d] = fma2ru<DH>(aP, dr, d, dv[p][d]);
+            dk[p][d] = fma2ru<DH>(dS, qr, d, dk[p][d]);
+          }
         }
       }
-      if (DQ) {
-        float c[8];
+      if (DQ) {   // F[d] = {dQ_d of query i0, of query i0 + 1} over this lane's keys
+        f2 F[DH];
 #pragma unroll
-        for (int d = 0; d < 8; ++d) c[d] = dq2[d].x + dq2[d].y;
-        // the 8 lanes of a group hold the same total: all store it (no branch)
-        Qw[((threadIdx.x >> 6) * TK + i) * DH + ((threadIdx.x >> 3) & 7)] =
-            wave_sum8_spread(c);
+        for (int p = 0; p < NP; ++p) {
+          const f2 sx = {dSq[0][p].x, dSq[1][p].x}, sy = {dSq[0][p].y, dSq[1][p].y};
+#pragma unroll
+          for (int d = 0; d < DH; ++d) {
+            F[d] = p == 0 ? mul2_lo(sx, k[p][d]) : fma2_lo_u(sx, k[p][d], F[d]);
+            F[d] = fma2_hi_u(sy, k[p][d], F[d]);
+          }
+        }
+        float c[16];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) { c[d] = F[d].x; c[8 + d] = F[d].y; }
+        // the 4 lanes of a group hold the same total: all store it (no branch)
+        Qw[((threadIdx.x >> 6) * TK + i0 + ((threadIdx.x >> 5) & 1)) * DH +
+           ((threadIdx.x >> 2) & 7)] = wave_sum16_spread(c);
       }
     }
     if (DQ) {   // dQ rows of this tile: sum over the waves (the whole key axis)
