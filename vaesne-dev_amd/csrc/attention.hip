@@ -676,12 +676,7 @@ __device__ __forceinline__ void block_reduce(float (&v)[N], float* red, float* o
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    float x = v[i];
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const float y = __shfl_xor(x, off, 64);
-      x = MAX ? fmaxf(x, y) : x + y;
-    }
+    const float x = MAX ? wave_max(v[i]) : wave_sum(v[i]);
     if (lane == 0) red[w * N + i] = x;
   }
   __syncthreads();

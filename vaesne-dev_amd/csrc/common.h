@@ -28,15 +28,51 @@ namespace vaesne {
 
 constexpr int WAVE = 64;
 
+// Cross-lane exchanges without the LDS: v_permlane32/16_swap (gfx950) and DPP.
+// (__shfl_xor lowers to ds_bpermute_b32: an LDS round trip per exchange.)
+// lane l: {v[l], v[l ^ 32]} as (r0, r1) in some order; r0 + r1 = v[l] + v[l ^ 32]
+__device__ __forceinline__ float xsum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v),
+                                                  false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xmax32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v),
+                                                  false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xsum16(float v) {   // v[l] + v[l ^ 16]
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v),
+                                                  false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xmax16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v),
+                                                  false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// all-lane sum / max over the wave: xor 32, xor 16 (permlane swaps), then
+// within each 16-lane row: rotate 8, rotate 4 (sums the lane's coset mod 4),
+// quad xor 2, quad xor 1 (DPP)
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v = xsum16(xsum32(v));
+  v += dpp_mov<0x128>(v);
+  v += dpp_mov<0x124>(v);
+  v += dpp_mov<0x4e>(v);
+  v += dpp_mov<0xb1>(v);
   return v;
 }
 
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  v = xmax16(xmax32(v));
+  v = fmaxf(v, dpp_mov<0x128>(v));
+  v = fmaxf(v, dpp_mov<0x124>(v));
+  v = fmaxf(v, dpp_mov<0x4e>(v));
+  v = fmaxf(v, dpp_mov<0xb1>(v));
   return v;
 }
 

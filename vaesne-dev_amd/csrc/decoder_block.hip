@@ -138,12 +138,12 @@ __device__ __forceinline__ void layernorm(float (&v)[16], float& rstd, float (&x
   float s = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) s += v[r];
-  s += __shfl_xor(s, 32, 64);
+  s = xsum32(s);
   const float mu = s * (1.f / E);
   float q = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) { float d = v[r] - mu; q = fmaf(d, d, q); }
-  q += __shfl_xor(q, 32, 64);
+  q = xsum32(q);
   rstd = rsqrtf(q * (1.f / E) + 1e-5f);
 #pragma unroll
   for (int r = 0; r < 16; ++r) xh[r] = (v[r] - mu) * rstd;
@@ -160,8 +160,8 @@ __device__ __forceinline__ void layernorm_bwd(const float (&g)[16], const float 
     a += gg[r];
     b = fmaf(gg[r], xh[r], b);
   }
-  a += __shfl_xor(a, 32, 64);
-  b += __shfl_xor(b, 32, 64);
+  a = xsum32(a);
+  b = xsum32(b);
   a *= (1.f / E);
   b *= (1.f / E);
 #pragma unroll
@@ -205,7 +205,7 @@ __device__ __forceinline__ void cross_fwd(const float* kv, int Lc, const float (
 #pragma unroll
         for (int i = 0; i < 4; ++i) part = fmaf(q[4 * hd + i], kj[i], part);
       }
-      part += __shfl_xor(part, 32, 64);
+      part = xsum32(part);
       s[j] = j < Lc ? part * scale : -INFINITY;
       mx = fmaxf(mx, s[j]);
     }
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
 #pragma unroll
             for (int i = 0; i < 4; ++i) part = fmaf(dc[4 * hd + i], vj[i], part);
           }
-          part += __shfl_xor(part, 32, 64);
+          part = xsum32(part);
           const bool kp = (km >> (hd * LCMAX + j)) & 1u;
           dp[j] = (j < a.Lc && kp) ? part * ik : 0.f;
           pdv[4 * j + hd] = (j < a.Lc && kp) ? p[hd][j] * ik : 0.f;

@@ -290,7 +290,7 @@ __global__ __launch_bounds__(NT) void linear_wgrad_kernel(WgtArgs p, int nib, fl
       acc = mfma(gg, xx, acc);
     }
   }
-  cs += __shfl_xor(cs, 32, 64);
+  cs = xsum32(cs);
 #pragma unroll
   for (int rg = 0; rg < 16; ++rg) red[wave][F(rg, hh) * 32 + col] = acc[rg];
   if (hh == 0) red[wave][1024 + col] = cs;
