@@ -387,7 +387,10 @@ def test_fused_decoder_tail_dropout_fwd_bwd_consistent():
 
 def test_fused_decoder_tail_stored_masks_match_rehash():
     """The tail backward reading the forward's stored dropout masks gives the
-    same gradients, bit for bit, as re-hashing them from the counter RNG."""
+    same gradients as re-hashing them from the counter RNG.  The two paths are
+    separate kernel instantiations (the compiler may contract mul/add pairs
+    differently), so the bar is 1e-5 relative: one mismatched keep decision
+    moves a gradient by O(1)."""
     from VAESNe import _ops, rng
     from VAESNe.util_layers import decoder_stack
     blocks = _decoder_blocks(2, 5).to(DEV)
@@ -414,5 +417,6 @@ def test_fused_decoder_tail_stored_masks_match_rehash():
             res.append([out, xx.grad, cc.grad] + [p.grad.clone() for p in blocks.parameters()])
         finally:
             _ops.STORE_TAIL_MASKS = True
-    for a, b in zip(*res):
-        assert torch.equal(a, b)
+    assert torch.equal(res[0][0], res[1][0])   # forward: same kernel both times
+    for a, b in zip(res[0][1:], res[1][1:]):
+        assert (a - b).abs().max().item() <= 1e-5 * max(a.abs().max().item(), 1e-3)

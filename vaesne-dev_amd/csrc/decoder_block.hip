@@ -183,6 +183,38 @@ __device__ __forceinline__ uint32_t site_key(uint32_t key, uint32_t site) {
 
 __device__ __forceinline__ float gelu(float x) { return gelu_erf(x); }
 
+// head hd's pre-dropout attention probabilities p[j] of one token over the Lc
+// context tokens -- the same arithmetic, in the same order, as cross_fwd (the
+// backward recomputes them instead of keeping 32 registers live)
+template <int LC>
+__device__ __forceinline__ void cross_probs(const float* kv, int Lc, const float (&q)[16], int h,
+                                            int hd, float (&p)[LC]) {
+  const float scale = 0.35355339059327373f;  // 1/sqrt(8)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < LC; ++j) {
+    float part = 0.f;
+    if (j < Lc) {
+      const float* kj = kv + j * 2 * E + 8 * hd + 4 * h;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part = fmaf(q[4 * hd + i], kj[i], part);
+    }
+    part = xsum32(part);
+    p[j] = j < Lc ? part * scale : -INFINITY;
+    mx = fmaxf(mx, p[j]);
+  }
+  float l = 0.f;
+#pragma unroll
+  for (int j = 0; j < LC; ++j) {
+    float e = j < Lc ? __expf(p[j] - mx) : 0.f;
+    p[j] = e;
+    l += e;
+  }
+  const float il = 1.f / l;
+#pragma unroll
+  for (int j = 0; j < LC; ++j) p[j] *= il;
+}
+
 // cross attention of one token over the Lc context tokens (all heads):
 // p[hd][j] (pre-dropout), keep bits, c (feature layout)
 // have_km: keepm already holds the keep bits (stored by the forward); else hash
@@ -191,38 +223,15 @@ __device__ __forceinline__ void cross_fwd(const float* kv, int Lc, const float (
                                           uint32_t akey, int64_t row, bool drop, uint32_t thr,
                                           float inv_keep, float (&p)[H][LC], uint32_t& keepm,
                                           float (&c)[16], bool have_km = false) {
-  const float scale = 0.35355339059327373f;  // 1/sqrt(8)
   if (!have_km) keepm = 0u;
 #pragma unroll
   for (int hd = 0; hd < H; ++hd) {
-    float s[LC];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < LC; ++j) {
-      float part = 0.f;
-      if (j < Lc) {
-        const float* kj = kv + j * 2 * E + 8 * hd + 4 * h;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) part = fmaf(q[4 * hd + i], kj[i], part);
-      }
-      part = xsum32(part);
-      s[j] = j < Lc ? part * scale : -INFINITY;
-      mx = fmaxf(mx, s[j]);
-    }
-    float l = 0.f;
-#pragma unroll
-    for (int j = 0; j < LC; ++j) {
-      float e = j < Lc ? __expf(s[j] - mx) : 0.f;
-      s[j] = e;
-      l += e;
-    }
-    const float il = 1.f / l;
+    cross_probs<LC>(kv, Lc, q, h, hd, p[hd]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) c[4 * hd + i] = 0.f;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
-      float pj = s[j] * il;
-      p[hd][j] = pj;
+      const float pj = p[hd][j];
       float pd = pj;
       if (drop && j < Lc) {
         bool kp;
@@ -339,9 +348,28 @@ enum Vec {
   V_DLN1, V_DLN1X, V_DLN2, V_DLN2X, V_DLN3, V_DLN3X, V_Q, V_DC, V_DS, V_PD, NVEC
 };
 
-template <int LC, bool NEXT, bool DROP>
-__global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restrict__ scr) {
+// a wave's 16-float-per-lane row parked in LDS ([16][64], lane-contiguous:
+// conflict-free); the asm memory clobber keeps the compiler from forwarding the
+// value in registers, which is the point
+__device__ __forceinline__ void park(float (*slot)[64], const float (&v)[16], int lane) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) slot[r][lane] = v[r];
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void unpark(float (*slot)[64], float (&v)[16], int lane) {
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = slot[r][lane];
+}
+
+// MASKS: the forward's stored keep masks are read (else re-hashed; compiled
+// apart so the common path carries no registers for the other).  Two waves per
+// SIMD: the MASKS path fits 256 registers without spills (one wave per SIMD
+// left every LDS / MFMA / memory latency exposed).
+template <int LC, bool NEXT, bool DROP, bool MASKS>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void dec_tail_bwd_data(Tail a, float* __restrict__ scr) {
   __shared__ Smem S;
+  __shared__ float Pk[NW][2][16][64];   // parked LN1 / LN2 normalised inputs
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
   const int chunks = (a.L + a.chunk - 1) / a.chunk;
   const int seq = blockIdx.x / chunks, ch = blockIdx.x % chunks;
@@ -358,10 +386,10 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
     const bool valid = tok < t1;
     const int64_t row = (int64_t)seq * a.L + (valid ? tok : t1 - 1);
     // ---------------- forward recompute -----------------
-    float xh1[16], xh2[16], xh3[16], q[16], c[16], f1[16];
-    float rs1, rs2, rs3, p[H][LC];
+    float xh1[16], xh2[16], xh3[16], f1[16];
+    float rs1, rs2, rs3;
     uint32_t km, k0 = 0xffffffffu, k1 = 0xffffffffu, k2 = 0xffffffffu;
-    const bool have = DROP && a.masks != nullptr;   // masks stored by the forward
+    constexpr bool have = DROP && MASKS;   // masks stored by the forward
     if (have) {
       const uint4 mw = *reinterpret_cast<const uint4*>(a.masks + row * 4);
       const int sh = 16 * h;
@@ -371,7 +399,7 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
       km = mw.w;
     }
     {
-      float v[16], t[16];
+      float v[16], t[16], q[16], c[16], p[H][LC];
       load_row(a.O, row, h, t);
       mv(S.Wo1, S.bo1, t, v, lane);
       load_row(a.x, row, h, t);
@@ -390,9 +418,16 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
       layernorm(v, rs1, xh1);
 #pragma unroll
       for (int r = 0; r < 16; ++r) t[r] = fmaf(xh1[r], S.g1[F(r, h)], S.be1[F(r, h)]);   // x1
+      // forward values the weight gradients need go to the scratch as soon as they
+      // exist, the normalised LN inputs wait in LDS (short live ranges: this kernel
+      // is register-bound)
+      if (valid) store_row(SV(V_X1), row, E, 0, h, t);
+      park(Pk[wave][0], xh1, lane);
       mv(S.Wq, S.bq, t, q, lane);
+      if (valid) store_row(SV(V_Q), row, E, 0, h, q);
       cross_fwd<LC>(S.kv, a.Lc, q, h, site_key(key, 3), row, DROP, a.thr, a.inv_keep, p, km, c,
                     have);
+      if (valid) store_row(SV(V_C), row, E, 0, h, c);
       mv(S.Wo2, S.bo2, c, v, lane);
       if (DROP && have) {
 #pragma unroll
@@ -409,9 +444,12 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
       layernorm(v, rs2, xh2);
 #pragma unroll
       for (int r = 0; r < 16; ++r) t[r] = fmaf(xh2[r], S.g2[F(r, h)], S.be2[F(r, h)]);   // x2
+      if (valid) store_row(SV(V_X2), row, E, 0, h, t);
+      park(Pk[wave][1], xh2, lane);
       mv(S.W1, S.b1, t, f1, lane);
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = gelu(f1[r]);
+      if (valid) store_row(SV(V_GL), row, E, 0, h, v);
       mv(S.W2, S.b2, v, v, lane);
       if (DROP && have) {
 #pragma unroll
@@ -459,10 +497,6 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
     for (int r = 0; r < 16; ++r) t[r] = ((k2 >> r) & 1u) ? d[r] * ik : 0.f;   // df2
     if (valid) store_row(SV(V_DF2), row, E, 0, h, t);
     {
-      float gl[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) gl[r] = gelu(f1[r]);
-      if (valid) store_row(SV(V_GL), row, E, 0, h, gl);
       f16v acc = {};
       mvt(S.W2, t, acc, lane);
 #pragma unroll
@@ -477,20 +511,15 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
 #pragma unroll
       for (int r = 0; r < 16; ++r) d[r] = acc[r];                        // dx2
     }
-    {
-      float x2[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) x2[r] = fmaf(xh2[r], S.g2[F(r, h)], S.be2[F(r, h)]);
-      if (valid) store_row(SV(V_X2), row, E, 0, h, x2);
-    }
     // LN2
+    unpark(Pk[wave][1], xh2, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) t[r] = d[r] * xh2[r];
     if (valid) { store_row(SV(V_DLN2), row, E, 0, h, d); store_row(SV(V_DLN2X), row, E, 0, h, t); }
     layernorm_bwd(d, xh2, S.g2, rs2, h, d);                 // dv2 (residual into x1)
 #pragma unroll
     for (int r = 0; r < 16; ++r) t[r] = ((k1 >> r) & 1u) ? d[r] * ik : 0.f;   // da2
-    if (valid) { store_row(SV(V_DA2), row, E, 0, h, t); store_row(SV(V_C), row, E, 0, h, c); }
+    if (valid) store_row(SV(V_DA2), row, E, 0, h, t);
     float dc[16];
     {
       f16v acc = {};
@@ -498,15 +527,18 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
 #pragma unroll
       for (int r = 0; r < 16; ++r) dc[r] = acc[r];
     }
-    if (valid) { store_row(SV(V_DC), row, E, 0, h, dc); store_row(SV(V_Q), row, E, 0, h, q); }
+    if (valid) store_row(SV(V_DC), row, E, 0, h, dc);
     // cross attention backward (dq -> reuse t)
     {
-      float dsv[32], pdv[32];   // j' = 4j + hd
+      // this half-wave's share of the ds / pd rows: k = 4j + hd for j in [4h, 4h + 4)
+      float dsv[16], pdv[16], q[16];
 #pragma unroll
-      for (int k = 0; k < 32; ++k) { dsv[k] = 0.f; pdv[k] = 0.f; }
+      for (int k = 0; k < 16; ++k) { dsv[k] = 0.f; pdv[k] = 0.f; }
+      load_row(SV(V_Q), row, h, q);   // this lane's own store (invalid lanes: unused)
 #pragma unroll
       for (int hd = 0; hd < H; ++hd) {
-        float dp[LC];
+        float dp[LC], ph[LC];
+        cross_probs<LC>(S.kv, a.Lc, q, h, hd, ph);
         float Dsum = 0.f;
 #pragma unroll
         for (int j = 0; j < LC; ++j) {
@@ -519,15 +551,15 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
           part = xsum32(part);
           const bool kp = (km >> (hd * LCMAX + j)) & 1u;
           dp[j] = (j < a.Lc && kp) ? part * ik : 0.f;
-          pdv[4 * j + hd] = (j < a.Lc && kp) ? p[hd][j] * ik : 0.f;
-          Dsum = fmaf(p[hd][j], dp[j], Dsum);
+          if ((j >> 2) == h) pdv[4 * (j & 3) + hd] = (j < a.Lc && kp) ? ph[j] * ik : 0.f;
+          Dsum = fmaf(ph[j], dp[j], Dsum);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) t[4 * hd + i] = 0.f;
 #pragma unroll
         for (int j = 0; j < LC; ++j) {
-          const float ds = j < a.Lc ? p[hd][j] * (dp[j] - Dsum) * scale : 0.f;
-          dsv[4 * j + hd] = ds;
+          const float ds = j < a.Lc ? ph[j] * (dp[j] - Dsum) * scale : 0.f;
+          if ((j >> 2) == h) dsv[4 * (j & 3) + hd] = ds;
           if (j < a.Lc) {
             const float* kj = S.kv + j * 2 * E + 8 * hd + 4 * h;
 #pragma unroll
@@ -535,15 +567,14 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
           }
         }
       }
-      // ds / pd rows: both half-waves hold identical values; half h writes
-      // j' in [16h, 16h+16)
+      // ds / pd rows: half h writes k in [16h, 16h + 16)
       if (valid) {
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const int k = 16 * h + 4 * g4;
-          *reinterpret_cast<float4*>(SV(V_DS) + row * E + k) =
+          const int k = 4 * g4;
+          *reinterpret_cast<float4*>(SV(V_DS) + row * E + 16 * h + k) =
               make_float4(dsv[k], dsv[k + 1], dsv[k + 2], dsv[k + 3]);
-          *reinterpret_cast<float4*>(SV(V_PD) + row * E + k) =
+          *reinterpret_cast<float4*>(SV(V_PD) + row * E + 16 * h + k) =
               make_float4(pdv[k], pdv[k + 1], pdv[k + 2], pdv[k + 3]);
         }
       }
@@ -557,13 +588,8 @@ __global__ __launch_bounds__(NT) void dec_tail_bwd_data(Tail a, float* __restric
 #pragma unroll
       for (int r = 0; r < 16; ++r) d[r] = acc[r];                        // dx1
     }
-    {
-      float x1[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) x1[r] = fmaf(xh1[r], S.g1[F(r, h)], S.be1[F(r, h)]);
-      if (valid) store_row(SV(V_X1), row, E, 0, h, x1);
-    }
     // LN1
+    unpark(Pk[wave][0], xh1, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) t[r] = d[r] * xh1[r];
     if (valid) { store_row(SV(V_DLN1), row, E, 0, h, d); store_row(SV(V_DLN1X), row, E, 0, h, t); }
@@ -723,7 +749,12 @@ int launch_fwd(const Tail& a, int grid, float*, hipStream_t s) {
 }
 template <int LC, bool NEXT, bool DROP>
 int launch_bwd(const Tail& a, int grid, float* scr, hipStream_t s) {
-  hipLaunchKernelGGL((dec_tail_bwd_data<LC, NEXT, DROP>), dim3(grid), dim3(NT), 0, s, a, scr);
+  if (DROP && !a.masks)
+    hipLaunchKernelGGL((dec_tail_bwd_data<LC, NEXT, DROP, false>), dim3(grid), dim3(NT), 0, s, a,
+                       scr);
+  else
+    hipLaunchKernelGGL((dec_tail_bwd_data<LC, NEXT, DROP, true>), dim3(grid), dim3(NT), 0, s, a,
+                       scr);
   VAESNE_CHECK_LAUNCH();
   hipLaunchKernelGGL(dec_tail_wgrad, dim3(grid, NJOB), dim3(NT), 0, s, a, (const float*)scr);
   VAESNE_CHECK_LAUNCH();
