@@ -394,6 +394,13 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
   __shared__ float Ls[TK], Dd[TK];
   __shared__ uint32_t Ws[TK * NWB];
   __shared__ __attribute__((aligned(16))) float Qw[DQ ? NWV * TK * DH : 1];   // per-wave dQ
+  // keep-bit lookup: 4 bits of the bitmap -> the two key pairs' 0/1 float masks
+  // (one conflict-free ds_read_b128 instead of ~16 bit-extract / compare / select
+  // VALU ops per query; the 16 entries fill the 64 banks exactly once)
+  __shared__ float4 Mt[16];
+  if (DROP && threadIdx.x < 16)
+    Mt[threadIdx.x] = make_float4((float)(threadIdx.x & 1), (float)((threadIdx.x >> 1) & 1),
+                                  (float)((threadIdx.x >> 2) & 1), (float)((threadIdx.x >> 3) & 1));
   const int nkb = (a.Lk + KB - 1) / KB;
   const int kb = blockIdx.x % nkb;
   const int bh = blockIdx.x / nkb;
@@ -474,7 +481,12 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
         lrow2<DH>(Qs + i * DH, qr);
         lrow2<DH>(Ds_ + i * DH, dr);
         const f2 li = bc(Ls[i]), Di = bc(Dd[i]);
-        const uint32_t kw = DROP ? (Ws[i * NWB + wl] >> sh) : 0xffffffffu;
+        f2 km[2];
+        if (DROP) {
+          const float4 t = Mt[(Ws[i * NWB + wl] >> sh) & 15u];
+          km[0] = (f2){t.x, t.y};
+          km[1] = (f2){t.z, t.w};
+        }
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
           f2 s = kbias[p], g = mul2_lo(v[p][0], dr[0]);
@@ -486,9 +498,8 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
           const f2 pr = ex2(s - li);
           f2 aP = pr, dP = g;
           if (DROP) {
-            const uint32_t m0 = (kw >> (2 * p)) & 1u, m1 = (kw >> (2 * p + 1)) & 1u;
-            aP = sel2(m0, m1, pr);
-            dP = sel2(m0, m1, g);
+            aP = pr * km[p];
+            dP = g * km[p];
           }
           const f2 dS = pr * (dP - Di);
           dSq[i - i0][p] = dS;
