@@ -242,17 +242,29 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
           x[p] = __builtin_elementwise_max(x[p], acc);
         }
       }
+      // Lazy rescaling: m is the exponent origin, moved (and o, l rescaled) only
+      // when some row's running max x passes it by more than 8 (p <= 2^8, no
+      // overflow) -- a wave-uniform branch taken on the first groups only.
+      bool move = false;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) move |= (x[p].x > m[p].x + 8.f) | (x[p].y > m[p].y + 8.f);
+      if (__any(move)) {
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          // rows whose keys are all masked so far keep m = -inf: exponent origin 0
+          const f2 mo = (f2){m[p].x == -INFINITY ? 0.f : m[p].x, m[p].y == -INFINITY ? 0.f : m[p].y};
+          const f2 mn = (f2){x[p].x == -INFINITY ? 0.f : x[p].x, x[p].y == -INFINITY ? 0.f : x[p].y};
+          const f2 c = ex2(mo - mn);
+          m[p] = x[p];
+          l[p] *= c;
+#pragma unroll
+          for (int d = 0; d < DH; ++d) o[p][d] *= c;
+        }
+      }
       f2 mu[NP];
 #pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        // rows whose keys are all masked so far keep m = -inf: exponent origin 0
-        mu[p] = (f2){x[p].x == -INFINITY ? 0.f : x[p].x, x[p].y == -INFINITY ? 0.f : x[p].y};
-        const f2 c = ex2(m[p] - mu[p]);
-        m[p] = x[p];
-        l[p] *= c;
-#pragma unroll
-        for (int d = 0; d < DH; ++d) o[p][d] *= c;
-      }
+      for (int p = 0; p < NP; ++p)
+        mu[p] = (f2){m[p].x == -INFINITY ? 0.f : m[p].x, m[p].y == -INFINITY ? 0.f : m[p].y};
 #pragma unroll
       for (int u = 0; u < 8; u += 2) {
         f2 p0[NP], p1[NP];
