@@ -1,0 +1,48 @@
+"""HBM bytes per launch of the roofline kernels from two rocprofv3 --pmc passes
+(FETCH_SIZE, WRITE_SIZE) over `bench.py --roofline-only`, corrected as
+MI355X_MICROARCH.md's HBM section prescribes for gfx950:
+bytes = 1024 * (2 * FETCH_SIZE + WRITE_SIZE)   (FETCH_SIZE in kB reports half
+the bytes of wide coalesced reads).  Writes profiles/pmc_traffic.json.
+    python profiles/pmc_traffic.py <fetch.csv> <write.csv> <source-label>"""
+import collections
+import csv
+import json
+import os
+import re
+import sys
+
+KERNELS = ("attn_fwd_kernel", "attn_bwd_kv_kernel")
+
+
+def per_kernel(path, counter):
+    vals = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        name = re.sub(r"^void ", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))
+        name = name.split("(")[0]
+        if name.startswith(KERNELS) and "<8, 256, 2, true" in name:
+            vals[name].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+def main(fetch, write, label):
+    f, w = per_kernel(fetch, "FETCH_SIZE"), per_kernel(write, "WRITE_SIZE")
+    out = {"source": f"{label} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
+                     "bench.py --roofline-only)",
+           "correction": "MI355X_MICROARCH.md HBM section: FETCH_SIZE (kB) reports half the "
+                         "bytes of wide coalesced reads on gfx950 -> bytes = 1024*(2*FETCH_SIZE "
+                         "+ WRITE_SIZE)",
+           "kernels": {}}
+    for inst in sorted(f):
+        base = inst.split("<")[0]
+        if inst in w:
+            out["kernels"][base] = {"instance": inst,
+                                    "hbm_bytes_per_launch": int(1024 * (2 * f[inst] + w[inst]))}
+    dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), "pmc_traffic.json")
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
