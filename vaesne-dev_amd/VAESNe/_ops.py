@@ -109,6 +109,77 @@ def linear(x, weight, bias=None, act=None, x2=None, base=None):
     return LinearFn.apply(x, weight, bias, ACT[act], x2, base)
 
 
+class InProjPairFn(torch.autograd.Function):
+    """Cross-attention in-projection: q = query W[:E]^T + b[:E] and
+    kv = key W[E:]^T + b[E:] (functional.py's in_proj split, as
+    util_layers.py:301 calls it), returning ONE gradient tensor for the whole
+    in_proj weight / bias: autograd's per-slice glue (zero fill + copy + add for
+    each of the four slices) would otherwise add ~8 launches per block."""
+
+    @staticmethod
+    def forward(ctx, query, key, W, b):
+        _lib.require_device(query, key, W, b)
+        _f32(query)
+        E = W.shape[1]
+        W = W.contiguous()
+        b = b.contiguous() if b is not None else None
+        qr, Mq, ldq = _rows(query)
+        kr, Mk, ldk = _rows(key)
+        dev = query.device
+        q = torch.empty((Mq, E), dtype=torch.float32, device=dev)
+        kv = torch.empty((Mk, 2 * E), dtype=torch.float32, device=dev)
+        s = stream()
+        bp = ptr(b)
+        lib.linear_fwd(qr.data_ptr(), ldq, None, 0, Mq, E, W.data_ptr(), bp, E, q.data_ptr(), E,
+                       None, 0, 0, 0, s)
+        lib.linear_fwd(kr.data_ptr(), ldk, None, 0, Mk, E, W.data_ptr() + 4 * E * E,
+                       None if bp is None else bp + 4 * E, 2 * E, kv.data_ptr(), 2 * E,
+                       None, 0, 0, 0, s)
+        ctx.meta = (E, Mq, ldq, Mk, ldk, query.shape, key.shape, b is not None)
+        ctx.save_for_backward(qr, kr, W)
+        return q.view(*query.shape[:-1], E), kv.view(*key.shape[:-1], 2 * E)
+
+    @staticmethod
+    def backward(ctx, dq, dkv):
+        qr, kr, W = ctx.saved_tensors
+        E, Mq, ldq, Mk, ldk, qshape, kshape, has_b = ctx.meta
+        dev = qr.device
+        dq = torch.zeros((Mq, E), dtype=torch.float32, device=dev) if dq is None \
+            else dq.contiguous()
+        dkv = torch.zeros((Mk, 2 * E), dtype=torch.float32, device=dev) if dkv is None \
+            else dkv.contiguous()
+        s = stream()
+        ng = ctx.needs_input_grad
+        dquery = dkey = dW = db = None
+        if ng[0]:
+            dquery = torch.empty((Mq, E), dtype=torch.float32, device=dev)
+            lib.linear_bwd_data(dq.data_ptr(), E, None, 0, 0, Mq, E, W.data_ptr(), E,
+                                dquery.data_ptr(), E, 0, s)
+            dquery = dquery.view(qshape)
+        if ng[1]:
+            dkey = torch.empty((Mk, E), dtype=torch.float32, device=dev)
+            lib.linear_bwd_data(dkv.data_ptr(), 2 * E, None, 0, 0, Mk, 2 * E,
+                                W.data_ptr() + 4 * E * E, E, dkey.data_ptr(), E, 0, s)
+            dkey = dkey.view(kshape)
+        if ng[2] or ng[3]:
+            dW = torch.empty((3 * E, E), dtype=torch.float32, device=dev)
+            db = torch.empty((3 * E,), dtype=torch.float32, device=dev) if has_b else None
+            ws = _ws(max(lib.linear_bwd_weight_workspace(Mq, E, E),
+                         lib.linear_bwd_weight_workspace(Mk, 2 * E, E)), dev)
+            dbp = ptr(db)
+            lib.linear_bwd_weight(dq.data_ptr(), E, None, 0, 0, qr.data_ptr(), ldq, None, 0,
+                                  Mq, E, E, dW.data_ptr(), dbp, 0, ws.data_ptr(), s)
+            lib.linear_bwd_weight(dkv.data_ptr(), 2 * E, None, 0, 0, kr.data_ptr(), ldk, None, 0,
+                                  Mk, 2 * E, E, dW.data_ptr() + 4 * E * E,
+                                  None if dbp is None else dbp + 4 * E, 0, ws.data_ptr(), s)
+        return dquery, dkey, dW if ng[2] else None, db if ng[3] else None
+
+
+def in_proj_pair(query, key, weight, bias):
+    """(q, kv) of a cross-attention in-projection with whole-tensor gradients."""
+    return InProjPairFn.apply(query, key, weight, bias)
+
+
 # ---------------------------------------------------------------------------
 # residual + dropout + LayerNorm
 # ---------------------------------------------------------------------------

@@ -143,8 +143,7 @@ class MultiheadAttention(nn.MultiheadAttention):
             qkv = _ops.linear(query, W, b)
             o = _ops.self_attention(qkv, key_padding_mask, H, p)
         else:
-            q = _ops.linear(query, W[:E], b[:E])
-            kv = _ops.linear(key, W[E:], b[E:])
+            q, kv = _ops.in_proj_pair(query, key, W, b)
             o = _ops.cross_attention(q, kv, key_padding_mask, H, p)
         return _ops.linear(o, self.out_proj.weight, self.out_proj.bias), None
 
