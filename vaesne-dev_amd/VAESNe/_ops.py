@@ -250,7 +250,20 @@ def _bias_of(mask, kbias):
         return None
     if mask.dtype == torch.float32:
         return mask.contiguous()
-    return key_bias(mask)
+    # the encoders hand the same mask tensor to every layer's two attentions:
+    # convert it once (identity + version checked; the entry holds the mask, so
+    # its storage cannot be recycled under the cache)
+    for ent in _KBIAS_CACHE:
+        if ent[0] is mask and ent[1] == mask._version and ent[2].device == mask.device:
+            return ent[2]
+    kb = key_bias(mask)
+    _KBIAS_CACHE.append((mask, mask._version, kb))
+    if len(_KBIAS_CACHE) > 8:
+        _KBIAS_CACHE.pop(0)
+    return kb
+
+
+_KBIAS_CACHE = []
 
 
 def _attn_ws(B, H, Lq, Lk, dh, bwd, dev):
