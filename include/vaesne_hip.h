@@ -153,6 +153,32 @@ int vaesne_dec_tail_bwd(const float* x, const float* O, const float* kvc, int M,
                         float* gflat, float* workspace, void* stream);
 int vaesne_dec_tail_grad_layout(int* offsets);
 
+/* ---- encoder-block halves ------------------------------------------------------
+ * An encoder TransformerBlock (util_layers.py:285-309 as called by
+ * SpectraLayers.py:135-136 / PhotometricLayers.py:141-143) over the B * latent
+ * tokens, split around its cross-attention to the data tokens (the attention core
+ * runs in vaesne_attn_fwd/bwd):
+ *   mode 1 (PRE):  x, O = self-attention core output -> y = x1 = LN1(x + Drop(O Wo1^T
+ *                  + bo1)), q_or_qkv = q = x1 Wq^T + bq  [M, 32]
+ *   mode 2 (POST): x = x1, O = cross-attention core output c -> x2 = LN2(x1 +
+ *                  Drop(c Wo2^T + bo2)), FFN(GELU), y = LN3(x2 + Drop(f)),
+ *                  q_or_qkv = y Wn^T + bn [M, 96] (when Wn, the next block's in_proj)
+ * w: the 18-pointer array of vaesne_dec_tail_fwd (entries the mode does not use may
+ * be null); gflat / its layout as vaesne_dec_tail_bwd (the other half's entries
+ * are 0).  bwd: dy = d y; dq_or_dqkv = d q (PRE) or d qkv_next (POST, iff Wn);
+ * dx = d x (PRE) / d x1 (POST); dO = d O (PRE) / d c (POST).  drop_masks: uint32
+ * [M][4], required when p_drop > 0 (written by fwd, read by bwd).  Workspace sized
+ * by vaesne_enc_block_workspace(M). */
+int64_t vaesne_enc_block_workspace(int M);
+int vaesne_enc_block_fwd(int mode, const float* x, const float* O, int M, const float* const* w,
+                         float p_drop, const int64_t* rng_state, uint32_t call_id, float* y,
+                         float* q_or_qkv, uint32_t* drop_masks, void* stream);
+int vaesne_enc_block_bwd(int mode, const float* x, const float* O, int M, const float* const* w,
+                         float p_drop, const int64_t* rng_state, uint32_t call_id,
+                         const float* y, const float* dy, const float* dq_or_dqkv,
+                         const uint32_t* drop_masks, float* dx, float* dO, float* gflat,
+                         float* workspace, void* stream);
+
 /* ---- embeddings ------------------------------------------------------------
  * [sin(x*div) | cos(x*div)]: util_layers.py:125-129 (plain, 16 freqs) and
  * :142-146 (MLP form, 32 freqs).  x is read at index r % period, so the

@@ -420,3 +420,77 @@ def test_fused_decoder_tail_stored_masks_match_rehash():
     assert torch.equal(res[0][0], res[1][0])   # forward: same kernel both times
     for a, b in zip(res[0][1:], res[1][1:]):
         assert (a - b).abs().max().item() <= 1e-5 * max(a.abs().max().item(), 1e-3)
+
+
+def _encoder_blocks(n, seed, selfattn):
+    from VAESNe.util_layers import TransformerBlock
+    torch.manual_seed(seed)
+    blocks = torch.nn.ModuleList([TransformerBlock(32, 4, 32, 0.0, selfattn) for _ in range(n)])
+    with torch.no_grad():
+        for prm in blocks.parameters():
+            prm.add_(0.1 * torch.randn_like(prm))
+    return blocks
+
+
+@pytest.mark.parametrize("selfattn,B,T,Lc", [(False, 16, 8, 60), (True, 5, 8, 129), (False, 3, 5, 37)])
+def test_fused_encoder_stack_matches_per_op(selfattn, B, T, Lc):
+    """util_layers.encoder_stack (PRE / cross-attention / POST kernels) against the
+    per-op TransformerBlock chain on the same blocks: outputs and every gradient."""
+    from VAESNe.util_layers import encoder_stack
+    blocks = _encoder_blocks(3, B + Lc, selfattn).to(DEV)
+    blocks.train()
+    g = torch.Generator().manual_seed(Lc)
+    x = torch.randn(B, T, 32, generator=g).to(DEV)
+    ctx = torch.randn(B, Lc, 32, generator=g).to(DEV)
+    mask = _rand_mask(B, Lc, 0.1, g).to(DEV)
+    go = torch.randn(B, T, 32, generator=g).to(DEV)
+    res = []
+    for fused in (True, False):
+        blocks.zero_grad(set_to_none=True)
+        xx = x.clone().requires_grad_(True)
+        cc = ctx.clone().requires_grad_(True)
+        if fused:
+            out = encoder_stack(blocks, xx, cc, context_mask=mask)
+        else:
+            out = xx
+            for blk in blocks:
+                out = blk(out, cc, context_mask=mask)
+        (out * go).sum().backward()
+        res.append([out, xx.grad, cc.grad] + [p.grad.clone() for p in blocks.parameters()])
+    names = ["out", "dx", "dcontext"] + [n for n, _ in blocks.named_parameters()]
+    for n, a, b in zip(names, *res):
+        assert _rel(a, b) < 2e-5, n
+
+
+def test_fused_encoder_stack_dropout_fwd_bwd_consistent():
+    """With dropout on, the encoder halves' backward replays the forward's masks:
+    a directional finite difference matches <grad, v>."""
+    from VAESNe import rng
+    from VAESNe.util_layers import encoder_stack
+    blocks = _encoder_blocks(2, 9, True).to(DEV)
+    for b in blocks:
+        b.dropout.p = 0.1
+        b.self_attn.dropout = 0.1
+        b.cross_attn.dropout = 0.1
+        b.context_self_attn.dropout = 0.1
+    blocks.train()
+    g = torch.Generator().manual_seed(21)
+    B, T, Lc = 4, 8, 70
+    x = torch.randn(B, T, 32, generator=g).to(DEV)
+    ctx = torch.randn(B, Lc, 32, generator=g).to(DEV)
+    go = torch.randn(B, T, 32, generator=g).to(DEV)
+    v = torch.randn(B, T, 32, generator=g).to(DEV)
+
+    def f(xx, grad=False):
+        rng._call = 300
+        xx = xx.clone().requires_grad_(grad)
+        out = encoder_stack(blocks, xx, ctx)
+        return xx, (out * go).sum()
+
+    xx, val = f(x, True)
+    val.backward()
+    dirn = (xx.grad * v).sum().item()
+    eps = 1e-2
+    with torch.no_grad():
+        fd = (f(x + eps * v)[1].item() - f(x - eps * v)[1].item()) / (2 * eps)
+    assert abs(fd - dirn) < 2e-2 * abs(dirn) + 1e-3, (fd, dirn)

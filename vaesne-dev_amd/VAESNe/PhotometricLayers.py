@@ -9,7 +9,7 @@ from torch import nn
 from . import _ops
 from .util_layers import (MLP, Linear, SinusoidalMLPPositionalEmbedding,
                           SinusoidalPositionalEmbedding, TransformerBlock, decoder_stack,
-                          singlelayerMLP)
+                          singlelayerMLP, encoder_stack)
 
 
 class photometricTransformerDecoder(nn.Module):
@@ -75,7 +75,5 @@ class photometricTransformerEncoder(nn.Module):
             tok = _ops.embedding(band, self.bandembd.weight,
                                  base=self.fluxfc(flux[:, :, None], base=self.time_embd(time)))
         x = _ops.repeat_batch(self.initbottleneck, flux.shape[0])
-        h = x
-        for transformerblock in self.transformerblocks:
-            h = transformerblock(h, tok, mask=None, context_mask=mask)
+        h = encoder_stack(self.transformerblocks, x, tok, context_mask=mask)
         return self.bottleneckfc(x, h)   # bottleneckfc(x + h)

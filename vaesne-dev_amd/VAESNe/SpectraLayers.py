@@ -11,7 +11,7 @@ from torch import nn
 from . import _ops
 from .util_layers import (MLP, Linear, SinusoidalMLPPositionalEmbedding,
                           SinusoidalPositionalEmbedding, TransformerBlock, decoder_stack,
-                          singlelayerMLP)
+                          singlelayerMLP, encoder_stack)
 
 
 class spectraTransformerDecoder(nn.Module):
@@ -77,7 +77,5 @@ class spectraTransformerEncoder(nn.Module):
             mask = torch.cat([mask, torch.zeros(mask.shape[0], 1, dtype=mask.dtype,
                                                 device=mask.device)], dim=1)
         x = _ops.repeat_batch(self.initbottleneck, context.shape[0])
-        h = x
-        for transformerblock in self.transformerblocks:
-            h = transformerblock(h, context, context_mask=mask)
+        h = encoder_stack(self.transformerblocks, x, context, context_mask=mask)
         return self.bottleneckfc(x, h)   # bottleneckfc(x + h)

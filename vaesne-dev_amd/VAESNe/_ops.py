@@ -782,3 +782,133 @@ class DecTailFn(torch.autograd.Function):
               for j, (t, o) in enumerate(zip(w[:4] + w[6:], offs[:4] + offs[6:]))]
         return (None, None, dx.view(xshape), dO, dctx, dWc if ng[5] else None,
                 dbc if ng[6] else None, *gw)
+
+
+# ---------------------------------------------------------------------------
+# encoder-block halves (vaesne_enc_block_*): the latent-token side of an
+# encoder TransformerBlock around its cross-attention core
+# ---------------------------------------------------------------------------
+class EncPreFn(torch.autograd.Function):
+    """(x [B, T, 32], self-attention core output O, data tokens `context`,
+    self-attn out_proj W/b, LN1 g/b, cross in_proj Wc [96, 32] / bc [96])
+    -> (x1, q, kv): x1 = LN1(x + Drop(O Wo1^T + bo1)), q = x1 Wc[:32]^T + bc[:32]
+    (one kernel) and kv = context Wc[32:]^T + bc[32:] (the context k|v
+    projection, util_layers.py:301).  The whole in_proj gradient comes back as
+    one tensor."""
+
+    @staticmethod
+    def forward(ctx, p, x, O, context, Wo1, bo1, g1, be1, Wc, bc):
+        _lib.require_device(x, O, context, Wo1, bo1, g1, be1, Wc, bc)
+        E = 32
+        x, O, context = x.contiguous(), O.contiguous(), context.contiguous()
+        w = [t.contiguous() for t in (Wo1, bo1, g1, be1, Wc, bc)]
+        M = x.numel() // E
+        Mc = context.numel() // E
+        dev = x.device
+        x1 = torch.empty((M, E), dtype=torch.float32, device=dev)
+        q = torch.empty((M, E), dtype=torch.float32, device=dev)
+        kv = torch.empty((Mc, 2 * E), dtype=torch.float32, device=dev)
+        st = rng.state(dev) if p > 0 else None
+        cid = rng.next_call_id() if p > 0 else 0
+        masks = torch.empty((M, 4), dtype=torch.int32, device=dev) if p > 0 else None
+        s = stream()
+        lib.enc_block_fwd(1, x.data_ptr(), O.data_ptr(), M, _lib.ptr_array(w + [None] * 12),
+                          float(p), ptr(st), cid, x1.data_ptr(), q.data_ptr(), ptr(masks), s)
+        lib.linear_fwd(context.data_ptr(), E, None, 0, Mc, E, w[4].data_ptr() + 4 * E * E,
+                       w[5].data_ptr() + 4 * E, 2 * E, kv.data_ptr(), 2 * E, None, 0, 0, 0, s)
+        ctx.meta = (float(p), cid, M, Mc, x.shape, context.shape)
+        ctx.save_for_backward(x, O, context, x1, st, masks, *w)
+        return x1.view(x.shape), q.view(x.shape), kv.view(*context.shape[:-1], 2 * E)
+
+    @staticmethod
+    def backward(ctx, dx1, dq, dkv):
+        x, O, context, x1, st, masks, *w = ctx.saved_tensors
+        p, cid, M, Mc, xshape, cshape = ctx.meta
+        E = 32
+        dev = x.device
+        dx1 = torch.zeros((M, E), dtype=torch.float32, device=dev) if dx1 is None \
+            else dx1.contiguous()
+        dq = torch.zeros((M, E), dtype=torch.float32, device=dev) if dq is None \
+            else dq.contiguous()
+        dkv = torch.zeros((Mc, 2 * E), dtype=torch.float32, device=dev) if dkv is None \
+            else dkv.contiguous()
+        dx = torch.empty_like(x)
+        dO = torch.empty_like(O)
+        offs, total = _tail_layout()
+        gflat = torch.empty(total, dtype=torch.float32, device=dev)
+        s = stream()
+        ws = _ws(lib.enc_block_workspace(M), dev)
+        lib.enc_block_bwd(1, x.data_ptr(), O.data_ptr(), M, _lib.ptr_array(w + [None] * 12),
+                          p, ptr(st), cid, x1.data_ptr(), dx1.data_ptr(), dq.data_ptr(),
+                          ptr(masks), dx.data_ptr(), dO.data_ptr(), gflat.data_ptr(),
+                          ws.data_ptr(), s)
+        Wc = w[4]
+        dWc = torch.empty_like(Wc)
+        dbc = torch.empty_like(w[5])
+        lib.pack(_lib.ptr_array([dWc, dbc]), (C.c_int64 * 2)(offs[4], offs[5]),
+                 (C.c_int64 * 2)(E * E, E), 2, gflat.data_ptr(), 1, s)
+        wsk = _ws(lib.linear_bwd_weight_workspace(Mc, 2 * E, E), dev)
+        lib.linear_bwd_weight(dkv.data_ptr(), 2 * E, None, 0, 0, context.data_ptr(), E, None, 0,
+                              Mc, 2 * E, E, dWc.data_ptr() + 4 * E * E, dbc.data_ptr() + 4 * E, 0,
+                              wsk.data_ptr(), s)
+        dctx = torch.empty_like(context)
+        lib.linear_bwd_data(dkv.data_ptr(), 2 * E, None, 0, 0, Mc, 2 * E,
+                            Wc.data_ptr() + 4 * E * E, E, dctx.data_ptr(), E, 0, s)
+        gw = [gflat[o:o + t.numel()].view_as(t) for t, o in zip(w[:4], offs[:4])]
+        return (None, dx.view(xshape), dO, dctx.view(cshape), *gw, dWc, dbc)
+
+
+class EncPostFn(torch.autograd.Function):
+    """(x1, cross-attention core output c, cross out_proj W/b, LN2 g/b, FFN
+    W1/b1/W2/b2, LN3 g/b, next block's self in_proj Wn/bn or None)
+    -> (y [, qkv_next]): one kernel for util_layers.py:301-309 (+ the next
+    block's in_proj) over the latent tokens."""
+
+    @staticmethod
+    def forward(ctx, p, x1, c, *w12):
+        _lib.require_device(x1, c, *w12)
+        E = 32
+        x1, c = x1.contiguous(), c.contiguous()
+        w = [None if t is None else t.contiguous() for t in w12]
+        nxt = w[10] is not None
+        M = x1.numel() // E
+        dev = x1.device
+        y = torch.empty((M, E), dtype=torch.float32, device=dev)
+        qkv = torch.empty((M, 3 * E), dtype=torch.float32, device=dev) if nxt else None
+        st = rng.state(dev) if p > 0 else None
+        cid = rng.next_call_id() if p > 0 else 0
+        masks = torch.empty((M, 4), dtype=torch.int32, device=dev) if p > 0 else None
+        lib.enc_block_fwd(2, x1.data_ptr(), c.data_ptr(), M, _lib.ptr_array([None] * 6 + w),
+                          float(p), ptr(st), cid, y.data_ptr(), ptr(qkv), ptr(masks), stream())
+        ctx.meta = (float(p), cid, M, nxt, x1.shape)
+        ctx.save_for_backward(x1, c, y, st, masks, *w)
+        y = y.view(x1.shape)
+        if nxt:
+            return y, qkv.view(*x1.shape[:-1], 3 * E)
+        return y, None
+
+    @staticmethod
+    def backward(ctx, dy, dqkv):
+        x1, c, y, st, masks, *w = ctx.saved_tensors
+        p, cid, M, nxt, xshape = ctx.meta
+        E = 32
+        dev = x1.device
+        dy = torch.zeros_like(y) if dy is None else dy.contiguous()
+        if nxt:
+            dqkv = torch.zeros((M, 3 * E), dtype=torch.float32, device=dev) if dqkv is None \
+                else dqkv.contiguous()
+        else:
+            dqkv = None
+        dx1 = torch.empty_like(x1)
+        dc = torch.empty_like(c)
+        offs, total = _tail_layout()
+        gflat = torch.empty(total, dtype=torch.float32, device=dev)
+        ws = _ws(lib.enc_block_workspace(M), dev)
+        lib.enc_block_bwd(2, x1.data_ptr(), c.data_ptr(), M, _lib.ptr_array([None] * 6 + w),
+                          p, ptr(st), cid, y.data_ptr(), dy.data_ptr(), ptr(dqkv), ptr(masks),
+                          dx1.data_ptr(), dc.data_ptr(), gflat.data_ptr(), ws.data_ptr(),
+                          stream())
+        ng = ctx.needs_input_grad
+        gw = [gflat[o:o + t.numel()].view_as(t) if (t is not None and ng[3 + j]) else None
+              for j, (t, o) in enumerate(zip(w, offs[6:]))]
+        return (None, dx1.view(xshape), dc, *gw)

@@ -230,6 +230,52 @@ def decoder_stack(blocks, x, context, mask=None):
     return x
 
 
+def _fusable_encoder_block(blk):
+    E = blk.layernorm1.normalized_shape[0]
+    return (E == 32 and blk.self_attn.num_heads == 4 and blk.cross_attn.num_heads == 4
+            and blk.ffn[0].out_features == 32
+            and all(ln.eps == 1e-5 for ln in (blk.layernorm1, blk.layernorm2, blk.layernorm3)))
+
+
+def encoder_stack(blocks, x, context, context_mask=None):
+    """`for blk in blocks: x = blk(x, context, context_mask=context_mask)` for the
+    encoders (SpectraLayers.py:135-136, PhotometricLayers.py:141-143: unmasked
+    latent tokens x, the ORIGINAL data tokens as every block's context).  With the
+    reference's shape each block runs as: latent self-attention core -> PRE
+    (out_proj, LN1, cross q) + context k|v projection -> cross-attention core ->
+    POST (out_proj, LN2, FFN, LN3 and the next block's in_proj).  The optional
+    context self-attention (spectra `selfattn`) stays on its per-op path."""
+    blocks = list(blocks)
+    if not blocks or not all(_fusable_encoder_block(b) for b in blocks) or x.dim() != 3:
+        for blk in blocks:
+            x = blk(x, context, context_mask=context_mask)
+        return x
+    b0 = blocks[0].self_attn
+    qkv = _ops.linear(x, b0.in_proj_weight, b0.in_proj_bias)
+    for i, blk in enumerate(blocks):
+        p = blk.dropout.p if blk.training else 0.0
+        pa = blk.self_attn.dropout if blk.training else 0.0
+        pc = blk.cross_attn.dropout if blk.training else 0.0
+        O = _ops.self_attention(qkv, None, blk.self_attn.num_heads, pa)
+        ctx = context
+        if blk.context_self_attn is not None:
+            c, _ = blk.context_self_attn(context, context, context, key_padding_mask=context_mask)
+            ctx = _ops.add_layernorm(context, c, blk.layernorm_context, p)
+        x1, q, kv = _ops.EncPreFn.apply(
+            p, x, O, ctx, blk.self_attn.out_proj.weight, blk.self_attn.out_proj.bias,
+            blk.layernorm1.weight, blk.layernorm1.bias,
+            blk.cross_attn.in_proj_weight, blk.cross_attn.in_proj_bias)
+        c = _ops.cross_attention(q, kv, context_mask, blk.cross_attn.num_heads, pc)
+        nxt = blocks[i + 1].self_attn if i + 1 < len(blocks) else None
+        x, qkv = _ops.EncPostFn.apply(
+            p, x1, c, blk.cross_attn.out_proj.weight, blk.cross_attn.out_proj.bias,
+            blk.layernorm2.weight, blk.layernorm2.bias,
+            blk.ffn[0].weight, blk.ffn[0].bias, blk.ffn[2].weight, blk.ffn[2].bias,
+            blk.layernorm3.weight, blk.layernorm3.bias,
+            None if nxt is None else nxt.in_proj_weight, None if nxt is None else nxt.in_proj_bias)
+    return x
+
+
 ############## vae use ###################
 def get_mean(d, K=100):
     """util_layers.py:313-323."""

@@ -72,7 +72,19 @@ struct Tail {
   float* dO;           // [M, 32]
   float* wpart;        // [G][WPART]
   float* cpart;        // [chunks][Nseq * Lc * 64]
+  int mode;            // MODE_FULL (decoder block tail) / MODE_PRE / MODE_POST (encoder halves)
 };
+
+// Encoder blocks (util_layers.py:285-309 with the cross-attention over the
+// ~60 / 984 data tokens, too many for the in-register cross attention of the
+// tail) run as two halves around the external cross-attention kernel:
+//   PRE : a1 = O Wo1^T + bo1, x1 = LN1(x + Drop(a1)), q = x1 Wq^T + bq
+//   POST: a2 = c Wo2^T + bo2, x2 = LN2(x1 + Drop(a2)), FFN, y = LN3(x2 + Drop(f)),
+//         [qkv_next = y Wn^T + bn]
+// over the B * latent tokens (one "sequence" of M rows), replacing ~10 forward and
+// ~25 backward op-level launches per block (graph launches of tiny kernels cost
+// ~5 us each).
+enum Mode { MODE_FULL = 0, MODE_PRE = 1, MODE_POST = 2 };
 
 // --- LDS image of the weights --------------------------------------------
 struct __attribute__((aligned(16))) Smem {
@@ -609,6 +621,269 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   }
 }
 
+// ============================ encoder halves ================================
+__device__ void stage_pre(Smem& S, const Tail& a) {
+  stage_w(S.Wo1, a.Wo1, E); stage_w(S.Wq, a.Wq, E);
+  stage_v(S.bo1, a.bo1, E); stage_v(S.bq, a.bq, E); stage_v(S.g1, a.g1, E); stage_v(S.be1, a.be1, E);
+}
+__device__ void stage_post(Smem& S, const Tail& a, bool next) {
+  stage_w(S.Wo2, a.Wo2, E); stage_w(S.W1, a.W1, E); stage_w(S.W2, a.W2, E);
+  if (next) { stage_w(S.Wn, a.Wn, 3 * E); stage_v(S.bn, a.bn, 3 * E); }
+  stage_v(S.bo2, a.bo2, E); stage_v(S.b1, a.b1, E); stage_v(S.b2, a.b2, E);
+  stage_v(S.g2, a.g2, E); stage_v(S.be2, a.be2, E); stage_v(S.g3, a.g3, E); stage_v(S.be3, a.be3, E);
+}
+
+// residual dropout of one site: v *= keep / (1 - p); keep bits recorded in m16[slot]
+template <bool DROP>
+__device__ __forceinline__ void drop_site_fwd(float (&v)[16], uint32_t key, int site, int64_t row,
+                                              int h, const Tail& a, uint16_t* m16, int slot,
+                                              bool keep_masks) {
+  if (!DROP) return;
+  float sc[16];
+  drop_res(site_key(key, site), row, h, a.thr, a.inv_keep, sc);
+  uint32_t m = 0u;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; m |= (sc[r] != 0.f ? 1u : 0u) << r; }
+  if (keep_masks) m16[slot] = (uint16_t)m;
+}
+
+template <bool DROP>
+__global__ __launch_bounds__(NT) void enc_pre_fwd(Tail a) {
+  __shared__ Smem S;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  stage_pre(S, a);
+  __syncthreads();
+  const uint32_t key = DROP ? key_of(a.rng, a.call_id) : 0u;
+  const int t0 = blockIdx.x * a.chunk, t1 = min(a.M, t0 + a.chunk);
+  for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32) {
+    const int tok = tt + (lane & 31);
+    const bool valid = tok < t1;
+    const int64_t row = valid ? tok : t1 - 1;
+    float xin[16], v[16], xh[16], rs;
+    load_row(a.O, row, h, v);
+    mv(S.Wo1, S.bo1, v, v, lane);                          // a1
+    load_row(a.x, row, h, xin);
+    uint16_t* m16 = reinterpret_cast<uint16_t*>(a.masks) + row * 8 + h;
+    drop_site_fwd<DROP>(v, key, 0, row, h, a, m16, 0, DROP && a.masks != nullptr && valid);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += xin[r];
+    layernorm(v, rs, xh);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xin[r] = fmaf(xh[r], S.g1[F(r, h)], S.be1[F(r, h)]);  // x1
+    if (valid) store_row(a.y, row, E, 0, h, xin);
+    mv(S.Wq, S.bq, xin, v, lane);                           // q
+    if (valid) store_row(a.qkv, row, E, 0, h, v);
+  }
+}
+
+template <bool NEXT, bool DROP>
+__global__ __launch_bounds__(NT) void enc_post_fwd(Tail a) {
+  __shared__ Smem S;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  stage_post(S, a, NEXT);
+  __syncthreads();
+  const uint32_t key = DROP ? key_of(a.rng, a.call_id) : 0u;
+  const int t0 = blockIdx.x * a.chunk, t1 = min(a.M, t0 + a.chunk);
+  for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32) {
+    const int tok = tt + (lane & 31);
+    const bool valid = tok < t1;
+    const int64_t row = valid ? tok : t1 - 1;
+    float xin[16], v[16], xh[16], rs;
+    const bool km = DROP && a.masks != nullptr && valid;
+    uint16_t* m16 = reinterpret_cast<uint16_t*>(a.masks) + row * 8 + h;
+    load_row(a.O, row, h, v);
+    mv(S.Wo2, S.bo2, v, v, lane);                           // a2
+    load_row(a.x, row, h, xin);                             // x1
+    drop_site_fwd<DROP>(v, key, 1, row, h, a, m16, 2, km);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += xin[r];
+    layernorm(v, rs, xh);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) xin[r] = fmaf(xh[r], S.g2[F(r, h)], S.be2[F(r, h)]);  // x2
+    mv(S.W1, S.b1, xin, v, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = gelu(v[r]);
+    mv(S.W2, S.b2, v, v, lane);                             // f
+    drop_site_fwd<DROP>(v, key, 2, row, h, a, m16, 4, km);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += xin[r];
+    layernorm(v, rs, xh);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = fmaf(xh[r], S.g3[F(r, h)], S.be3[F(r, h)]);    // y
+    if (valid) store_row(a.y, row, E, 0, h, v);
+    if (NEXT) {
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        float o[16];
+        mv(S.Wn + cc * E * LP, S.bn + cc * E, v, o, lane);
+        if (valid) store_row(a.qkv, row, 3 * E, cc * E, h, o);
+      }
+    }
+  }
+}
+
+// keep bits of one residual site (16 per half) from the forward's stored words
+__device__ __forceinline__ uint32_t site_mask(const Tail& a, int64_t row, int word, int h) {
+  return (a.masks[row * 4 + word] >> (16 * h)) & 0xffffu;
+}
+template <bool DROP>
+__device__ __forceinline__ void drop_apply(float (&v)[16], uint32_t k, float ik) {
+  if (!DROP) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] *= ((k >> r) & 1u) ? ik : 0.f;
+}
+
+// PRE backward: dy = d x1 (from POST and the residual), dqkv = d q [M, 32];
+// writes dx, dO and the scratch vectors of Wo1 / Wq / LN1
+template <bool DROP>
+__global__ __launch_bounds__(NT) void enc_pre_bwd_data(Tail a, float* __restrict__ scr) {
+  __shared__ Smem S;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  stage_pre(S, a);
+  __syncthreads();
+  const int64_t MS = (int64_t)a.M * E;
+  auto SV = [&](int v) { return scr + v * MS; };
+  const float ik = DROP ? a.inv_keep : 1.f;
+  const int t0 = blockIdx.x * a.chunk, t1 = min(a.M, t0 + a.chunk);
+  for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32) {
+    const int tok = tt + (lane & 31);
+    const bool valid = tok < t1;
+    const int64_t row = valid ? tok : t1 - 1;
+    const uint32_t k0 = DROP ? site_mask(a, row, 0, h) : 0xffffu;
+    float v[16], t[16], xh1[16], rs1;
+    load_row(a.O, row, h, t);
+    mv(S.Wo1, S.bo1, t, v, lane);
+    drop_apply<DROP>(v, k0, a.inv_keep);
+    load_row(a.x, row, h, t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += t[r];
+    layernorm(v, rs1, xh1);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = fmaf(xh1[r], S.g1[F(r, h)], S.be1[F(r, h)]);   // x1
+    if (valid) store_row(SV(V_X1), row, E, 0, h, t);
+    float d[16];
+    load_row(a.dy, row, h, d);
+    load_row(a.dqkv, row, h, t);                            // dq
+    if (valid) store_row(SV(V_DQ), row, E, 0, h, t);
+    {
+      f16v acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = d[r];
+      mvt(S.Wq, t, acc, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) d[r] = acc[r];                        // dx1
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = d[r] * xh1[r];
+    if (valid) { store_row(SV(V_DLN1), row, E, 0, h, d); store_row(SV(V_DLN1X), row, E, 0, h, t); }
+    layernorm_bwd(d, xh1, S.g1, rs1, h, d);                 // dx
+    if (valid) store_row(a.dx, row, E, 0, h, d);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = ((k0 >> r) & 1u) ? d[r] * ik : 0.f;   // da1
+    if (valid) store_row(SV(V_DA1), row, E, 0, h, t);
+    f16v acc = {};
+    mvt(S.Wo1, t, acc, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = acc[r];
+    if (valid) store_row(a.dO, row, E, 0, h, v);
+  }
+}
+
+// POST backward: dy = d y, dqkv = d qkv_next [M, 96] (NEXT); writes dx = d x1,
+// dO = d c and the scratch vectors of Wo2 / W1 / W2 / LN2 / LN3
+template <bool NEXT, bool DROP>
+__global__ __launch_bounds__(NT) void enc_post_bwd_data(Tail a, float* __restrict__ scr) {
+  __shared__ Smem S;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  stage_post(S, a, NEXT);
+  __syncthreads();
+  const int64_t MS = (int64_t)a.M * E;
+  auto SV = [&](int v) { return scr + v * MS; };
+  const float ik = DROP ? a.inv_keep : 1.f;
+  const int t0 = blockIdx.x * a.chunk, t1 = min(a.M, t0 + a.chunk);
+  for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32) {
+    const int tok = tt + (lane & 31);
+    const bool valid = tok < t1;
+    const int64_t row = valid ? tok : t1 - 1;
+    const uint32_t k1 = DROP ? site_mask(a, row, 1, h) : 0xffffu;
+    const uint32_t k2 = DROP ? site_mask(a, row, 2, h) : 0xffffu;
+    float v[16], t[16], xh2[16], xh3[16], f1[16], rs2, rs3;
+    load_row(a.O, row, h, t);
+    mv(S.Wo2, S.bo2, t, v, lane);
+    drop_apply<DROP>(v, k1, a.inv_keep);
+    load_row(a.x, row, h, t);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += t[r];
+    layernorm(v, rs2, xh2);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = fmaf(xh2[r], S.g2[F(r, h)], S.be2[F(r, h)]);   // x2
+    if (valid) store_row(SV(V_X2), row, E, 0, h, t);
+    mv(S.W1, S.b1, t, f1, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = gelu(f1[r]);
+    if (valid) store_row(SV(V_GL), row, E, 0, h, v);
+    mv(S.W2, S.b2, v, v, lane);
+    drop_apply<DROP>(v, k2, a.inv_keep);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += t[r];
+    layernorm(v, rs3, xh3);
+    float d[16];
+    load_row(a.dy, row, h, d);
+    if (NEXT) {
+      f16v acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = d[r];
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        float g3[16];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          float4 q4 = *reinterpret_cast<const float4*>(a.dqkv + row * 3 * E + cc * E + 8 * g4 + 4 * h);
+          g3[4 * g4] = q4.x; g3[4 * g4 + 1] = q4.y; g3[4 * g4 + 2] = q4.z; g3[4 * g4 + 3] = q4.w;
+        }
+        mvt(S.Wn + cc * E * LP, g3, acc, lane);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) d[r] = acc[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = d[r] * xh3[r];
+    if (valid) { store_row(SV(V_DLN3), row, E, 0, h, d); store_row(SV(V_DLN3X), row, E, 0, h, t); }
+    layernorm_bwd(d, xh3, S.g3, rs3, h, d);                 // dv3 (residual into x2)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = ((k2 >> r) & 1u) ? d[r] * ik : 0.f;   // df2
+    if (valid) store_row(SV(V_DF2), row, E, 0, h, t);
+    {
+      f16v acc = {};
+      mvt(S.W2, t, acc, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t[r] = acc[r] * gelu_erf_grad(f1[r]);   // df1
+    }
+    if (valid) store_row(SV(V_DF1), row, E, 0, h, t);
+    {
+      f16v acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = d[r];
+      mvt(S.W1, t, acc, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) d[r] = acc[r];                        // dx2
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = d[r] * xh2[r];
+    if (valid) { store_row(SV(V_DLN2), row, E, 0, h, d); store_row(SV(V_DLN2X), row, E, 0, h, t); }
+    layernorm_bwd(d, xh2, S.g2, rs2, h, d);                 // dx1
+    if (valid) store_row(a.dx, row, E, 0, h, d);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = ((k1 >> r) & 1u) ? d[r] * ik : 0.f;   // da2
+    if (valid) store_row(SV(V_DA2), row, E, 0, h, t);
+    f16v acc = {};
+    mvt(S.Wo2, t, acc, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = acc[r];
+    if (valid) store_row(a.dO, row, E, 0, h, v);               // dc
+  }
+}
+
 // gradient partial layout per workgroup (floats)
 constexpr int OFF_WO1 = 0, OFF_WQ = 1024, OFF_WO2 = 2048, OFF_W1 = 3072, OFF_W2 = 4096,
               OFF_WN = 5120, OFF_BO1 = 8192, OFF_BQ = 8224, OFF_BO2 = 8256, OFF_B1 = 8288,
@@ -662,6 +937,22 @@ __global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __rest
   const int job = blockIdx.y;
   const bool next = a.Wn != nullptr;
   if (!next && job >= J_WN0 && job <= J_WN2) return;
+  if (a.mode != MODE_FULL) {
+    // encoder halves: no context gradients; the other half's matrices are zero
+    if (job == J_K || job == J_V) return;
+    const bool mine = a.mode == MODE_PRE ? (job == J_WO1 || job == J_WQ || job == J_LN)
+                                         : !(job == J_WO1 || job == J_WQ);
+    if (!mine) {
+      const int mo = job == J_WO1 ? OFF_WO1 : job == J_WQ ? OFF_WQ : job == J_WO2 ? OFF_WO2
+                   : job == J_W1 ? OFF_W1 : job == J_W2 ? OFF_W2 : OFF_WN + 1024 * (job - J_WN0);
+      const int bo = job == J_WO1 ? OFF_BO1 : job == J_WQ ? OFF_BQ : job == J_WO2 ? OFF_BO2
+                   : job == J_W1 ? OFF_B1 : job == J_W2 ? OFF_B2 : OFF_BN + 32 * (job - J_WN0);
+      float* o = a.wpart + (int64_t)blockIdx.x * WPART;
+      for (int i = threadIdx.x; i < 1024; i += NT) o[mo + i] = 0.f;
+      if (threadIdx.x < 32) o[bo + threadIdx.x] = 0.f;
+      return;
+    }
+  }
   const int chunks = (a.L + a.chunk - 1) / a.chunk;
   const int seq = blockIdx.x / chunks, ch = blockIdx.x % chunks;
   const int64_t MS = (int64_t)a.M * E;
@@ -672,7 +963,9 @@ __global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __rest
   switch (job) {
     case J_WO1: G = scr + V_DA1 * MS; X = a.O; moff = OFF_WO1; boff = OFF_BO1; break;
     case J_WQ: G = scr + V_DQ * MS; X = scr + V_X1 * MS; moff = OFF_WQ; boff = OFF_BQ; break;
-    case J_WO2: G = scr + V_DA2 * MS; X = scr + V_C * MS; moff = OFF_WO2; boff = OFF_BO2; break;
+    case J_WO2:   // POST reads c straight from its input (no V_C copy)
+      G = scr + V_DA2 * MS; X = a.mode == MODE_POST ? a.O : scr + V_C * MS;
+      moff = OFF_WO2; boff = OFF_BO2; break;
     case J_W1: G = scr + V_DF1 * MS; X = scr + V_X2 * MS; moff = OFF_W1; boff = OFF_B1; break;
     case J_W2: G = scr + V_DF2 * MS; X = scr + V_GL * MS; moff = OFF_W2; boff = OFF_B2; break;
     case J_WN0: case J_WN1: case J_WN2: {
@@ -693,7 +986,9 @@ __global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __rest
     float cs[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32)
 #pragma unroll
-      for (int i = 0; i < 6; ++i) cs[i] += cs_tile(scr + voff[i] * MS, E, base + tt, rmax, lane);
+      for (int i = 0; i < 6; ++i)   // PRE holds LN1 only, POST LN2 / LN3
+        if (a.mode == MODE_FULL || (a.mode == MODE_PRE) == (i < 2))
+          cs[i] += cs_tile(scr + voff[i] * MS, E, base + tt, rmax, lane);
 #pragma unroll
     for (int i = 0; i < 6; ++i) red[i * 256 + threadIdx.x] = cs[i];
     __syncthreads();
@@ -844,6 +1139,74 @@ VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* 
   // context grads: sum over chunks -> dkvc [Nseq * Lc * 64]
   return launch_colsum(a.cpart, chunks, (M / L) * Lc * 2 * E, dkvc, nullptr,
                        (M / L) * Lc * 2 * E, 0, s);
+}
+
+VAESNE_API int64_t vaesne_enc_block_workspace(int M) {
+  return M > 0 ? vaesne_dec_tail_workspace(M, M, 1) : 0;
+}
+
+VAESNE_API int vaesne_enc_block_fwd(int mode, const float* x, const float* O, int M,
+                                    const float* const* w, float p_drop, const int64_t* rng,
+                                    uint32_t call_id, float* y, float* q_or_qkv,
+                                    uint32_t* drop_masks, void* stream) {
+  if (M <= 0 || (mode != MODE_PRE && mode != MODE_POST)) return (int)hipErrorInvalidValue;
+  if (p_drop > 0.f && (!drop_masks || !rng)) return (int)hipErrorInvalidValue;
+  Tail a = make(x, O, nullptr, M, M, 1, w, p_drop, rng, call_id);
+  a.mode = mode;
+  a.masks = p_drop > 0.f ? drop_masks : nullptr;
+  a.y = y; a.qkv = q_or_qkv;
+  if (!q_or_qkv && (mode == MODE_PRE || a.Wn)) return (int)hipErrorInvalidValue;
+  const int grid = (M + a.chunk - 1) / a.chunk;
+  hipStream_t s = (hipStream_t)stream;
+  const bool drop = p_drop > 0.f, next = a.Wn != nullptr;
+  if (mode == MODE_PRE) {
+    if (drop) hipLaunchKernelGGL((enc_pre_fwd<true>), dim3(grid), dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((enc_pre_fwd<false>), dim3(grid), dim3(NT), 0, s, a);
+  } else if (next) {
+    if (drop) hipLaunchKernelGGL((enc_post_fwd<true, true>), dim3(grid), dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((enc_post_fwd<true, false>), dim3(grid), dim3(NT), 0, s, a);
+  } else {
+    if (drop) hipLaunchKernelGGL((enc_post_fwd<false, true>), dim3(grid), dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL((enc_post_fwd<false, false>), dim3(grid), dim3(NT), 0, s, a);
+  }
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_enc_block_bwd(int mode, const float* x, const float* O, int M,
+                                    const float* const* w, float p_drop, const int64_t* rng,
+                                    uint32_t call_id, const float* y, const float* dy,
+                                    const float* dq_or_dqkv, const uint32_t* drop_masks,
+                                    float* dx, float* dO, float* gflat, float* workspace,
+                                    void* stream) {
+  if (M <= 0 || (mode != MODE_PRE && mode != MODE_POST)) return (int)hipErrorInvalidValue;
+  if (p_drop > 0.f && !drop_masks) return (int)hipErrorInvalidValue;
+  Tail a = make(x, O, nullptr, M, M, 1, w, p_drop, rng, call_id);
+  a.mode = mode;
+  a.masks = p_drop > 0.f ? const_cast<uint32_t*>(drop_masks) : nullptr;
+  a.dy = dy; a.dqkv = dq_or_dqkv; a.dx = dx; a.dO = dO;
+  a.y = const_cast<float*>(y);
+  if (!dq_or_dqkv && (mode == MODE_PRE || a.Wn)) return (int)hipErrorInvalidValue;
+  const int grid = (M + a.chunk - 1) / a.chunk;
+  a.wpart = workspace;
+  a.cpart = workspace + (int64_t)grid * WPART;
+  float* scr = a.cpart + (int64_t)grid * 2 * E;   // vaesne_dec_tail_workspace(M, M, 1) layout
+  hipStream_t s = (hipStream_t)stream;
+  const bool drop = p_drop > 0.f, next = a.Wn != nullptr;
+  if (mode == MODE_PRE) {
+    if (drop) hipLaunchKernelGGL((enc_pre_bwd_data<true>), dim3(grid), dim3(NT), 0, s, a, scr);
+    else hipLaunchKernelGGL((enc_pre_bwd_data<false>), dim3(grid), dim3(NT), 0, s, a, scr);
+  } else if (next) {
+    if (drop) hipLaunchKernelGGL((enc_post_bwd_data<true, true>), dim3(grid), dim3(NT), 0, s, a, scr);
+    else hipLaunchKernelGGL((enc_post_bwd_data<true, false>), dim3(grid), dim3(NT), 0, s, a, scr);
+  } else {
+    if (drop) hipLaunchKernelGGL((enc_post_bwd_data<false, true>), dim3(grid), dim3(NT), 0, s, a, scr);
+    else hipLaunchKernelGGL((enc_post_bwd_data<false, false>), dim3(grid), dim3(NT), 0, s, a, scr);
+  }
+  VAESNE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(dec_tail_wgrad, dim3(grid, NJOB), dim3(NT), 0, s, a, (const float*)scr);
+  VAESNE_CHECK_LAUNCH();
+  return launch_colsum(workspace, grid, WPART, gflat, nullptr, WPART, 0, s);
 }
 
 VAESNE_API int vaesne_dec_tail_grad_layout(int* offsets) {
