@@ -543,7 +543,8 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
     }
     if (DQ) {   // dQ rows of this tile: sum over the waves (the whole key axis)
       __syncthreads();
-      float* dqb = a.dq + (int64_t)b * a.dq_bs + h * DH;
+      // key block kb's share (nkb > 1: a partial slot, summed after the launch)
+      float* dqb = a.dq + kb * a.dq_ss + (int64_t)b * a.dq_bs + h * DH;
       for (int idx = threadIdx.x; idx < qend * (DH / 4); idx += NTT) {
         const int i = idx / (DH / 4), c = (idx - i * (DH / 4)) * 4;
         float4 acc = *reinterpret_cast<const float4*>(Qw + i * DH + c);
@@ -1036,13 +1037,27 @@ int64_t fwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sp) {
   if (sp.n <= 1) return 0;
   return (int64_t)sp.n * B * Lq * H * dh + (int64_t)sp.n * B * H * Lq * 2;
 }
+// key blocks of the dK/dV launch (the fused dQ's partial count)
+int kv_blocks(int64_t bh, int Lk) {
+  const Geo g = pick_geo(bh, Lk);
+  return (Lk + 2 * g.np * g.nt - 1) / (2 * g.np * g.nt);
+}
+// floats of the dQ region: per-key-chunk partials of the dQ kernel, or (head_dim
+// 8, dQ fused into the dK/dV kernel) one partial per key block when there are
+// several; the larger of the two so either path fits
+int64_t bwd_dq_floats(int B, int H, int Lq, int Lk, int dh, const Split& sq) {
+  const int64_t unfused = (int64_t)(sq.n > 1 ? sq.n : 0) * B * Lq * H * dh;
+  const int nkb = kv_blocks((int64_t)B * H, Lk);
+  const int64_t fused = dh == 8 && nkb > 1 ? (int64_t)nkb * B * Lq * H * dh : 0;
+  return std::max(unfused, fused);
+}
 int64_t bwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sq, Split& sk) {
   sq = {1, Lk};   // dQ: key chunks
   sk = {1, Lq};   // dK/dV: query chunks
   if (Lq <= 2 * SQ) return 0;
   sq = pick_split(waves_of((int64_t)B * H, Lq), Lk);
   sk = pick_split(waves_of((int64_t)B * H, Lk), Lq);
-  return (int64_t)(sq.n > 1 ? sq.n : 0) * B * Lq * H * dh +
+  return bwd_dq_floats(B, H, Lq, Lk, dh, sq) +
          (int64_t)(sk.n > 1 ? sk.n : 0) * B * Lk * H * dh * 2;
 }
 
@@ -1123,10 +1138,12 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
   if (wsf == 0 || !ws) { sq = {1, a.Lk}; sk = {1, a.Lq}; }
   const int E = a.H * DHV;
   float* ws_dq = ws;
-  float* ws_dkv = ws ? ws + (int64_t)(sq.n > 1 ? sq.n : 0) * a.B * a.Lq * E : nullptr;
-  // fused dK/dV/dQ: head_dim 8 and the whole key axis in one workgroup
-  const Geo gk0 = pick_geo((int64_t)a.B * a.H, a.Lk);
-  const bool fuse = DHV == 8 && part == 3 && a.Lk <= 2 * gk0.np * gk0.nt && fused_dq_enabled();
+  float* ws_dkv = ws && wsf > 0 ? ws + bwd_dq_floats(a.B, a.H, a.Lq, a.Lk, DHV, sq) : nullptr;
+  // fused dK/dV/dQ (head_dim 8): one key block covers the whole key axis (dQ
+  // written directly), or several write dQ partials into the workspace
+  const int nkb = kv_blocks((int64_t)a.B * a.H, a.Lk);
+  const bool fuse = DHV == 8 && part == 3 && fused_dq_enabled() &&
+                    (nkb == 1 || (ws && wsf > 0));
   if (part & 1) {
     AttnArgs c = a;
     if (sk.n > 1) {   // chunked queries: partial dK / dV per chunk
@@ -1134,6 +1151,10 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
       c.dk = ws_dkv; c.dk_bs = (int64_t)a.Lk * E; c.dk_ls = E;
       c.dv = ws_dkv + (int64_t)sk.n * a.B * a.Lk * E; c.dv_bs = c.dk_bs; c.dv_ls = E;
       c.dk_ss = (int64_t)a.B * a.Lk * E;
+    }
+    if (fuse && nkb > 1) {   // fused dQ over several key blocks: partial per block
+      c.dq = ws_dq; c.dq_bs = (int64_t)a.Lq * E; c.dq_ls = E;
+      c.dq_ss = (int64_t)a.B * a.Lq * E;
     }
     const Geo gk = pick_geo((int64_t)a.B * a.H, a.Lk);
     VAESNE_GEO_SWITCH(gk, {
@@ -1161,6 +1182,12 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
       VAESNE_CHECK_LAUNCH();
       hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3(nb), dim3(256), 0, s, c.dv, c.dk_ss, sk.n,
                          a.B, a.Lk, E, a.dv, a.dv_bs, a.dv_ls);
+      VAESNE_CHECK_LAUNCH();
+    }
+    if (fuse && nkb > 1) {
+      const int64_t n = (int64_t)a.B * a.Lq * E;
+      hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                         c.dq, c.dq_ss, nkb, a.B, a.Lq, E, a.dq, a.dq_bs, a.dq_ls);
       VAESNE_CHECK_LAUNCH();
     }
   }
