@@ -15,7 +15,9 @@ Forward passes run on the HIP kernels (VAESNe._ops); there is no CPU path.
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import os
 
 import torch
 from torch import nn
@@ -230,6 +232,21 @@ def decoder_stack(blocks, x, context, mask=None):
     return x
 
 
+_CTX_STREAMS = {}
+
+
+def _ctx_stream(t):
+    """The stream the encoders' context self-attention paths run on
+    (VAESNE_STREAMS=0 turns the extra streams off)."""
+    if not t.is_cuda or os.environ.get("VAESNE_STREAMS", "1") == "0":
+        return None
+    dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
+    st = _CTX_STREAMS.get(dev)
+    if st is None:
+        st = _CTX_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return st
+
+
 def _fusable_encoder_block(blk):
     E = blk.layernorm1.normalized_shape[0]
     return (E == 32 and blk.self_attn.num_heads == 4 and blk.cross_attn.num_heads == 4
@@ -251,16 +268,42 @@ def encoder_stack(blocks, x, context, context_mask=None):
             x = blk(x, context, context_mask=context_mask)
         return x
     b0 = blocks[0].self_attn
+    # The context self-attention of every block reads the ORIGINAL context, so the
+    # blocks' context paths are independent of each other and of the latent chain:
+    # they run ahead on their own stream, one event per block for the join.
+    ctxs = [context] * len(blocks)
+    if any(b.context_self_attn is not None for b in blocks):
+        cs = _ctx_stream(context)
+        main = torch.cuda.current_stream() if cs is not None else None
+        if cs is not None:
+            cs.wait_stream(main)
+        evs = []
+        for i, blk in enumerate(blocks):
+            if blk.context_self_attn is None:
+                evs.append(None)
+                continue
+            p = blk.dropout.p if blk.training else 0.0
+            with torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext():
+                c, _ = blk.context_self_attn(context, context, context,
+                                             key_padding_mask=context_mask)
+                ctxs[i] = _ops.add_layernorm(context, c, blk.layernorm_context, p)
+                if cs is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(cs)
+                    evs.append(ev)
+                else:
+                    evs.append(None)
+    else:
+        evs = [None] * len(blocks)
     qkv = _ops.linear(x, b0.in_proj_weight, b0.in_proj_bias)
     for i, blk in enumerate(blocks):
         p = blk.dropout.p if blk.training else 0.0
         pa = blk.self_attn.dropout if blk.training else 0.0
         pc = blk.cross_attn.dropout if blk.training else 0.0
         O = _ops.self_attention(qkv, None, blk.self_attn.num_heads, pa)
-        ctx = context
-        if blk.context_self_attn is not None:
-            c, _ = blk.context_self_attn(context, context, context, key_padding_mask=context_mask)
-            ctx = _ops.add_layernorm(context, c, blk.layernorm_context, p)
+        ctx = ctxs[i]
+        if evs[i] is not None:
+            torch.cuda.current_stream().wait_event(evs[i])
         x1, q, kv = _ops.EncPreFn.apply(
             p, x, O, ctx, blk.self_attn.out_proj.weight, blk.self_attn.out_proj.bias,
             blk.layernorm1.weight, blk.layernorm1.bias,
