@@ -533,12 +533,19 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
             F[d] = fma2_hi_u(sy, k[p][d], F[d]);
           }
         }
+        // component order: level-32 pairs (feature 2j, 2j + 1) of one query, so
+        // each permlane swap reads two separate register pairs (no copies);
+        // lane l ends with query (l >> 4) & 1, feature 2 b2 + 4 b3 + b5
         float c[16];
 #pragma unroll
-        for (int d = 0; d < 8; ++d) { c[d] = F[d].x; c[8 + d] = F[d].y; }
+        for (int j = 0; j < 4; ++j) {
+          c[j] = F[2 * j].x; c[j + 8] = F[2 * j + 1].x;
+          c[j + 4] = F[2 * j].y; c[j + 12] = F[2 * j + 1].y;
+        }
+        const int l = threadIdx.x & 63;
         // the 4 lanes of a group hold the same total: all store it (no branch)
-        Qw[((threadIdx.x >> 6) * TK + i0 + ((threadIdx.x >> 5) & 1)) * DH +
-           ((threadIdx.x >> 2) & 7)] = wave_sum16_spread(c);
+        Qw[((threadIdx.x >> 6) * TK + i0 + ((l >> 4) & 1)) * DH +
+           (2 * ((l >> 2) & 1) + 4 * ((l >> 3) & 1) + ((l >> 5) & 1))] = wave_sum16_spread(c);
       }
     }
     if (DQ) {   // dQ rows of this tile: sum over the waves (the whole key axis)
