@@ -18,8 +18,8 @@ def main(path):
     t_end = max(int(r["End_Timestamp"]) for r in step) - t0
     n_enc_f = sum(1 for r in step if int(r["Start_Timestamp"]) - t0 < t_dec0)
     n_enc_b = sum(1 for r in step if int(r["Start_Timestamp"]) - t0 > t_dec1)
-    print(f"encoder fwd {t_dec0 / 1e3:.3f} ms ({n_enc_f} launches) | decoders {(t_dec1 - t_dec0) / 1e3:.3f} ms"
-          f" | encoder bwd + update {(t_end - t_dec1) / 1e3:.3f} ms ({n_enc_b} launches) | step {t_end / 1e3:.3f} ms")
+    print(f"encoder fwd {t_dec0 / 1e6:.3f} ms ({n_enc_f} launches) | decoders {(t_dec1 - t_dec0) / 1e6:.3f} ms"
+          f" | encoder bwd + update {(t_end - t_dec1) / 1e6:.3f} ms ({n_enc_b} launches) | step {t_end / 1e6:.3f} ms")
 
 
 if __name__ == "__main__":
