@@ -124,6 +124,11 @@ int vaesne_attn_bwd_q(const float* q, int64_t q_bs, int64_t q_ls, const float* k
                       const int64_t* rng_state, uint32_t call_id, const uint32_t* keep_bits,
                       float* workspace, void* stream);
 
+/* Test / tuning hook: force the query-tiled attention kernels' geometry (nt threads
+ * per workgroup in {64, 128, 256}, np in {1, 2}: 2*np rows per lane); nt = 0 restores
+ * the automatic choice.  Process-wide; not for use while launches are in flight. */
+int vaesne_attn_force_geometry(int nt, int np);
+
 /* ---- fused decoder-block tail --------------------------------------------------
  * Everything of a decoder TransformerBlock after its masked self-attention core
  * (util_layers.py:292-307 as called by SpectraLayers.py:61-62 and

@@ -153,6 +153,20 @@ def test_attention_dropout_statistics_and_backward_mask(B, Lq, Lk):
     assert _rel(dv, expect) < 1e-5
 
 
+@pytest.mark.parametrize("nt,np_", [(256, 2), (128, 2), (64, 2), (256, 1)])
+@pytest.mark.parametrize("B,Lq,Lk", [(2, 200, 40), (2, 300, 300)])
+def test_attention_forced_geometries_vs_dense(nt, np_, B, Lq, Lk):
+    """Every query-tiled geometry (the decoders' 982-token launches run 256 x 2,
+    which small shapes never pick by themselves), dropout on, against the dense
+    reference: forward, dQ (fused into the dK / dV kernel), dK, dV."""
+    from VAESNe._lib import lib
+    assert lib.attn_force_geometry(nt, np_) == 0
+    try:
+        test_attention_dropout_outputs_and_all_gradients_vs_dense(B, Lq, Lk)
+    finally:
+        lib.attn_force_geometry(0, 0)
+
+
 @pytest.mark.parametrize("B,Lq,Lk", [(2, 200, 40), (3, 37, 70), (2, 300, 300)])
 def test_attention_dropout_outputs_and_all_gradients_vs_dense(B, Lq, Lk):
     """With dropout on, out / dQ / dK / dV of the query-tiled kernels equal a

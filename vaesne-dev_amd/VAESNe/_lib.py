@@ -54,6 +54,7 @@ SIGNATURES = {
                                   P, P, P]),
     "vaesne_dec_tail_grad_layout": (I32, [C.POINTER(I32)]),
     "vaesne_enc_block_workspace": (I64, [I32]),
+    "vaesne_attn_force_geometry": (I32, [I32, I32]),
     "vaesne_enc_block_fwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P]),
     "vaesne_enc_block_bwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P, P, P, P, P, P]),
     "vaesne_sincos": (I32, [P, I64, I64, P, I32, P, I64, P]),

@@ -935,13 +935,15 @@ void fill_common(AttnArgs& a, int B, int H, int Lq, int Lk, int dh, float p_drop
 // row-slot efficiency; the small encoder grids (B*H = 64) fall through to NP=1
 // / 64 threads.
 struct Geo { int nt, np; };
+// forced geometry: VAESNE_ATTN_GEO="nt,np" at load, or vaesne_attn_force_geometry()
+// (tuning and tests: every geometry is reachable on small shapes); nt = 0 -> auto
+Geo g_forced = [] {
+  Geo f{0, 0};
+  if (const char* e = getenv("VAESNE_ATTN_GEO")) sscanf(e, "%d,%d", &f.nt, &f.np);
+  return f;
+}();
 Geo pick_geo(int64_t bh, int L) {
-  static const Geo forced = [] {   // tuning hook: VAESNE_ATTN_GEO="nt,np" (np in 1, 2)
-    Geo f{0, 0};
-    if (const char* e = getenv("VAESNE_ATTN_GEO")) sscanf(e, "%d,%d", &f.nt, &f.np);
-    return f;
-  }();
-  if (forced.nt > 0) return forced;
+  if (g_forced.nt > 0) return g_forced;
   // among geometries with >= 1024 workgroups, the one wasting the fewest row
   // slots (short sequences: the photometry decoder's 60 tokens x 1024 (b, h)
   // fill 60 of 1024 rows at 256x2 but 60 of 128 at 64x1); ties keep the order
@@ -1226,6 +1228,13 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
 }
 
 }  // namespace
+
+VAESNE_API int vaesne_attn_force_geometry(int nt, int np) {
+  if (nt == 0) { g_forced = {0, 0}; return 0; }
+  if ((nt != 64 && nt != 128 && nt != 256) || (np != 1 && np != 2)) return (int)hipErrorInvalidValue;
+  g_forced = {nt, np};
+  return 0;
+}
 
 VAESNE_API int vaesne_mask_bias(const uint8_t* mask, int64_t n, float* out, void* stream) {
   if (n <= 0) return 0;
