@@ -264,6 +264,19 @@ int vaesne_elbo_bwd(const float* x, int L, float llik, const float* loc, const f
                     const float* pz_scale, int K, int B, int n, const float* gout,
                     float* dloc, float* dmu, float* dsc, void* stream);
 
+/* negInfoNCE: losses.py:98-110 (ContraPhotSpec pretraining, contrastiveNets.py:20-101;
+ * driven by cannon/test_photospectra_contrast.py:124-127).  Symmetric InfoNCE over
+ * the B x B cosine logits of the two projections z1, z2 [B, D], temperature T;
+ * `loss` = -(CE(logits) + CE(logits^T)) / 2 (the value negInfoNCE returns).
+ * Saves nz [2, B, D] (normalised rows), nrm [2, B], lse [2, B], diag [B] for the
+ * backward.  Limits: 4 * (2D + B + 260) bytes <= 64 KB of LDS per workgroup. */
+int vaesne_infonce_fwd(const float* z1, const float* z2, int B, int D, float temperature,
+                       float* nz, float* nrm, float* lse, float* diag, float* loss,
+                       void* stream);
+int vaesne_infonce_bwd(const float* nz, const float* nrm, const float* lse, int B, int D,
+                       float temperature, const float* gout, float* dz1, float* dz2,
+                       void* stream);
+
 /* ---- optimizer / step plumbing ----------------------------------------------
  * torch.optim.AdamW (the scripts' optimizer, e.g. cannon/test_photospectra.py:133)
  * over one flat fp32 parameter buffer; `step` is a device float incremented by

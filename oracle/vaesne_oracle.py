@@ -434,6 +434,101 @@ def adamw_step(p: Params, grads: Dict[str, torch.Tensor], st: AdamWState):
 
 
 # ----------------------------------------------------------------------------
+# contrastive pretraining + regression heads (§8(f) row 4)
+# ----------------------------------------------------------------------------
+@dataclass
+class ContrastCfg:
+    """ContraPhotSpec(...) kwargs — contrastiveNets.py:24-46 (concat=True encoders)."""
+    latent_len: int = 4
+    latent_dim: int = 4
+    proj_dim: int = 8
+    num_bands: int = 6
+    photo_model_dim: int = 32
+    photo_num_heads: int = 4
+    photo_ff_dim: int = 32
+    photo_num_layers: int = 4
+    spec_model_dim: int = 32
+    spec_num_heads: int = 4
+    spec_num_layers: int = 4
+    spec_ff_dim: int = 32
+    selfattn: bool = False
+
+    def photo(self) -> VaeCfg:
+        return VaeCfg("photo", self.latent_len, self.latent_dim, self.photo_model_dim,
+                      self.photo_num_heads, self.photo_ff_dim, self.photo_num_layers,
+                      self.selfattn, True, 1.0, self.num_bands)
+
+    def spec(self) -> VaeCfg:
+        return VaeCfg("spec", self.latent_len, self.latent_dim, self.spec_model_dim,
+                      self.spec_num_heads, self.spec_ff_dim, self.spec_num_layers,
+                      self.selfattn, True)
+
+
+def contrast_forward(p: Params, c: ContrastCfg, x, p_drop=0.0, training=False):
+    """ContraPhotSpec.forward — contrastiveNets.py:74-85: both encoders (the spectra
+    one with the reference's (flux, wavelength) slot swap), flatten, singlelayerMLP
+    projections."""
+    pf, pt, pb, pm = x[0]
+    sf, sw, sp, sm = x[1]
+    z1 = photo_encoder(p, "photometry_encoder", c.photo(), pf, pt, pb, pm, p_drop, training)
+    z2 = spec_encoder(p, "spectra_encoder", c.spec(), sf, sw, sp, sm, p_drop, training)
+    z1 = single_layer_mlp(p, "photo_proj", z1.reshape(z1.shape[0], -1))
+    z2 = single_layer_mlp(p, "spectra_proj", z2.reshape(z2.shape[0], -1))
+    return z1, z2
+
+
+def neg_info_nce(z1, z2, temperature=0.07):
+    """negInfoNCE — losses.py:98-110, with F.normalize (x / max(||x||, 1e-12),
+    torch/nn/functional.py normalize) and cross_entropy(mean) written out."""
+    n1 = z1 / z1.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+    n2 = z2 / z2.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+    logits = n1 @ n2.T / temperature
+    diag = torch.diagonal(logits)
+    ce_r = (torch.logsumexp(logits, dim=1) - diag).mean()
+    ce_c = (torch.logsumexp(logits, dim=0) - diag).mean()
+    return -(ce_r + ce_c) / 2
+
+
+def mlp(p: Params, pre: str, x, n_hidden: int):
+    """MLP(in, out, hidden) — util_layers.py:20-34: Linear/ReLU pairs at Sequential
+    indices 0, 2, ..., final Linear at 2*n_hidden."""
+    for i in range(n_hidden):
+        x = torch.relu(_lin(p, f"{pre}.mlp.{2 * i}", x))
+    return _lin(p, f"{pre}.mlp.{2 * n_hidden}", x)
+
+
+def end2end_regression(p: Params, kind: str, c: VaeCfg, x, n_hidden: int, p_drop=0.0,
+                       training=False):
+    """photoend2endregression / specend2endregression.forward — regression.py:100-105,
+    137-141: encoder -> flatten -> MLP."""
+    enc = photo_encoder if kind == "photo" else spec_encoder
+    h = enc(p, "enc", c, *x, p_drop, training)
+    return mlp(p, "outfc", h.reshape(h.shape[0], -1), n_hidden)
+
+
+def encoder_param_shapes(c: VaeCfg, prefix: str) -> Dict[str, Tuple[int, ...]]:
+    """The bare encoder module's keys (contrastive / end-to-end nets build the
+    encoder with latent_len query tokens, not the VAE's 2*latent_len)."""
+    src = "enc.inference_transformer."
+    out = {}
+    for k, v in param_shapes(c).items():
+        if k.startswith(src):
+            kk = prefix + k[len(src):]
+            out[kk] = (c.latent_len, c.model_dim) if kk.endswith("initbottleneck") else v
+    return out
+
+
+def contrast_param_shapes(c: ContrastCfg) -> Dict[str, Tuple[int, ...]]:
+    s = encoder_param_shapes(c.photo(), "photometry_encoder.")
+    s.update(encoder_param_shapes(c.spec(), "spectra_encoder."))
+    n = c.latent_len * c.latent_dim
+    for pre in ("photo_proj", "spectra_proj"):
+        s[pre + ".fc1.weight"], s[pre + ".fc1.bias"] = (n, n), (n,)
+        s[pre + ".fc2.weight"], s[pre + ".fc2.bias"] = (c.proj_dim, n), (c.proj_dim,)
+    return s
+
+
+# ----------------------------------------------------------------------------
 # deterministic parameter construction (shared with tests/golden/gen_golden.py)
 # ----------------------------------------------------------------------------
 def _attn_keys(pre):
@@ -531,7 +626,9 @@ def make_params(cfg, fill, dtype=torch.float32, requires_grad=False) -> Params:
     """Build a param dict with ``fill(key, shape) -> np.ndarray | None``
     (None = keep the reference's constant init: _pz_params zeros/ones)."""
     out: Params = {}
-    for k, shp in param_shapes(cfg).items():
+    shapes = cfg if isinstance(cfg, dict) else (
+        contrast_param_shapes(cfg) if isinstance(cfg, ContrastCfg) else param_shapes(cfg))
+    for k, shp in shapes.items():
         v = fill(k, shp)
         if v is None:
             t = torch.zeros(shp) if k.endswith("_pz_params.0") else torch.ones(shp)

@@ -58,9 +58,9 @@ def golden_x(g, device="cpu", dtype=torch.float32):
     fl = lambda k: torch.from_numpy(g[k]).to(device=device, dtype=dtype)
     P = lambda: (fl("pflux"), fl("ptime"), f("pband"), f("pmask"))
     S = lambda: (fl("sflux"), fl("swave"), fl("sphase"), f("smask"))
-    if c["kind"] == "mmvae":
+    if c["kind"] in ("mmvae", "contrast"):
         return [P(), S()]
-    return S() if c["kind"] == "spec" else P()
+    return S() if c["kind"] in ("spec", "end2end_spec") else P()
 
 
 def has_gpu():
@@ -97,3 +97,51 @@ def build_model(c, device="cuda", dropout=0.0):
 
 def golden_us(g):
     return [torch.from_numpy(g[k]) for k in sorted(k for k in g if k.startswith("u") and k[1:].isdigit())]
+
+
+# ---------------------------------------------------------------------------
+# contrastive pretraining / regression heads (tests/golden/gen_golden_contrast.py)
+# ---------------------------------------------------------------------------
+CONTRAST_CASES = ["contrast_tiny", "contrast_selfattn"]
+END2END_CASES = ["end2end_photo", "end2end_spec"]
+
+
+def contrast_oracle_cfg(c):
+    from oracle.vaesne_oracle import ContrastCfg, VaeCfg
+    if c["kind"] == "contrast":
+        return ContrastCfg(latent_len=c["Lz"], latent_dim=c["Dz"], proj_dim=c["proj"],
+                           num_bands=c["nb"], photo_num_layers=c["layers"],
+                           spec_num_layers=c["layers"], selfattn=c["selfattn"])
+    kind = "photo" if c["kind"] == "end2end_photo" else "spec"
+    return VaeCfg(kind, latent_len=c["Lz"], latent_dim=c["Dz"], num_layers=c["layers"],
+                  selfattn=c["selfattn"], num_bands=c.get("nb", 6))
+
+
+def _filled(model):
+    new = {}
+    for k, v in model.state_dict().items():
+        f = fill_rule.fill(k, tuple(v.shape))
+        new[k] = v.clone() if f is None else torch.from_numpy(f)
+    model.load_state_dict(new)
+    return model
+
+
+def build_contrast_model(c, device="cuda", dropout=0.0):
+    """The build's ContraPhotSpec / end2end regressor for a golden config."""
+    from VAESNe.contrastiveNets import ContraPhotSpec
+    from VAESNe.regression import photoend2endregression, specend2endregression
+    if c["kind"] == "contrast":
+        m = ContraPhotSpec(latent_len=c["Lz"], latent_dim=c["Dz"], proj_dim=c["proj"],
+                           num_bands=c["nb"], photo_model_dim=32, photo_num_heads=4,
+                           photo_ff_dim=32, photo_num_layers=c["layers"], photo_dropout=dropout,
+                           spec_model_dim=32, spec_num_heads=4, spec_num_layers=c["layers"],
+                           spec_ff_dim=32, spec_dropout=dropout, selfattn=c["selfattn"])
+    elif c["kind"] == "end2end_photo":
+        m = photoend2endregression(c["out"], num_bands=c["nb"], latent_len=c["Lz"],
+                                   latent_dim=c["Dz"], num_layers=c["layers"], dropout=dropout,
+                                   selfattn=c["selfattn"], MLPlatent=c["hidden"])
+    else:
+        m = specend2endregression(c["out"], latent_len=c["Lz"], latent_dim=c["Dz"],
+                                  num_layers=c["layers"], dropout=dropout,
+                                  selfattn=c["selfattn"], MLPlatent=c["hidden"])
+    return _filled(m).to(device)

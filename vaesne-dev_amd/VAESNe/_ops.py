@@ -683,6 +683,44 @@ class ElboFn(torch.autograd.Function):
         return None, None, dloc, None, dmu, dsc, None, None
 
 
+class InfoNCEFn(torch.autograd.Function):
+    """negInfoNCE's value (losses.py:98-110) from the two projections z1, z2 [B, D]:
+    -(CE(logits) + CE(logits^T)) / 2 over logits = normalize(z1) normalize(z2)^T / T
+    (include/vaesne_hip.h: vaesne_infonce_*)."""
+
+    @staticmethod
+    def forward(ctx, z1, z2, temperature):
+        _lib.require_device(z1, z2)
+        z1, z2 = _f32(z1).contiguous(), _f32(z2).contiguous()
+        if z1.dim() != 2 or z1.shape != z2.shape:
+            raise RuntimeError(f"negInfoNCE: projections must be [B, D] of one shape, got "
+                               f"{tuple(z1.shape)} and {tuple(z2.shape)}")
+        B, D = z1.shape
+        dev = z1.device
+        nz = torch.empty((2, B, D), dtype=torch.float32, device=dev)
+        nrm = torch.empty((2, B), dtype=torch.float32, device=dev)
+        lse = torch.empty((2, B), dtype=torch.float32, device=dev)
+        diag = torch.empty((B,), dtype=torch.float32, device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        lib.infonce_fwd(z1.data_ptr(), z2.data_ptr(), B, D, float(temperature), nz.data_ptr(),
+                        nrm.data_ptr(), lse.data_ptr(), diag.data_ptr(), loss.data_ptr(),
+                        stream())
+        ctx.meta = (B, D, float(temperature))
+        ctx.save_for_backward(nz, nrm, lse)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        nz, nrm, lse = ctx.saved_tensors
+        B, D, T = ctx.meta
+        g = g.contiguous()
+        dz1 = torch.empty((B, D), dtype=torch.float32, device=nz.device)
+        dz2 = torch.empty_like(dz1)
+        lib.infonce_bwd(nz.data_ptr(), nrm.data_ptr(), lse.data_ptr(), B, D, T, g.data_ptr(),
+                        dz1.data_ptr(), dz2.data_ptr(), stream())
+        return dz1, dz2, None
+
+
 # ---------------------------------------------------------------------------
 # fused decoder-block tail (include/vaesne_hip.h: vaesne_dec_tail_*)
 # ---------------------------------------------------------------------------

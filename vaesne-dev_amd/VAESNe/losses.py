@@ -8,6 +8,7 @@ Laplace objects the models return:
     _m_iwae(model, x, K=1) -> lw       losses.py:47-62   ([2K, B])
     m_iwae(model, x, K=1)              losses.py:78-93   (sum over B)
     compute_microbatch_split           losses.py:68-76
+    negInfoNCE(model, x, temperature)  losses.py:98-110  (contrastive pretraining)
 """
 import numpy as np
 import torch
@@ -97,3 +98,14 @@ def m_iwae(model, x, K=1):
         lw.append(_m_iwae(model, split_i, K))
     lw = lw[0] if len(lw) == 1 else torch.cat(lw, 1)
     return _ops.LmeSumFn.apply(lw)
+
+
+### contrastive loss ###
+def negInfoNCE(model, x, temperature=0.07):
+    """Negative symmetric InfoNCE of the model's two projections (losses.py:98-110):
+    -(CE(z1n z2n^T / T, arange) + CE(its transpose, arange)) / 2, one fused HIP
+    kernel chain (normalise -> row/column log-sum-exp -> mean) that never
+    materialises the B x B logits in HBM.  NB it couples every sample of the
+    batch, so unlike m_iwae / elbo it does not shard across data-parallel ranks."""
+    z1, z2 = model(x)
+    return _ops.InfoNCEFn.apply(z1, z2, temperature)
