@@ -32,5 +32,25 @@ def main(path, top=30):
         print(f"{v / 1e6:8.3f} ms {c[k]:5d}x  avg {v / c[k] / 1e3:8.1f} us  {k}")
 
 
+
+
+def by_grid(path, pattern="colsum"):
+    """Launches of one kernel in one step, split by grid size (which call site)."""
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
+    step = rows[idx[-3] + 1: idx[-2] + 1]
+    c, t = collections.Counter(), collections.Counter()
+    for r in step:
+        if pattern in r["Kernel_Name"]:
+            k = (r.get("Grid_Size_X") or r.get("Grid_Size"), r.get("Workgroup_Size_X"))
+            c[k] += 1
+            t[k] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    for k, v in t.most_common():
+        print(f"{v / 1e6:8.3f} ms {c[k]:5d}x  avg {v / c[k] / 1e3:8.1f} us  grid {k[0]} wg {k[1]}")
+
+
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 30)
+    if len(sys.argv) > 2 and not sys.argv[2].isdigit():
+        by_grid(sys.argv[1], sys.argv[2])
+    else:
+        main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 30)

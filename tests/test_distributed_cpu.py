@@ -113,3 +113,59 @@ def test_shard_slices():
     assert torch.equal(torch.cat([p[1][0] for p in parts]), x[1][0])
     single = (torch.arange(5),)
     assert shard(single, 0, 1) is single
+
+
+def _contrast_worker(rank, ws, port, name, q):
+    """negInfoNCE couples the batch: shard -> forward -> distributed.global_rows
+    (all-gather of the projections) -> full-batch loss / world -> backward ->
+    SUM all-reduce must give the single-process full-batch gradient."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from conftest import contrast_oracle_cfg
+        from oracle import vaesne_oracle as O
+        from VAESNe import distributed as D
+        torch.set_num_threads(2)
+        g = load_golden(name)
+        c = g["config"]
+        cfg = contrast_oracle_cfg(c)
+        # fp64: the CE gradient cancels heavily, so fp32 summation-order noise would
+        # hide a wrong exchange; in fp64 the check is sharp
+        x = golden_x(g, dtype=torch.float64)
+        p_full = O.make_params(cfg, fill_rule.fill, dtype=torch.float64, requires_grad=True)
+        full = -O.neg_info_nce(*O.contrast_forward(p_full, cfg, x), c["T"])
+        full.backward()
+        ref = _grads(p_full)
+        p = O.make_params(cfg, fill_rule.fill, dtype=torch.float64, requires_grad=True)
+        z1, z2 = O.contrast_forward(p, cfg, D.shard(x, rank, ws))
+        z1a, z2a, scale = D.global_rows(z1, z2)
+        loss = -O.neg_info_nce(z1a, z2a, c["T"]) * scale
+        loss.backward()
+        keys = sorted(ref)
+        D.allreduce_grads([p[k] for k in keys], "sum")
+        err = max(float((p[k].grad - ref[k]).abs().max() / ref[k].abs().max().clamp_min(1e-30))
+                  for k in keys)
+        tot = loss.detach().clone()
+        dist.all_reduce(tot)              # training_step's logged value
+        q.put((rank, err, abs(tot.item() - full.item()) / abs(full.item()), z1a.shape[0]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["contrast_tiny", "contrast_selfattn"])   # B = 6 (3+3), 5 (2+3)
+def test_dp_contrastive_gradient_equals_full_batch(name):
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_contrast_worker, args=(r, ws, port, name, q)) for r in range(ws)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(300)
+        assert pr.exitcode == 0, f"rank exit code {pr.exitcode}"
+    B = load_golden(name)["config"]["B"]
+    for rank, err, lerr, nrows in sorted(q.get() for _ in range(ws)):
+        assert nrows == B
+        assert err < 1e-10, (rank, err)
+        assert lerr < 1e-12, (rank, lerr)

@@ -11,6 +11,13 @@ only exchange is ONE all-reduce of the flat fp32 gradient per step
   * elbo is a MEAN over K*B         -> each rank scales its gradient by its
     shard's share of the batch (b_r / B; 1/world for equal shards), then SUM.
 
+The one exception is the contrastive objective (losses.negInfoNCE over
+ContraPhotSpec projections): its B x B logits couple every pair of samples, so
+it has a real exchange step.  Each rank all-gathers the [b_r, proj_dim]
+projections (a few KB), evaluates the full-batch loss scaled by 1/world, and
+the gather's backward all-reduces the projection gradient and keeps its own
+rows; the SUM gradient all-reduce then reproduces the full-batch gradient.
+
 Parameters are broadcast from rank 0 once at setup.  Backend "nccl" is RCCL on
 ROCm; "gloo" is used by the CPU-side tests of the process-group logic.
 """
@@ -103,3 +110,42 @@ def allreduce_grads(params, reduction="sum", weight=None):
         n = p.grad.numel()
         p.grad.copy_(flat[o:o + n].view_as(p.grad))
         o += n
+
+
+class _GatherRows(torch.autograd.Function):
+    """all_gather along dim 0 in rank order (ragged shards allowed).  Backward:
+    every rank holds the gradient of its own copy of the full-batch loss, so the
+    full [B, ...] gradient is all-reduced (SUM) and this rank keeps its rows."""
+
+    @staticmethod
+    def forward(ctx, z, group):
+        ws = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        n = torch.tensor([z.shape[0]], dtype=torch.int64, device=z.device)
+        sizes = [torch.zeros_like(n) for _ in range(ws)]
+        dist.all_gather(sizes, n, group=group)
+        sizes = [int(t.item()) for t in sizes]
+        zp = z.new_zeros((max(sizes),) + tuple(z.shape[1:]))
+        zp[:z.shape[0]] = z
+        outs = [torch.empty_like(zp) for _ in range(ws)]
+        dist.all_gather(outs, zp, group=group)
+        ctx.lo, ctx.n, ctx.group = sum(sizes[:rank]), z.shape[0], group
+        return torch.cat([o[:k] for o, k in zip(outs, sizes)])
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous().clone()
+        dist.all_reduce(g, op=dist.ReduceOp.SUM, group=ctx.group)
+        return g[ctx.lo:ctx.lo + ctx.n], None
+
+
+def global_rows(*zs, group=None):
+    """For a batch-coupled objective: the full-batch rows of every per-sample
+    tensor in `zs` (this rank's shard gathered with the others'), plus the
+    factor 1/world the full-batch loss is scaled by on each rank, so that the
+    SUM gradient all-reduce reproduces the single-process gradient.  Identity
+    (factor 1) without a process group."""
+    ws = world()[1]
+    if ws == 1:
+        return zs + (1.0,)
+    return tuple(_GatherRows.apply(z, group) for z in zs) + (1.0 / ws,)

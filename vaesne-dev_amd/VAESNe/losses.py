@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from . import _ops
+from . import distributed as D
 
 
 def expand_first_dim(t, K):
@@ -105,7 +106,12 @@ def negInfoNCE(model, x, temperature=0.07):
     """Negative symmetric InfoNCE of the model's two projections (losses.py:98-110):
     -(CE(z1n z2n^T / T, arange) + CE(its transpose, arange)) / 2, one fused HIP
     kernel chain (normalise -> row/column log-sum-exp -> mean) that never
-    materialises the B x B logits in HBM.  NB it couples every sample of the
-    batch, so unlike m_iwae / elbo it does not shard across data-parallel ranks."""
+    materialises the B x B logits in HBM.  It couples every sample of the batch:
+    under torch.distributed each rank passes its batch shard, the projections are
+    all-gathered (distributed.global_rows) and each rank returns the full-batch
+    value / world, so training_step's SUM gradient all-reduce (its multimodal
+    default) gives the full-batch gradient and its logged loss the full value."""
     z1, z2 = model(x)
-    return _ops.InfoNCEFn.apply(z1, z2, temperature)
+    z1, z2, scale = D.global_rows(z1, z2)
+    loss = _ops.InfoNCEFn.apply(z1, z2, temperature)
+    return loss if scale == 1.0 else loss * scale
