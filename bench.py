@@ -307,6 +307,62 @@ def elbo_rel_err(device):
     return abs(loss.item() - ref) / abs(ref)
 
 
+def extras(device, use_graph, reps=10):
+    """§8(f) paths beside the headline (N=1 only; not `value`):
+    * reconstruct: photospecMMVAE.reconstruct(x, K=100) in eval mode (mmVAE.py:120-126,
+      as test/goldstein/spect_cond_LC.py drives it), B=16 pairs, forward kernels only;
+    * contrastive: one ContraPhotSpec + negInfoNCE training step (fwd, bwd, FusedAdamW)
+      at cannon/test_photospectra_contrast.py's config (B=16, T=0.1, dropout 0.1), eager."""
+    from VAESNe.contrastiveNets import ContraPhotSpec
+    from VAESNe.losses import negInfoNCE
+    from VAESNe.optim import FusedAdamW
+    out = {}
+    torch.manual_seed(2)
+    model = make_model(device, CFG["dropout"])
+    model.eval()
+    x = synthetic_batch(16, 99, device)
+    with torch.no_grad():
+        for _ in range(2):
+            model.reconstruct(x, K=100)
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            rec = model.reconstruct(x, K=100)
+        torch.cuda.synchronize(device)
+    dt = (time.perf_counter() - t0) / reps
+    ok = all(bool(torch.isfinite(rec[e][d]).all()) for e in range(2) for d in range(2))
+    out["reconstruct_K100"] = dict(value=round(16 / dt, 2), unit="SN pairs/s", ms_per_call=round(dt * 1e3, 3),
+                                   batch=16, K=100, finite=ok)
+    del model, rec
+    net = ContraPhotSpec(latent_len=4, latent_dim=4, proj_dim=8, num_bands=6, photo_model_dim=32,
+                         photo_num_heads=4, photo_ff_dim=32, photo_num_layers=4, photo_dropout=0.1,
+                         spec_model_dim=32, spec_num_heads=4, spec_num_layers=4, spec_ff_dim=32,
+                         spec_dropout=0.1, selfattn=False).to(device)
+    net.train()
+    opt = FusedAdamW(net.parameters(), lr=2.5e-4)
+    xc = synthetic_batch(16, 77, device)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = -negInfoNCE(net, xc, temperature=0.1)
+        loss.backward()
+        opt.step()
+        return loss
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        loss = step()
+    torch.cuda.synchronize(device)
+    dt = (time.perf_counter() - t0) / reps
+    out["contrastive_step"] = dict(value=round(16 / dt, 2), unit="SN pairs/s", ms_per_step=round(dt * 1e3, 3),
+                                   batch=16, finite_loss=math.isfinite(loss.item()))
+    del net, opt
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -318,6 +374,8 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--throughput-batch", type=int, default=64,
                     help="also time the same step at this per-GPU batch (N=1 only; 0 = skip)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the §8(f) side measurements (reconstruct K=100, contrastive step)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the roofline kernel launches (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
@@ -399,6 +457,12 @@ def main():
             out["roofline"] = roofline(device, args.batch)
         if world == 1 and args.throughput_batch > 0:
             out["throughput_batch"] = throughput_point(device, args.throughput_batch, not args.no_graph)
+        if world == 1 and not args.no_extras:
+            try:
+                out["extras"] = extras(device, not args.no_graph)
+            except Exception as e:   # a side measurement never hides the headline line
+                out["extras"] = None
+                log(f"[bench] extras failed: {e!r}")
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
