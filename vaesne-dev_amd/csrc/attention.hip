@@ -508,12 +508,14 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
             if (d > 0) g = fma2ru<DH>(v[p][d], dr, d, g);
           }
           const f2 pr = ex2(s - li);
-          f2 aP = pr, dP = g;
+          f2 aP = pr, dS;
           if (DROP) {
+            // dS = pr * (keep * g - Di) = aP * g - pr * Di: 3 packed ops, not 4
             aP = pr * km[p];
-            dP = g * km[p];
+            dS = fma2(aP, g, -(pr * Di));
+          } else {
+            dS = pr * (g - Di);
           }
-          const f2 dS = pr * (dP - Di);
           dSq[i - i0][p] = dS;
 #pragma unroll
           for (int d = 0; d < DH; ++d) {
