@@ -43,6 +43,10 @@ CFG = dict(workload="ZTF_photospect MMVAE training step (cfg 5)", num_bands=2, l
            beta=0.5, K=8, Lp=60, Ls=982, spectra_selfattn=True, lr=1e-3)
 
 
+STEP_GFLOP_PER_PAIR = 29.214     # SURVEY.md §8(d), cfg 5, fwd + bwd matmul FLOPs
+STEP_MSCORES_PER_PAIR = 262.4    # SURVEY.md §8(d), cfg 5, forward softmax scores
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -445,6 +449,14 @@ def main():
                    "dropout": CFG["dropout"], "spectra_selfattn": True, "parallelism": f"dp{world}",
                    "hipgraph": graph},
         "value_per_gpu": round(value / world, 2),
+        # whole-step rates from SURVEY.md §8(d)'s per-pair work at cfg 5 (FlopCounterMode on
+        # the reference: 29.214 GFLOP of matmul fwd+bwd per pair; 262.4 M softmax scores per
+        # pair in the forward), against the fp32 peak the step computes at
+        "step_utilization": {
+            "matmul_tflops": round(value * STEP_GFLOP_PER_PAIR / 1e3, 2),
+            "frac_fp32_peak": round(value * STEP_GFLOP_PER_PAIR / 1e3 / FP32_PEAK_TFLOPS, 4),
+            "softmax_gscores_per_s": round(value * STEP_MSCORES_PER_PAIR / 1e3, 1),
+            "gflop_per_pair": STEP_GFLOP_PER_PAIR, "mscores_per_pair_fwd": STEP_MSCORES_PER_PAIR},
         "final_loss": loss,
     }
     if rank == 0:

@@ -201,8 +201,9 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
     }
   }
   uint32_t rk[R];
+  uint32_t skey = 0u;
   if (DROP) {
-    const uint32_t skey = key_of(a.rng_state, a.call_id);
+    skey = key_of(a.rng_state, a.call_id);
 #pragma unroll
     for (int u = 0; u < R; ++u) rk[u] = attn_row_key(skey, (uint32_t)((int64_t)bh * a.Lq + qc[u]));
   }
@@ -275,12 +276,12 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
           l[p] += p0[p] + p1[p];
         }
         if (DROP) {
-          const uint32_t kp = (uint32_t)((kt + g0 + u) >> 1);
+          const uint32_t kpm = attn_keypair_mix(skey, (uint32_t)((kt + g0 + u) >> 1));
           const int sh = (g0 + u) & 31;
           uint32_t kk[R];
 #pragma unroll
           for (int t = 0; t < R; ++t) {
-            const uint32_t bits = attn_pair_bits(rk[t], kp);
+            const uint32_t bits = attn_pair_bits_mixed(rk[t], kpm);
             kk[t] = ((bits & 0xffffu) >= a.thr ? 1u : 0u) | ((bits >> 16) >= a.thr ? 2u : 0u);
             w[t] |= kk[t] << sh;
           }
