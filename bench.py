@@ -81,14 +81,16 @@ def synthetic_batch(B, seed, device):
 class Step:
     """fwd + bwd + pack (graph 1) | all-reduce (N>1) | AdamW update + RNG advance (graph 2)."""
 
-    def __init__(self, model, x, device, world, use_graph):
+    def __init__(self, model, x, device, world, use_graph, loss_fn=None, lr=None):
         from VAESNe import rng
         from VAESNe.distributed import GradAllReduce
         from VAESNe.losses import m_iwae
         from VAESNe.optim import FusedAdamW
         self.model, self.x, self.device, self.world = model, x, device, world
-        self.m_iwae, self.rng = m_iwae, rng
-        self.opt = FusedAdamW([p for p in model.parameters() if p.requires_grad], lr=CFG["lr"],
+        self.loss_fn = loss_fn or (lambda m, x: m_iwae(m, x, K=CFG["K"]))
+        self.rng = rng
+        self.opt = FusedAdamW([p for p in model.parameters() if p.requires_grad],
+                              lr=lr or CFG["lr"],
                               grad_hook=GradAllReduce("sum") if world > 1 else None)
         self.loss = torch.zeros((), device=device)
         self.graphs = None
@@ -97,7 +99,7 @@ class Step:
 
     def fwd_bwd(self):
         self.opt.zero_grad(set_to_none=True)
-        loss = -self.m_iwae(self.model, self.x, K=CFG["K"])
+        loss = -self.loss_fn(self.model, self.x)
         loss.backward()
         self.opt.pack_grads()
         self.loss.copy_(loss.detach())
@@ -316,10 +318,10 @@ def extras(device, use_graph, reps=10):
     * reconstruct: photospecMMVAE.reconstruct(x, K=100) in eval mode (mmVAE.py:120-126,
       as test/goldstein/spect_cond_LC.py drives it), B=16 pairs, forward kernels only;
     * contrastive: one ContraPhotSpec + negInfoNCE training step (fwd, bwd, FusedAdamW)
-      at cannon/test_photospectra_contrast.py's config (B=16, T=0.1, dropout 0.1), eager."""
+      at cannon/test_photospectra_contrast.py's config (B=16, T=0.1, dropout 0.1), captured
+      as a hipGraph like the headline step."""
     from VAESNe.contrastiveNets import ContraPhotSpec
     from VAESNe.losses import negInfoNCE
-    from VAESNe.optim import FusedAdamW
     out = {}
     torch.manual_seed(2)
     model = make_model(device, CFG["dropout"])
@@ -343,26 +345,29 @@ def extras(device, use_graph, reps=10):
                          spec_model_dim=32, spec_num_heads=4, spec_num_layers=4, spec_ff_dim=32,
                          spec_dropout=0.1, selfattn=False).to(device)
     net.train()
-    opt = FusedAdamW(net.parameters(), lr=2.5e-4)
     xc = synthetic_batch(16, 77, device)
-
-    def step():
-        opt.zero_grad(set_to_none=True)
-        loss = -negInfoNCE(net, xc, temperature=0.1)
-        loss.backward()
-        opt.step()
-        return loss
+    step = Step(net, xc, device, 1, use_graph, lr=2.5e-4,
+                loss_fn=lambda m, x: negInfoNCE(m, x, temperature=0.1))
+    graph = False
+    if use_graph:
+        try:
+            step.capture()
+            graph = True
+        except Exception as e:
+            log(f"[bench] contrastive hipGraph capture failed ({e!r}); timing eager steps")
+            step.graphs = None
+            torch.cuda.synchronize(device)
     for _ in range(3):
         step()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(reps):
-        loss = step()
+        step()
     torch.cuda.synchronize(device)
     dt = (time.perf_counter() - t0) / reps
     out["contrastive_step"] = dict(value=round(16 / dt, 2), unit="SN pairs/s", ms_per_step=round(dt * 1e3, 3),
-                                   batch=16, finite_loss=math.isfinite(loss.item()))
-    del net, opt
+                                   batch=16, hipgraph=graph, finite_loss=math.isfinite(step.loss.item()))
+    del net, step
     torch.cuda.empty_cache()
     return out
 

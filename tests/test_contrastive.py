@@ -206,3 +206,44 @@ def test_gpu_infonce_rejects_bad_shapes():
                              torch.randn(20000, 2, device="cuda"), 0.1)
     with pytest.raises(RuntimeError):        # no CPU path
         _ops.InfoNCEFn.apply(torch.randn(4, 8), torch.randn(4, 8), 0.1)
+
+
+@pytest.mark.gpu
+def test_gpu_contrastive_step_graph_capturable():
+    """The contrastive forward + backward has no host synchronisation: captured as a
+    hipGraph (as bench.py's extras step) it replays to the eager loss and gradients
+    bit for bit (dropout 0, fixed-order reductions)."""
+    from VAESNe.losses import negInfoNCE
+    g = load_golden("contrast_tiny")
+    c = g["config"]
+    model = build_contrast_model(c)
+    model.train()
+    x = golden_x(g, "cuda")
+    params = [p for p in model.parameters()]
+
+    def fwd_bwd():
+        for p in params:
+            p.grad = None
+        loss = -negInfoNCE(model, x, temperature=c["T"])
+        loss.backward()
+        return loss
+
+    ref = fwd_bwd().detach().clone()
+    ref_g = [p.grad.clone() for p in params]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            fwd_bwd()
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    for p in params:
+        p.grad = None
+    with torch.cuda.graph(graph):
+        loss = -negInfoNCE(model, x, temperature=c["T"])
+        loss.backward()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert loss.item() == ref.item()
+    for p, r in zip(params, ref_g):
+        assert torch.equal(p.grad, r)
