@@ -17,8 +17,10 @@ Rank 0 prints ONE JSON line (value = whole-job SN pairs/s).  Beside it:
   cpu_baseline : the CPU oracle (pure-PyTorch restatement of the reference,
                  oracle/vaesne_oracle.py) timed on the host cores on a bounded
                  sample (rank 0, N=1 only);
-  elbo_rel_err : |loss_build - loss_ref| / |loss_ref| on the reference's own
-                 cfg-5 golden fixture (dropout off, injected noise).
+  parity       : on the reference's own golden fixture of THIS configuration
+                 (tests/golden/mmvae_cfg5_b16.npz: B=16, K=8, dropout off, injected
+                 noise): elbo_rel_err = |loss_build - loss_ref| / |loss_ref|, and the
+                 max-rel errors of the latent mu / scale.
 """
 import argparse
 import json
@@ -184,6 +186,38 @@ def time_kernel(fn, iters, device):
     return e0.elapsed_time(e1) / iters * 1e-3
 
 
+def _usable_cores():
+    """CPUs this process may actually run on: the affinity mask, capped by a cgroup
+    CPU quota (cpu.max) when one is set (os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def _rocprof_avg_ms(kernel_prefix):
+    """Average duration of a kernel in the committed rocprofv3 --kernel-trace --stats
+    summary of the latest profile (profiles/LATEST names it), or None."""
+    import csv
+    import re
+    try:
+        d = open(os.path.join(ROOT, "profiles", "LATEST")).read().strip()
+        path = os.path.join(ROOT, "profiles", d, "kernel_stats.csv")
+        pat = re.compile(r"(^|::|\s)" + re.escape(kernel_prefix) + r"<")
+        rows = [r for r in csv.DictReader(open(path)) if pat.search(r["Name"])]
+        if rows:   # the instantiation with the most total time (the step's decoder launch)
+            best = max(rows, key=lambda r: float(r["TotalDurationNs"]))
+            return float(best["AverageNs"]) * 1e-6, f"profiles/{d}/kernel_stats.csv"
+    except (OSError, KeyError, ValueError):
+        pass
+    return None, None
+
+
 def roofline(device, B):
     """Spectra-decoder masked self-attention at its step shape (N = 2*K*B
     sequences x 982 tokens: the decoder runs once over both modalities'
@@ -191,9 +225,11 @@ def roofline(device, B):
     the dominant op of the step.  The roofline kernel is
     the fused attention backward (attn_bwd_kv_kernel<..., DQ=true>: dK, dV and
     dQ in one pass), the most expensive single kernel of the step; the forward
-    is reported beside it.  Algorithmic FLOPs per score: fwd 4*dh (QK^T, PV),
-    bwd 10*dh (S, dP, dV, dK, dQ) -- the flash backward's recomputation of S
-    counts, as the kernel must do it."""
+    is reported beside it.  Algorithmic FLOPs per score on SURVEY.md §8(d)'s
+    FlopCounterMode basis: fwd 4*dh (QK^T, PV), bwd 8*dh (= 2x forward: dP, dV,
+    dK, dQ).  The flash backward also recomputes S (2*dh more per score):
+    reported separately as flops_incl_recompute, never in `achieved`.  The kernel
+    is packed-VALU fp32 (v_pk_fma_f32), so the peak is the FP32 vector rate."""
     from VAESNe import _lib, rng
     N, L, E, H, dh = 2 * CFG["K"] * B, CFG["Ls"], CFG["model_dim"], CFG["num_heads"], 8
     pd = float(os.environ.get("VAESNE_ROOFLINE_PDROP", CFG["dropout"]))   # A/B studies only
@@ -226,10 +262,14 @@ def roofline(device, B):
     scores = N * H * L * L
     res = {}
     for name, kern, fn, fl in [("fwd", "attn_fwd_kernel", fwd, 4 * dh),
-                               ("bwd", "attn_bwd_kv_kernel", bwd(lib.attn_bwd), 10 * dh)]:
+                               ("bwd", "attn_bwd_kv_kernel", bwd(lib.attn_bwd), 8 * dh)]:
         t = time_kernel(fn, 20, device)
         res[name] = dict(kernel=kern, ms=t * 1e3, tflops=scores * fl / t / 1e12,
                          flops_per_launch=scores * fl)
+        tr, src = _rocprof_avg_ms(kern)
+        if tr is not None:
+            res[name].update(ms_rocprof=tr, tflops_rocprof=scores * fl / (tr * 1e-3) / 1e12,
+                             rocprof_source=src)
     r = res["bwd"]
     a = r["tflops"]
     traffic, tsrc = None, None
@@ -239,22 +279,34 @@ def roofline(device, B):
         tsrc = t["source"] + "; " + t["correction"]
     except (OSError, KeyError, ValueError):
         pass
-    return dict(bound="mfma", kernel=r["kernel"], achieved=round(a, 3), peak=FP32_PEAK_TFLOPS,
-                unit="TFLOP/s", frac=round(a / FP32_PEAK_TFLOPS, 4), traffic=traffic,
-                traffic_source=tsrc,
-                launch_ms=round(r["ms"], 4), flops_per_launch=r["flops_per_launch"],
-                detail={k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
-                            for kk, vv in v.items()} for k, v in res.items()},
-                note="fp32 packed-VALU kernel (v_pk_fma_f32); peak = FP32 157.3 TF (vector = "
-                     "f32-MFMA rate on gfx950); "
-                     "scores per launch = 2*K*B*H*982^2 = %d" % scores)
+    out = dict(bound="valu_fp32", kernel=r["kernel"], achieved=round(a, 3), peak=FP32_PEAK_TFLOPS,
+               unit="TFLOP/s", frac=round(a / FP32_PEAK_TFLOPS, 4), traffic=traffic,
+               traffic_source=tsrc,
+               launch_ms=round(r["ms"], 4), flops_per_launch=r["flops_per_launch"],
+               flops_incl_recompute=scores * 10 * dh,
+               detail={k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
+                           for kk, vv in v.items()} for k, v in res.items()},
+               note="fp32 packed-VALU kernel (v_pk_fma_f32); peak = FP32 157.3 TF (vector = "
+                    "f32-MFMA rate on gfx950); FLOPs per score 8*dh (FlopCounterMode: backward = "
+                    "2x forward, S recompute excluded); scores per launch = 2*K*B*H*982^2 = %d; "
+                    "launch_ms = HIP events on the kernel's stream (isolated launches), "
+                    "ms_rocprof = the committed kernel-trace average inside the step" % scores)
+    if "ms_rocprof" in r:
+        out["launch_ms_rocprof"] = round(r["ms_rocprof"], 4)
+        out["frac_rocprof"] = round(r["tflops_rocprof"] / FP32_PEAK_TFLOPS, 4)
+    return out
 
 
-def cpu_baseline(sample_B=2, steps=2):
+def cpu_baseline(sample_B=4, steps=1):
     """The oracle (CPU restatement of the reference) on the same workload:
-    cfg-5 shapes, K=8, dropout 0.1 train mode, AdamW; bounded sample."""
+    cfg-5 shapes, K=8, dropout 0.1 train mode, AdamW; bounded sample: one step of
+    4 pairs after a 1-pair warm-up step.  Every loss term is per sample (no
+    cross-sample coupling), so the step's cost is linear in B and pairs/s at B=4
+    extrapolates to the B=16 step (4x the work, 4x the time).  All cores this
+    process may use (affinity, capped by the cgroup quota the box enforces)."""
     from oracle import vaesne_oracle as O
-    torch.set_num_threads(max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))))
+    cores, affinity, quota = _usable_cores()
+    torch.set_num_threads(cores)
     c = CFG
     common = dict(latent_len=c["latent_len"], latent_dim=c["latent_dim"], model_dim=c["model_dim"],
                   num_heads=c["num_heads"], ff_dim=c["ff_dim"], num_layers=c["num_layers"])
@@ -263,12 +315,12 @@ def cpu_baseline(sample_B=2, steps=2):
     g = torch.Generator().manual_seed(0)
     p = O.make_params(cfg, lambda k, shp: (torch.randn(shp, generator=g) / math.sqrt(shp[-1])).numpy()
                       if "_pz" not in k else None, requires_grad=True)
-    x = synthetic_batch(sample_B, 99, "cpu")
     st = O.AdamWState(lr=c["lr"])
     eps = torch.finfo(torch.float32).eps
 
-    def one():
-        us = [torch.empty(c["K"], sample_B, c["latent_len"], c["latent_dim"]).uniform_(eps - 1, 1)
+    def one(nb):
+        x = synthetic_batch(nb, 99, "cpu")
+        us = [torch.empty(c["K"], nb, c["latent_len"], c["latent_dim"]).uniform_(eps - 1, 1)
               for _ in range(2)]
         for v in p.values():
             v.grad = None
@@ -276,14 +328,18 @@ def cpu_baseline(sample_B=2, steps=2):
         (-loss).backward()
         O.adamw_step(p, {k: v.grad for k, v in p.items() if v.requires_grad}, st)
 
-    one()
+    one(1)
     t0 = time.perf_counter()
     for _ in range(steps):
-        one()
+        one(sample_B)
     dt = time.perf_counter() - t0
-    return dict(value=round(sample_B * steps / dt, 4), unit="SN pairs/s", cores=torch.get_num_threads(),
-                kind="port", sample=f"{steps} oracle training steps of {sample_B} pairs (cfg-5 shapes, "
-                                    f"K=8, dropout 0.1, AdamW) after 1 warm-up step; {dt:.1f}s",
+    v = sample_B * steps / dt
+    return dict(value=round(v, 4), unit="SN pairs/s", cores=torch.get_num_threads(),
+                kind="port", sample=f"{steps} oracle training step(s) of {sample_B} pairs (cfg-5 shapes, "
+                                    f"K=8, dropout 0.1, AdamW) after a 1-pair warm-up step; {dt:.1f}s; "
+                                    f"per-pair cost is linear in B, so the B=16 step takes "
+                                    f"{16 / v:.1f}s on these cores",
+                cores_affinity=affinity, cgroup_cpu_quota=quota, os_cpu_count=os.cpu_count(),
                 cpu=_cpu_model())
 
 
@@ -297,20 +353,34 @@ def _cpu_model():
     return "unknown"
 
 
-def elbo_rel_err(device):
-    """Loss on the reference's cfg-5 golden fixture (identical params/inputs/u)."""
+def parity(device):
+    """The benchmarked configuration (B=16, K=8, cfg 5) on the reference's own golden
+    fixture: identical parameters, inputs and Laplace noise, dropout off.  Returns
+    the ELBO (m_iwae) rel-err and the max-rel errors of the latent mu / scale and
+    of the decoder locations."""
     from VAESNe import rng
     from VAESNe.losses import m_iwae
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from conftest import build_model, golden_us, golden_x, load_golden
-    g = load_golden("mmvae_cfg5")
+    g = load_golden("mmvae_cfg5_b16")
     c = g["config"]
     model = build_model(c, device=device)
     model.train()
+    x = golden_x(g, device)
+
+    def rel(a, b):
+        a = a.detach().double().cpu().numpy()
+        return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1e-30))
     with torch.no_grad(), rng.inject_uniform(golden_us(g)):
-        loss = -m_iwae(model, golden_x(g, device), K=c["K"])
+        qz, px, _ = model(x, K=c["K"])
+    with torch.no_grad(), rng.inject_uniform(golden_us(g)):
+        loss = -m_iwae(model, x, K=c["K"])
     ref = float(g["loss"])
-    return abs(loss.item() - ref) / abs(ref)
+    return dict(elbo_rel_err=abs(loss.item() - ref) / abs(ref),
+                mu_rel_err=max(rel(qz[m].loc, g[f"mu{m}"]) for m in range(2)),
+                scale_rel_err=max(rel(qz[m].scale, g[f"scale{m}"]) for m in range(2)),
+                loc_rel_err=max(rel(px[e][d].loc, g[f"loc{e}{d}"]) for e in range(2) for d in range(2)),
+                parity_fixture="tests/golden/mmvae_cfg5_b16.npz (B=16, K=8: this workload)")
 
 
 def extras(device, use_graph, reps=10):
@@ -408,7 +478,7 @@ def main():
     from VAESNe.distributed import broadcast_parameters
     _lib.load()
     torch.manual_seed(0)
-    rng.manual_seed(1234 + rank)
+    rng.manual_seed(1234)        # each rank folds its rank in (rng.rank_seed): own noise / dropout
     model = make_model(device, CFG["dropout"])
     broadcast_parameters(model)
     x = synthetic_batch(args.batch, 1234 + rank, device)
@@ -466,10 +536,10 @@ def main():
     }
     if rank == 0:
         try:
-            out["elbo_rel_err"] = elbo_rel_err(device)
+            out.update(parity(device))
         except Exception as e:
             out["elbo_rel_err"] = None
-            log(f"[bench] elbo_rel_err failed: {e!r}")
+            log(f"[bench] parity failed: {e!r}")
         if not args.no_roofline:
             out["roofline"] = roofline(device, args.batch)
         if world == 1 and args.throughput_batch > 0:

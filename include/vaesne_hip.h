@@ -205,9 +205,12 @@ int vaesne_embed_bwd(const int64_t* idx, int64_t period, int64_t rows, const flo
 int vaesne_sum_leading(const float* in, int G, int F, float* out, int accum, void* stream);
 
 /* ---- posterior, sampler, likelihood scale --------------------------------- */
-/* mu = b[:, :Lz], scale = softplus(b[:, Lz:])  PhotometricVAE.py:53-54, SpectraVAE.py:48-49 */
+/* mu = b[:, :Lz], scale = softplus(b[:, Lz:])  PhotometricVAE.py:53-54, SpectraVAE.py:48-49.
+ * nonfinite (nullable device int32[2]): set [0] = 1 when any mu / scale is NaN or Inf —
+ * the reference's posterior NaN check (PhotometricVAE.py:160-161 breakpoint()) as an
+ * asynchronous flag the host reads at its next sync (training_util.py:46 .item()). */
 int vaesne_latent_head_fwd(const float* bott, int B, int n, float* mu, float* scale,
-                           void* stream);
+                           int* nonfinite, void* stream);
 int vaesne_latent_head_bwd(const float* bott, int B, int n, const float* dmu,
                            const float* dscale, float* dbott, void* stream);
 /* u ~ U(eps-1, 1) (laplace.py:83) from the counter RNG */
@@ -223,6 +226,22 @@ int vaesne_rsample_bwd(const float* dz, const float* u, int K, int64_t n, float*
  * SpectraVAE.py:84-86 (1e10) */
 int vaesne_mask_scale(const uint8_t* mask, int64_t n, int K, float big, float* out,
                       void* stream);
+/* Bright*VAE decoders (PhotometricVAE.py:318-332, SpectraVAE.py:308-322):
+ *   brightness = brightnessfc(zs[:, :, 0, :] [| phase])     (input built here)
+ *   loc' = loc + brightness - loc.mean(axis=2)               (shift below)
+ * bright_input: R decoder rows; zs [R, zrow] (zrow = latent_len*latent_dim), token 0 =
+ * its first Dz floats; phase (nullable, spectra) read at r % period; out [R, Dz(+1)].
+ * _bwd: dzs [R, zrow] = din's token-0 part, zero elsewhere (width = Dz(+1)).
+ * bright_shift: loc, out [R, L] row-major, bright [R]; _bwd: dloc = g - rowmean(g),
+ * dbright = rowsum(g) (either output nullable). */
+int vaesne_bright_input_fwd(const float* zs, int64_t zrow, int Dz, const float* phase,
+                            int64_t period, int64_t R, float* out, void* stream);
+int vaesne_bright_input_bwd(const float* din, int width, int64_t zrow, int Dz, int64_t R,
+                            float* dzs, void* stream);
+int vaesne_bright_shift_fwd(const float* loc, const float* bright, int64_t R, int L, float* out,
+                            void* stream);
+int vaesne_bright_shift_bwd(const float* g, int64_t R, int L, float* dloc, float* dbright,
+                            void* stream);
 
 /* ---- objectives -------------------------------------------------------------
  * _m_iwae: losses.py:47-62 -> lw [2K, B]; the per-cell likelihood is
@@ -249,16 +268,18 @@ int vaesne_iwae_lw_bwd(const float* const* x, const float* llik, const int* L,
                        float* const* dmu, float* const* dsc, void* stream);
 /* m_iwae's reduction: loss = sum_b log_mean_exp_j lw[j, b]  (losses.py:92-93,
  * util_layers.py:326-327); bwd: dlw = g * softmax_j lw[:, b], g read on device. */
-int vaesne_lme_sum_fwd(const float* lw, int J, int B, float* loss, void* stream);
+int vaesne_lme_sum_fwd(const float* lw, int J, int B, float* loss, int* nonfinite,
+                      void* stream);
 int vaesne_lme_sum_bwd(const float* lw, int J, int B, const float* gout, float* dlw,
                        void* stream);
 /* elbo: losses.py:16-24 with the closed-form Laplace KL of
  * util_layers.py:330-336 -> torch/distributions/kl.py:331-338; lpx [K,B]
- * workspace, loss = mean(lpx) - mean_b sum_j KL. */
+ * workspace, loss = mean(lpx) - mean_b sum_j KL.
+ * nonfinite (nullable device int32[2], both losses): [1] = 1 when the loss is NaN / Inf. */
 int vaesne_elbo_fwd(const float* x, int L, float llik, const float* loc, const float* scale,
                     const float* mu, const float* sc, const float* pz_loc,
                     const float* pz_scale, int K, int B, int n, float* lpx, float* loss,
-                    void* stream);
+                    int* nonfinite, void* stream);
 int vaesne_elbo_bwd(const float* x, int L, float llik, const float* loc, const float* scale,
                     const float* mu, const float* sc, const float* pz_loc,
                     const float* pz_scale, int K, int B, int n, const float* gout,

@@ -44,6 +44,7 @@ class VaeCfg:
     beta: float = 1.0
     num_bands: int = 6          # photometry only
     llik_scaling: Optional[float] = None   # set by the MMVAE (mmVAE.py:82-84)
+    bright: bool = False        # BrightPhotometricVAE / BrightSpectraVAE (concat=True encoders)
 
     def llik(self) -> float:
         return (1.0 / self.beta) if self.llik_scaling is None else self.llik_scaling
@@ -311,7 +312,17 @@ def decode(p: Params, pre: str, c: VaeCfg, zs, x, p_drop=0.0, training=False) ->
     m = rep(mask)
     scale = torch.ones_like(loc)
     scale = scale + big * m
-    return Laplace(loc.reshape(K, -1, L), scale.reshape(K, -1, L))
+    loc = loc.reshape(K, -1, L)
+    if c.bright:
+        # BrightPhotometricVAE.decode (PhotometricVAE.py:321-329) / BrightSpectraVAE.decode
+        # (SpectraVAE.py:311-319): brightnessfc(first latent token [| phase]) replaces the
+        # decoded curve's mean over L.
+        inp = zs[:, :, 0, :]
+        if c.kind == "spec":
+            inp = torch.cat((inp, phase.unsqueeze(0).expand(K, -1)[:, :, None]), dim=-1)
+        brightness = mlp_one_hidden(p, pre + "brightnessfc", inp)
+        loc = loc + brightness - loc.mean(axis=2)[:, :, None]
+    return Laplace(loc, scale.reshape(K, -1, L))
 
 
 def vae_forward(p, pre, c: VaeCfg, x, K, u, p_drop=0.0, training=False):
@@ -619,6 +630,9 @@ def param_shapes(cfg, prefix: str = "") -> Dict[str, Tuple[int, ...]]:
         lin(dec + ".contextfc.mlp.2", E, E)
         lin(dec + ".get_flux.fc1", E, E)
         lin(dec + ".get_flux.fc2", E, 1)
+    if c.bright:   # MLP(latent_dim [+ 1 phase], 1, [model_dim]): PhotometricVAE.py:284, SpectraVAE.py:268
+        lin(prefix + "brightnessfc.mlp.0", Dz + (1 if c.kind == "spec" else 0), E)
+        lin(prefix + "brightnessfc.mlp.2", E, 1)
     return s
 
 

@@ -36,14 +36,18 @@ def load_golden(name):
     return d
 
 
+# every golden case of the HIP model classes (GPU parity); mmvae_cfg5_b16 is the exact
+# benchmarked configuration, too slow for the CPU oracle suite (ORACLE_CASES)
 GOLDEN_CASES = ["mmvae_tiny", "mmvae_tiny_noconcat", "mmvae_cfg4", "mmvae_cfg5",
-                "elbo_spec_cfg2", "elbo_photo_cfg3", "elbo_spec_tiny_K3"]
+                "elbo_spec_cfg2", "elbo_photo_cfg3", "elbo_spec_tiny_K3",
+                "mmvae_bright", "elbo_bright_spec", "elbo_bright_photo", "mmvae_cfg5_b16"]
+ORACLE_CASES = [c for c in GOLDEN_CASES if c != "mmvae_cfg5_b16"]
 
 
 def oracle_cfg(c):
     from oracle.vaesne_oracle import MMVAECfg, VaeCfg
     common = dict(latent_len=c["Lz"], latent_dim=c["Dz"], model_dim=32, num_heads=4, ff_dim=32,
-                  num_layers=c["layers"], concat=c["concat"])
+                  num_layers=c["layers"], concat=c["concat"], bright=c.get("bright", False))
     if c["kind"] == "mmvae":
         return MMVAECfg(photo=VaeCfg("photo", num_bands=c["nb"], selfattn=False, **common),
                         spec=VaeCfg("spec", selfattn=c["selfattn"], **common), beta=c["beta"])
@@ -58,6 +62,8 @@ def golden_x(g, device="cpu", dtype=torch.float32):
     fl = lambda k: torch.from_numpy(g[k]).to(device=device, dtype=dtype)
     P = lambda: (fl("pflux"), fl("ptime"), f("pband"), f("pmask"))
     S = lambda: (fl("sflux"), fl("swave"), fl("sphase"), f("smask"))
+    if c["kind"] == "image":
+        return (fl("image"), f("label"))
     if c["kind"] in ("mmvae", "contrast"):
         return [P(), S()]
     return S() if c["kind"] in ("spec", "end2end_spec") else P()
@@ -73,19 +79,7 @@ def has_gpu():
 def build_model(c, device="cuda", dropout=0.0):
     """The build's model for a golden config, parameters from the fill rule
     (same rule the golden generator applied to the reference)."""
-    from VAESNe.PhotometricVAE import PhotometricVAE
-    from VAESNe.SpectraVAE import SpectraVAE
-    from VAESNe.mmVAE import photospecMMVAE
-    common = dict(latent_len=c["Lz"], latent_dim=c["Dz"], model_dim=32, num_heads=4, ff_dim=32,
-                  num_layers=c["layers"], dropout=dropout, concat=c["concat"])
-    if c["kind"] == "mmvae":
-        photo = PhotometricVAE(num_bands=c["nb"], selfattn=False, **common)
-        spec = SpectraVAE(selfattn=c["selfattn"], **common)
-        model = photospecMMVAE(vaes=[photo, spec], beta=c["beta"])
-    elif c["kind"] == "spec":
-        model = SpectraVAE(selfattn=c["selfattn"], beta=c["beta"], **common)
-    else:
-        model = PhotometricVAE(num_bands=c["nb"], selfattn=c["selfattn"], beta=c["beta"], **common)
+    model = construct_model(c, dropout)
     sd = model.state_dict()
     new = {}
     for k, v in sd.items():
@@ -93,6 +87,33 @@ def build_model(c, device="cuda", dropout=0.0):
         new[k] = v.clone() if f is None else torch.from_numpy(f)
     model.load_state_dict(new)
     return model.to(device)
+
+
+def construct_model(c, dropout=0.0):
+    """The build's model for config c with its constructor's own (seeded) init —
+    the same constructor calls tests/golden/gen_golden.py:construct makes."""
+    from VAESNe.PhotometricVAE import BrightPhotometricVAE, PhotometricVAE
+    from VAESNe.SpectraVAE import BrightSpectraVAE, SpectraVAE
+    from VAESNe.mmVAE import photospecMMVAE
+    if c["kind"] == "image":
+        from VAESNe.ImageVAE import HostImgVAE
+        return HostImgVAE(img_size=c["img"], latent_len=c["Lz"], latent_dim=c["Dz"],
+                          patch_size=c["patch"], in_channels=c["C"], focal_loc=False, model_dim=32,
+                          num_heads=4, ff_dim=32, num_layers=c["layers"], dropout=dropout,
+                          selfattn=c["selfattn"], beta=c["beta"])
+    common = dict(latent_len=c["Lz"], latent_dim=c["Dz"], model_dim=32, num_heads=4, ff_dim=32,
+                  num_layers=c["layers"], dropout=dropout)
+    if c.get("bright", False):
+        P, S = BrightPhotometricVAE, BrightSpectraVAE
+    else:
+        common["concat"] = c["concat"]
+        P, S = PhotometricVAE, SpectraVAE
+    if c["kind"] == "mmvae":
+        return photospecMMVAE(vaes=[P(num_bands=c["nb"], selfattn=False, **common),
+                                    S(selfattn=c["selfattn"], **common)], beta=c["beta"])
+    if c["kind"] == "spec":
+        return S(selfattn=c["selfattn"], beta=c["beta"], **common)
+    return P(num_bands=c["nb"], selfattn=c["selfattn"], beta=c["beta"], **common)
 
 
 def golden_us(g):

@@ -8,7 +8,8 @@ Fill rule (by state_dict key, so module construction order does not matter):
   * '_pz_params.*'              -> None (keep the reference's zeros/ones)
   * LayerNorm weight            -> 1 + 0.1 N(0,1)
   * LayerNorm / Linear bias     -> 0.1 N(0,1)
-  * 2-D weights                 -> N(0,1) / sqrt(fan_in)
+  * >= 2-D weights              -> N(0,1) / sqrt(fan_in)   (fan_in = prod(shape[1:]):
+                                   Linear in_features, Conv2d in_channels * kh * kw)
   * initbottleneck              -> N(0,1)
 Inputs follow SURVEY.md §8(d).
 """
@@ -29,8 +30,8 @@ def fill(key: str, shape):
         v = 0.1 * z
     elif key.endswith("initbottleneck"):
         v = z
-    elif len(shape) == 2:
-        v = z / np.sqrt(shape[1])
+    elif len(shape) >= 2:
+        v = z / np.sqrt(np.prod(shape[1:]))
     else:
         v = z
     return v.astype(np.float32)
@@ -56,3 +57,11 @@ def spec_inputs(rng, B, L, p_mask=0.05):
     mask = rng.random((B, L)) < p_mask
     mask[:, 0] = False
     return flux, wavelength, phase, mask
+
+
+def image_inputs(rng, B, C, H):
+    """images ~ U(0, 1) [B, C, H, H] (MNIST-like intensities, cannon/mnist.py:13-16
+    ToTensor range) and the loader's label column (unused by the model)."""
+    img = rng.random((B, C, H, H)).astype(np.float32)
+    label = np.zeros((B,), dtype=np.int64)
+    return img, label

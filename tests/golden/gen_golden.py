@@ -29,8 +29,9 @@ spec = importlib.util.spec_from_file_location("fill_rule", os.path.join(HERE, "f
 fill_rule = importlib.util.module_from_spec(spec)
 spec.loader.exec_module(fill_rule)
 
-from VAESNe.PhotometricVAE import PhotometricVAE  # noqa: E402  (reference package)
-from VAESNe.SpectraVAE import SpectraVAE          # noqa: E402
+from VAESNe.PhotometricVAE import PhotometricVAE, BrightPhotometricVAE  # noqa: E402  (reference)
+from VAESNe.SpectraVAE import SpectraVAE, BrightSpectraVAE              # noqa: E402
+from VAESNe.ImageVAE import HostImgVAE                                  # noqa: E402
 from VAESNe.mmVAE import photospecMMVAE           # noqa: E402
 from VAESNe.losses import m_iwae, _m_iwae, elbo   # noqa: E402
 
@@ -52,7 +53,26 @@ CASES = {
                             selfattn=False, concat=True, steps=3),
     "elbo_spec_tiny_K3": dict(kind="spec", B=3, K=3, Ls=50, layers=2, Lz=4, Dz=3, beta=2.0,
                               selfattn=True, concat=True, steps=2),
+    # the exact benchmarked configuration (bench.py: cannon/ZTF_photospect.py per GPU)
+    "mmvae_cfg5_b16": dict(kind="mmvae", B=16, K=8, Lp=60, Ls=982, nb=2, layers=4, Lz=4, Dz=4,
+                           beta=0.5, selfattn=True, concat=True, steps=1),
+    # Bright* VAEs (PhotometricVAE.py:226-355, SpectraVAE.py:211-332)
+    "mmvae_bright": dict(kind="mmvae", bright=True, B=3, K=2, Lp=60, Ls=982, nb=2, layers=2, Lz=4,
+                         Dz=4, beta=0.5, selfattn=True, concat=True, steps=2),
+    "elbo_bright_spec": dict(kind="spec", bright=True, B=3, K=2, Ls=300, layers=2, Lz=4, Dz=3,
+                             beta=1.0, selfattn=False, concat=True, steps=2),
+    "elbo_bright_photo": dict(kind="photo", bright=True, B=4, K=1, Lp=60, nb=6, layers=2, Lz=4,
+                              Dz=2, beta=0.5, selfattn=False, concat=True, steps=2),
+    # BASELINE config 1: cannon/mnist.py HostImgVAE (host path), B=2 of its B=32
+    "image_cfg1": dict(kind="image", B=2, K=1, img=60, C=1, patch=3, layers=4, Lz=4, Dz=4,
+                       beta=0.1, selfattn=False, steps=2),
 }
+
+# Reference-initialised checkpoints: the model built right after torch.manual_seed(0)
+# exactly as a script does (no parameter fill), its state_dict saved with
+# torch.save (tensors only, loadable with weights_only=True), plus the loss of that
+# model on the case's inputs / noise.
+CKPT_CASES = ["mmvae_cfg5", "mmvae_bright", "image_cfg1"]
 
 FULL_GRAD_SUFFIXES = [
     "dec.generativetransformer.transformerblocks.0.self_attn.in_proj_weight",
@@ -63,20 +83,42 @@ FULL_GRAD_SUFFIXES = [
     "enc.inference_transformer.transformerblocks.0.cross_attn.out_proj.weight",
     "enc.inference_transformer.bandembd.weight",
     "dec.generativetransformer.bandembd.weight",
+    "brightnessfc.mlp.0.weight",
+    "brightnessfc.mlp.2.bias",
+    "enc.inference_transformer.patch_embed.proj.weight",
+    "dec.generativetransformer.final_refine.0.weight",
+    "dec.generativetransformer.final_refine.2.weight",
+    "dec.generativetransformer.decoder.weight",
 ]
 
 
-def build(c):
+def construct(c):
+    """The reference model for config c (random init; dropout 0)."""
+    if c["kind"] == "image":
+        return HostImgVAE(img_size=c["img"], latent_len=c["Lz"], latent_dim=c["Dz"],
+                          patch_size=c["patch"], in_channels=c["C"], focal_loc=False, model_dim=32,
+                          num_heads=4, ff_dim=32, num_layers=c["layers"], dropout=0.0,
+                          selfattn=c["selfattn"], beta=c["beta"])
     common = dict(latent_len=c["Lz"], latent_dim=c["Dz"], model_dim=32, num_heads=4, ff_dim=32,
-                  num_layers=c["layers"], dropout=0.0, concat=c["concat"])
-    if c["kind"] == "mmvae":
-        photo = PhotometricVAE(num_bands=c["nb"], selfattn=False, **common)
-        specv = SpectraVAE(selfattn=c["selfattn"], **common)
-        model = photospecMMVAE(vaes=[photo, specv], beta=c["beta"])
-    elif c["kind"] == "spec":
-        model = SpectraVAE(selfattn=c["selfattn"], beta=c["beta"], **common)
+                  num_layers=c["layers"], dropout=0.0)
+    bright = c.get("bright", False)
+    if bright:
+        assert c["concat"], "Bright* VAEs build their encoders with concat=True"
+        P, S = BrightPhotometricVAE, BrightSpectraVAE
     else:
-        model = PhotometricVAE(num_bands=c["nb"], selfattn=c["selfattn"], beta=c["beta"], **common)
+        common["concat"] = c["concat"]
+        P, S = PhotometricVAE, SpectraVAE
+    if c["kind"] == "mmvae":
+        photo = P(num_bands=c["nb"], selfattn=False, **common)
+        specv = S(selfattn=c["selfattn"], **common)
+        return photospecMMVAE(vaes=[photo, specv], beta=c["beta"])
+    if c["kind"] == "spec":
+        return S(selfattn=c["selfattn"], beta=c["beta"], **common)
+    return P(num_bands=c["nb"], selfattn=c["selfattn"], beta=c["beta"], **common)
+
+
+def build(c):
+    model = construct(c)
     sd = model.state_dict()
     new = {}
     for k, v in sd.items():
@@ -96,6 +138,9 @@ def inputs(c, seed=1234):
     if c["kind"] in ("mmvae", "spec"):
         f, w, ph, m = fill_rule.spec_inputs(rng, c["B"], c["Ls"])
         out.update(sflux=f, swave=w, sphase=ph, smask=m)
+    if c["kind"] == "image":
+        img, label = fill_rule.image_inputs(rng, c["B"], c["C"], c["img"])
+        out.update(image=img, label=label)
     return out
 
 
@@ -104,6 +149,8 @@ def to_x(c, arr):
                  torch.from_numpy(arr["pband"]), torch.from_numpy(arr["pmask"]))
     S = lambda: (torch.from_numpy(arr["sflux"]), torch.from_numpy(arr["swave"]),
                  torch.from_numpy(arr["sphase"]), torch.from_numpy(arr["smask"]))
+    if c["kind"] == "image":
+        return (torch.from_numpy(arr["image"]), torch.from_numpy(arr["label"]))
     if c["kind"] == "mmvae":
         return [P(), S()]
     return S() if c["kind"] == "spec" else P()
@@ -122,6 +169,26 @@ def loss_fn(c, model, x):
     if c["kind"] == "mmvae":
         return m_iwae(model, x, K=c["K"])
     return elbo(model, x, K=c["K"])
+
+
+def run_ckpt(name, c, outdir):
+    """ckpt_<name>.pt: state_dict of the reference model constructed after
+    torch.manual_seed(0) (default init); ckpt_<name>.npz: its loss on the case's
+    inputs with injected noise."""
+    torch.manual_seed(0)
+    model = construct(c)
+    model.train()
+    torch.save(model.state_dict(), os.path.join(outdir, f"ckpt_{name}.pt"))
+    x = to_x(c, inputs(c))
+    seed0 = 11
+    out = {f"u{i}": u.numpy() for i, u in enumerate(draws(c, seed0))}
+    torch.manual_seed(seed0)
+    with torch.no_grad():
+        loss = -loss_fn(c, model, x)
+    out["loss"] = np.array(loss.item(), dtype=np.float64)
+    out["config"] = np.array(json.dumps(c))
+    np.savez_compressed(os.path.join(outdir, f"ckpt_{name}.npz"), **out)
+    print(f"ckpt_{name}: loss={loss.item():.6f}")
 
 
 def run_case(name, c, outdir):
@@ -149,6 +216,10 @@ def run_case(name, c, outdir):
                     out[f"pxscale{m}{d}"] = px[m][d].scale.numpy()
             torch.manual_seed(seed0)
             out["lw"] = _m_iwae(model, x, K=c["K"]).numpy()
+        elif c["kind"] == "image":
+            q, pxz, zs = model(x, K=c["K"])
+            out["mu0"], out["scale0"], out["zs0"] = q.loc.numpy(), q.scale.numpy(), zs.numpy()
+            out["loc00"] = pxz.loc.numpy()
         else:
             q, pxz, zs = model(x, K=c["K"])
             out["mu0"], out["scale0"], out["zs0"] = q.loc.numpy(), q.scale.numpy(), zs.numpy()
@@ -198,3 +269,7 @@ if __name__ == "__main__":
         if only and name not in only:
             continue
         run_case(name, c, outdir)
+    for name in CKPT_CASES:
+        if only and ("ckpt_" + name) not in only:
+            continue
+        run_ckpt(name, CASES[name], outdir)

@@ -8,7 +8,7 @@ import re
 import pytest
 import torch
 
-from conftest import GOLDEN_CASES, ROOT, build_model, load_golden, oracle_cfg
+from conftest import ORACLE_CASES, ROOT, build_model, load_golden, oracle_cfg
 from oracle import vaesne_oracle as O
 
 HEADER = os.path.join(ROOT, "include", "vaesne_hip.h")
@@ -46,7 +46,7 @@ def test_ctypes_table_matches_header():
         assert len(args) == ar[n], (n, len(args), ar[n])
 
 
-@pytest.mark.parametrize("name", GOLDEN_CASES)
+@pytest.mark.parametrize("name", ORACLE_CASES)
 def test_state_dict_layout_matches_reference(name):
     """Key names and shapes equal the reference module tree (as recorded by
     the oracle's param_shapes, itself checked against the golden grads)."""

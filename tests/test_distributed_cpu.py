@@ -54,8 +54,7 @@ def _worker(rank, ws, port, name, q):
         # this rank's shard; u is sliced on its batch axis (dim 1) the same way
         p = O.make_params(cfg, fill_rule.fill, requires_grad=True)
         xs = D.shard(x, rank, ws)
-        b = B // ws
-        lo, hi = rank * b, (B if rank == ws - 1 else rank * b + b)
+        lo, hi = D.split_bounds(B, rank, ws)
         us_r = [u[:, lo:hi] for u in us]
         loss_of(p, xs, us_r).backward()
         reduction = "sum" if c["kind"] == "mmvae" else "mean"
@@ -108,7 +107,7 @@ def test_shard_slices():
     from VAESNe.distributed import shard
     x = [(torch.arange(10), torch.arange(10) * 2), (torch.arange(10)[:, None].repeat(1, 3),)]
     parts = [shard(x, r, 3) for r in range(3)]
-    assert [len(p[0][0]) for p in parts] == [3, 3, 4]
+    assert [len(p[0][0]) for p in parts] == [4, 3, 3]
     assert torch.equal(torch.cat([p[0][0] for p in parts]), x[0][0])
     assert torch.equal(torch.cat([p[1][0] for p in parts]), x[1][0])
     single = (torch.arange(5),)

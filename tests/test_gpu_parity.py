@@ -29,6 +29,24 @@ def _rel(a, b):
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
 
 
+def _shift_invariant(c, key):
+    """Bright* decoders: the loss is invariant to a constant shift of the decoded
+    curve, so the final head bias has an analytically zero gradient."""
+    return c.get("bright", False) and (key.endswith("get_photo.fc2.bias")
+                                       or key.endswith("get_flux.fc2.bias"))
+
+
+def _ill_conditioned(c, key):
+    """Keys whose AdamW trajectory is dominated by rounding noise: the self-attention
+    in_proj key-bias slice (zero gradient, softmax shift invariance) and, for Bright*
+    decoders, the head biases (near-zero gradients: only non-uniform shifts of the
+    curve count)."""
+    if key.endswith("in_proj_bias"):
+        return True
+    return c.get("bright", False) and any(key.endswith(s) for s in (
+        "get_photo.fc1.bias", "get_photo.fc2.bias", "get_flux.fc1.bias", "get_flux.fc2.bias"))
+
+
 def _loss(c, model, x):
     from VAESNe.losses import elbo, m_iwae
     if c["kind"] == "mmvae":
@@ -85,16 +103,23 @@ def test_loss_and_gradients_match_reference(name):
     params = dict(model.named_parameters())
     names = json.loads(str(g["grad_names"]))
     assert set(names) == {k for k, p in params.items() if p.requires_grad}
+    gmax = max(g["grad_norms"])
     for k, n in zip(names, g["grad_norms"]):
         gk = params[k].grad
         assert gk is not None, k
+        if _shift_invariant(c, k):
+            # analytically zero: the decoded curve's mean is replaced by the brightness
+            # head (PhotometricVAE.py:329), so a constant shift of loc has no gradient;
+            # both sides hold fp32 rounding noise only
+            assert gk.norm().item() <= 1e-6 * gmax and n <= 1e-6 * gmax, (k, gk.norm().item(), n)
+            continue
         assert abs(gk.norm().item() - n) <= 1e-3 * max(n, 1e-3), (k, gk.norm().item(), n)
         if ("grad:" + k) in g:
             assert _rel(gk, g["grad:" + k]) < 1e-3, k
 
 
 @pytest.mark.parametrize("name", ["mmvae_tiny", "elbo_photo_cfg3", "mmvae_tiny_noconcat",
-                                  "mmvae_cfg4"])
+                                  "mmvae_cfg4", "mmvae_bright", "elbo_bright_spec"])
 @pytest.mark.parametrize("opt", ["fused", "torch"])
 def test_adamw_trajectory_matches_reference(name, opt):
     """3 optimisation steps (lr 1e-3) reproduce the reference's losses, with the
@@ -120,8 +145,8 @@ def test_adamw_trajectory_matches_reference(name, opt):
     ref_norms = json.loads(str(g["traj_param_norms"]))
     sd = model.state_dict()
     for k, n in ref_norms.items():
-        if k.endswith("in_proj_bias"):
-            continue   # analytically-zero key-bias gradient: Adam amplifies rounding noise
+        if _ill_conditioned(c, k):
+            continue   # Adam normalises rounding noise to +-lr steps there
         assert abs(sd[k].norm().item() - n) <= 1e-4 * max(n, 1.0), k
 
 

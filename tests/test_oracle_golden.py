@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN_CASES, fill_rule, golden_x, load_golden, oracle_cfg
+from conftest import ORACLE_CASES, fill_rule, golden_x, load_golden, oracle_cfg
 from oracle import vaesne_oracle as O
 
 
@@ -25,7 +25,7 @@ def _loss(g, cfg, p, x, us):
     return -val, None, aux
 
 
-@pytest.mark.parametrize("name", GOLDEN_CASES)
+@pytest.mark.parametrize("name", ORACLE_CASES)
 def test_oracle_forward_and_grads(name):
     g = load_golden(name)
     c = g["config"]

@@ -1,0 +1,144 @@
+"""training_step under data parallelism, on CPU over gloo:
+
+* the launcher's environment alone (RANK / WORLD_SIZE / MASTER_*, as torchrun sets
+  them) is enough: training_step brings the process group up itself, as the
+  unchanged cannon scripts need;
+* sharding splits B as evenly as possible (sizes differ by <= 1), including B <
+  world (a rank with an empty slice joins the all-reduce with zero gradients);
+* mean objectives (elbo) weight each rank's gradient by its batch share, sum
+  objectives (m_iwae-style) SUM: after two epochs the parameters equal a single
+  process training on the full batches;
+* every rank draws its own device noise / dropout streams (rng.rank_seed).
+
+The model is a small deterministic host-side VAE (no sampling), so a full batch
+and its shards compose exactly; elbo runs through losses.elbo's host branch.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+from torch import nn
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class _ToyVAE(nn.Module):
+    """Deterministic stand-in with the VAE attribute contract elbo reads
+    (pz, pz_params, llik_scaling) and Laplace outputs: q(z|x) from a linear encoder,
+    zs = its location repeated K times, p(x|z) from a linear decoder."""
+
+    def __init__(self):
+        super().__init__()
+        self.enc = nn.Linear(6, 4)
+        self.dec = nn.Linear(2, 6)
+        self.pz = torch.distributions.Laplace
+        self._pz_params = nn.ParameterList([nn.Parameter(torch.zeros(1, 2), requires_grad=False),
+                                            nn.Parameter(torch.ones(1, 2), requires_grad=False)])
+        self.llik_scaling = 2.0
+
+    @property
+    def pz_params(self):
+        return self._pz_params
+
+    def forward(self, x, K=1):
+        h = self.enc(x[0])
+        mu, sc = h[:, None, :2], nn.functional.softplus(h[:, None, 2:])
+        zs = mu.unsqueeze(0).expand(K, -1, -1, -1)
+        loc = self.dec(zs[:, :, 0, :])
+        L = torch.distributions.Laplace
+        return L(mu, sc), L(loc, torch.ones_like(loc)), zs
+
+
+def _data(B, nb=2):
+    g = torch.Generator().manual_seed(5)
+    return [(torch.randn(B, 6, generator=g), torch.zeros(B)) for _ in range(nb)]
+
+
+def _train(model, batches, reduction, epochs=2):
+    from VAESNe.losses import elbo
+    from VAESNe.training_util import training_step
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+    fn = elbo if reduction == "mean" else (lambda m, x: elbo(m, x) * x[0].shape[0])
+    return [training_step(model, opt, batches, loss_fn=fn, grad_reduction=reduction)
+            for _ in range(epochs)]
+
+
+def _worker(rank, ws, port, B, reduction, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(ws), LOCAL_RANK=str(rank))
+    try:
+        torch.set_num_threads(1)
+        torch.manual_seed(0)
+        model = _ToyVAE()
+        batches = _data(B)
+        assert not dist.is_initialized()
+        losses = _train(model, batches, reduction)        # brings the group up itself
+        assert dist.is_initialized() and dist.get_world_size() == ws
+        from VAESNe import distributed as D
+        from VAESNe import rng
+        seeds = [None] * ws
+        dist.all_gather_object(seeds, rng.effective_seed())
+        sizes = [D.split_bounds(B, r, ws) for r in range(ws)]
+        q.put((rank, [p.detach().tolist() for p in model.parameters()], losses, seeds, sizes))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _single(B, reduction):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    torch.manual_seed(0)
+    model = _ToyVAE()
+    losses = _train(model, _data(B), reduction)
+    return [p.detach() for p in model.parameters()], losses
+
+
+@pytest.mark.parametrize("ws,B,reduction", [(2, 5, "mean"), (2, 5, "sum"), (3, 2, "mean"),
+                                            (3, 2, "sum")])
+def test_training_step_dp_equals_single_process(ws, B, reduction):
+    ref_params, ref_losses = _single(B, reduction)
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, ws, port, B, reduction, q)) for r in range(ws)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(300)
+        assert pr.exitcode == 0, f"rank exit code {pr.exitcode}"
+    res = sorted((q.get() for _ in range(ws)), key=lambda r: r[0])
+    for rank, params, losses, seeds, sizes in res:
+        for p, r in zip(params, ref_params):
+            p = torch.tensor(p)
+            assert torch.allclose(p, r, rtol=1e-5, atol=1e-6), (rank, (p - r).abs().max())
+        for a, b in zip(losses, ref_losses):
+            assert abs(a - b) <= 1e-5 * max(1.0, abs(b)), (rank, losses, ref_losses)
+        from VAESNe.rng import rank_seed   # every rank ran torch.manual_seed(0)
+        assert seeds == [rank_seed(0, r) for r in range(ws)] and len(set(seeds)) == ws
+        his = [hi - lo for lo, hi in sizes]
+        assert sum(his) == B and max(his) - min(his) <= 1
+        assert [lo for lo, _ in sizes] == sorted(lo for lo, _ in sizes)
+
+
+def test_rank_seed_rule():
+    from VAESNe.rng import rank_seed
+    assert rank_seed(12345, 0) == 12345
+    s = {rank_seed(0, r) for r in range(8)}
+    assert len(s) == 8 and all(0 <= v < (1 << 63) for v in s)
+
+
+def test_split_bounds_even():
+    from VAESNe.distributed import shard, split_bounds
+    assert [split_bounds(10, r, 3) for r in range(3)] == [(0, 4), (4, 7), (7, 10)]
+    assert [split_bounds(2, r, 3) for r in range(3)] == [(0, 1), (1, 2), (2, 2)]
+    x = [(torch.arange(10),), (torch.arange(10) * 2,)]
+    parts = [shard(x, r, 3) for r in range(3)]
+    assert torch.equal(torch.cat([p[1][0] for p in parts]), x[1][0])

@@ -1,4 +1,4 @@
-"""Photometry VAE, MI355X build (reference: PhotometricVAE.py:10-222).
+"""Photometry VAE, MI355X build (reference: PhotometricVAE.py:10-355).
 
 Encoder -> (mu, softplus scale) -> Laplace.rsample([K]) -> decoder, each step
 a HIP kernel.  Constructors accept and ignore `photometric_length` (the
@@ -11,6 +11,7 @@ from torch import nn
 from . import _ops
 from .PhotometricLayers import photometricTransformerDecoder, photometricTransformerEncoder
 from .base_vae import VAE, check_laplace
+from .util_layers import MLP
 
 
 class PhotometricEnc(nn.Module):
@@ -130,3 +131,32 @@ class PhotometricVAE(VAE):
             zs = _ops.laplace_rsample(loc.expand(time.shape[0], *loc.shape).contiguous(),
                                       scale.expand(time.shape[0], *scale.shape).contiguous(), N)
             return self.decode(zs, (None, time, band, mask)).mean
+
+
+class BrightPhotometricVAE(PhotometricVAE):
+    """PhotometricVAE.py:226-355: the first latent token carries the light curve's
+    overall brightness.  decode() adds brightnessfc(zs[:, :, 0, :]) to the decoded
+    curve after removing its mean over time (:321-329):
+
+        loc' = loc + MLP(z_0) - loc.mean(axis=2)
+
+    brightnessfc = MLP(latent_dim, 1, [model_dim]) (:284) on the HIP linear kernels;
+    the gather of token 0 and the mean-removal shift are two small HIP kernels
+    (vaesne_bright_input_*, vaesne_bright_shift_*).  Constructor signature of the
+    reference (no `concat`: the encoder uses its default, concat=True)."""
+
+    def __init__(self, num_bands=6, latent_len=8, latent_dim=4, model_dim=64, num_heads=4,
+                 ff_dim=64, num_layers=4, dropout=0.1, selfattn=False, beta=1.,
+                 prior=dist.Laplace, likelihood=dist.Laplace, posterior=dist.Laplace,
+                 photometric_length=None):
+        assert latent_len > 1, "first token for overall brightness"
+        super().__init__(num_bands=num_bands, latent_len=latent_len, latent_dim=latent_dim,
+                         model_dim=model_dim, num_heads=num_heads, ff_dim=ff_dim,
+                         num_layers=num_layers, dropout=dropout, selfattn=selfattn, concat=True,
+                         beta=beta, prior=prior, likelihood=likelihood, posterior=posterior)
+        self.brightnessfc = MLP(latent_dim, 1, [model_dim])
+
+    def decode_params(self, zs, x, groups=1):
+        loc, scale = super().decode_params(zs, x, groups)
+        brightness = self.brightnessfc(_ops.bright_input(zs))     # [K, groups*B, 1]
+        return _ops.bright_shift(loc, brightness), scale

@@ -1,4 +1,4 @@
-"""Spectra VAE, MI355X build (reference: SpectraVAE.py:11-206).
+"""Spectra VAE, MI355X build (reference: SpectraVAE.py:11-332).
 
 Constructors accept and ignore `spectra_length` (the cannon scripts pass it,
 SURVEY.md F9).
@@ -10,6 +10,7 @@ from torch import nn
 from . import _ops
 from .SpectraLayers import spectraTransformerDecoder, spectraTransformerEncoder
 from .base_vae import VAE, check_laplace
+from .util_layers import MLP
 
 
 class SpectraEnc(nn.Module):
@@ -127,3 +128,29 @@ class SpectraVAE(VAE):
             loc, scale = self.pz_params[0], self.pz_params[1]
             zs = _ops.laplace_rsample(loc.unsqueeze(0).contiguous(), scale.unsqueeze(0).contiguous(), N)
             return self.decode(zs, x).mean.unsqueeze(0)
+
+
+class BrightSpectraVAE(SpectraVAE):
+    """SpectraVAE.py:211-332: the first latent token (with the phase) carries the
+    spectrum's overall brightness.  decode() (:308-322):
+
+        loc' = loc + MLP([z_0 | phase]) - loc.mean(axis=2)
+
+    brightnessfc = MLP(latent_dim + 1, 1, [model_dim]) (:268).  Constructor signature
+    of the reference (no `concat`: the encoder uses its default, concat=True)."""
+
+    def __init__(self, latent_len=4, latent_dim=2, model_dim=32, num_heads=4, ff_dim=32,
+                 num_layers=4, dropout=0.1, selfattn=False, beta=1., prior=dist.Laplace,
+                 likelihood=dist.Laplace, posterior=dist.Laplace, spectra_length=None):
+        assert latent_len > 1, "Need at least one token for overall brightness"
+        super().__init__(latent_len=latent_len, latent_dim=latent_dim, model_dim=model_dim,
+                         num_heads=num_heads, ff_dim=ff_dim, num_layers=num_layers,
+                         dropout=dropout, selfattn=selfattn, concat=True, beta=beta, prior=prior,
+                         likelihood=likelihood, posterior=posterior)
+        self.brightnessfc = MLP(latent_dim + 1, 1, [model_dim])
+
+    def decode_params(self, zs, x, groups=1):
+        loc, scale = super().decode_params(zs, x, groups)
+        phase = x[2]
+        brightness = self.brightnessfc(_ops.bright_input(zs, phase))   # [K, groups*B, 1]
+        return _ops.bright_shift(loc, brightness), scale

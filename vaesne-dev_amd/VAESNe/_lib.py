@@ -62,19 +62,23 @@ SIGNATURES = {
     "vaesne_embed_bwd_workspace": (I64, [I64, I32, I32]),
     "vaesne_embed_bwd": (I32, [P, I64, I64, P, I64, I32, I32, P, I32, P, P]),
     "vaesne_sum_leading": (I32, [P, I32, I32, P, I32, P]),
-    "vaesne_latent_head_fwd": (I32, [P, I32, I32, P, P, P]),
+    "vaesne_latent_head_fwd": (I32, [P, I32, I32, P, P, P, P]),
     "vaesne_latent_head_bwd": (I32, [P, I32, I32, P, P, P, P]),
     "vaesne_uniform": (I32, [P, I64, P, U32, P]),
     "vaesne_rsample_fwd": (I32, [P, P, P, I32, I64, P, P]),
     "vaesne_rsample_bwd": (I32, [P, P, I32, I64, P, P, P]),
     "vaesne_mask_scale": (I32, [P, I64, I32, F32, P, P]),
+    "vaesne_bright_input_fwd": (I32, [P, I64, I32, P, I64, I64, P, P]),
+    "vaesne_bright_input_bwd": (I32, [P, I32, I64, I32, I64, P, P]),
+    "vaesne_bright_shift_fwd": (I32, [P, P, I64, I32, P, P]),
+    "vaesne_bright_shift_bwd": (I32, [P, I64, I32, P, P, P]),
     "vaesne_iwae_lw_fwd": (I32, [PP, C.POINTER(F32), C.POINTER(I32), PP, PP, C.POINTER(I64), PP,
                                  PP, PP, P, P, I32, I32, I32, P, P]),
     "vaesne_iwae_lw_bwd": (I32, [PP, C.POINTER(F32), C.POINTER(I32), PP, PP, C.POINTER(I64), PP,
                                  PP, PP, P, P, I32, I32, I32, P, PP, PP, PP, PP, P]),
-    "vaesne_lme_sum_fwd": (I32, [P, I32, I32, P, P]),
+    "vaesne_lme_sum_fwd": (I32, [P, I32, I32, P, P, P]),
     "vaesne_lme_sum_bwd": (I32, [P, I32, I32, P, P, P]),
-    "vaesne_elbo_fwd": (I32, [P, I32, F32, P, P, P, P, P, P, I32, I32, I32, P, P, P]),
+    "vaesne_elbo_fwd": (I32, [P, I32, F32, P, P, P, P, P, P, I32, I32, I32, P, P, P, P]),
     "vaesne_elbo_bwd": (I32, [P, I32, F32, P, P, P, P, P, P, I32, I32, I32, P, P, P, P, P]),
     "vaesne_infonce_fwd": (I32, [P, P, I32, I32, F32, P, P, P, P, P, P]),
     "vaesne_infonce_bwd": (I32, [P, P, P, I32, I32, F32, P, P, P, P]),

@@ -11,7 +11,7 @@ import math
 
 import torch
 
-from . import _lib, rng
+from . import _lib, guard, rng
 from ._lib import lib, ptr, stream
 
 ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
@@ -266,6 +266,22 @@ def _bias_of(mask, kbias):
 _KBIAS_CACHE = []
 
 
+def key_bias_of(mask):
+    """The (cached) additive key bias of a key_padding_mask, or None."""
+    return None if mask is None else _bias_of(mask, None)
+
+
+def used_on(stream, *ts):
+    """Mark device tensors produced on one HIP stream as used on `stream`
+    (Tensor.record_stream): the caching allocator then keeps their memory from
+    being reused before `stream`'s pending work on them has finished."""
+    if stream is None:
+        return
+    for t in ts:
+        if t is not None and t.is_cuda:
+            t.record_stream(stream)
+
+
 def _attn_ws(B, H, Lq, Lk, dh, bwd, dev):
     """Workspace of a chunked (split) attention launch, or None (not needed)."""
     n = lib.attn_workspace(B, H, Lq, Lk, dh, bwd)
@@ -458,7 +474,8 @@ class LatentHeadFn(torch.autograd.Function):
             raise RuntimeError("bottleneck length must be 2*latent_len")
         mu = torch.empty((B, Lz, Dz), dtype=torch.float32, device=bott.device)
         sc = torch.empty_like(mu)
-        lib.latent_head_fwd(bott.data_ptr(), B, Lz * Dz, mu.data_ptr(), sc.data_ptr(), stream())
+        lib.latent_head_fwd(bott.data_ptr(), B, Lz * Dz, mu.data_ptr(), sc.data_ptr(),
+                            guard.ptr(bott), stream())
         ctx.save_for_backward(bott)
         ctx.n = Lz * Dz
         return mu, sc
@@ -516,6 +533,74 @@ def mask_scale(mask, K, big, shape_like):
     out = torch.empty((K * m.shape[0], m.shape[1]), dtype=torch.float32, device=m.device)
     lib.mask_scale(m.data_ptr(), m.numel(), K, float(big), out.data_ptr(), stream())
     return out
+
+
+# ---------------------------------------------------------------------------
+# Bright*VAE brightness head (PhotometricVAE.py:318-332, SpectraVAE.py:308-322)
+# ---------------------------------------------------------------------------
+class BrightInputFn(torch.autograd.Function):
+    """zs [K, N, Lz, Dz] (+ phase [P], row n of every k reads phase[n % P]) ->
+    [K, N, Dz(+1)] = cat(zs[:, :, 0, :], phase) — the brightnessfc input."""
+
+    @staticmethod
+    def forward(ctx, zs, phase):
+        _lib.require_device(zs, phase)
+        zs = _f32(zs).contiguous()
+        K, N, Lz, Dz = zs.shape
+        R = K * N
+        W = Dz + (1 if phase is not None else 0)
+        ph = None if phase is None else _f32(phase).contiguous()
+        period = 1 if ph is None else ph.numel()
+        out = torch.empty((K, N, W), dtype=torch.float32, device=zs.device)
+        lib.bright_input_fwd(zs.data_ptr(), Lz * Dz, Dz, ptr(ph), period, R, out.data_ptr(),
+                             stream())
+        ctx.meta = (zs.shape, W)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        shape, W = ctx.meta
+        K, N, Lz, Dz = shape
+        dzs = torch.empty(shape, dtype=torch.float32, device=dout.device)
+        lib.bright_input_bwd(dout.contiguous().data_ptr(), W, Lz * Dz, Dz, K * N, dzs.data_ptr(),
+                             stream())
+        return dzs, None
+
+
+def bright_input(zs, phase=None):
+    return BrightInputFn.apply(zs, phase)
+
+
+class BrightShiftFn(torch.autograd.Function):
+    """loc [K, N, L], bright [K, N(, 1)] -> (loc + bright) - loc.mean(-1)."""
+
+    @staticmethod
+    def forward(ctx, loc, bright):
+        _lib.require_device(loc, bright)
+        loc = _f32(loc).contiguous()
+        bright = _f32(bright).contiguous()
+        L = loc.shape[-1]
+        R = loc.numel() // L
+        if bright.numel() != R:
+            raise RuntimeError(f"bright_shift: brightness has {bright.numel()} rows, loc {R}")
+        out = torch.empty_like(loc)
+        lib.bright_shift_fwd(loc.data_ptr(), bright.data_ptr(), R, L, out.data_ptr(), stream())
+        ctx.meta = (R, L, bright.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        R, L, bshape = ctx.meta
+        g = g.contiguous()
+        dloc = torch.empty_like(g) if ctx.needs_input_grad[0] else None
+        db = torch.empty(bshape, dtype=torch.float32, device=g.device) \
+            if ctx.needs_input_grad[1] else None
+        lib.bright_shift_bwd(g.data_ptr(), R, L, ptr(dloc), ptr(db), stream())
+        return dloc, db
+
+
+def bright_shift(loc, bright):
+    return BrightShiftFn.apply(loc, bright)
 
 
 # ---------------------------------------------------------------------------
@@ -638,7 +723,7 @@ class LmeSumFn(torch.autograd.Function):
         lw = lw.contiguous()
         J, B = lw.shape
         loss = torch.empty((), dtype=torch.float32, device=lw.device)
-        lib.lme_sum_fwd(lw.data_ptr(), J, B, loss.data_ptr(), stream())
+        lib.lme_sum_fwd(lw.data_ptr(), J, B, loss.data_ptr(), guard.ptr(lw), stream())
         ctx.save_for_backward(lw)
         return loss
 
@@ -664,7 +749,7 @@ class ElboFn(torch.autograd.Function):
         loss = torch.empty((), dtype=torch.float32, device=x.device)
         lib.elbo_fwd(x.data_ptr(), L, float(llik), loc.data_ptr(), scale.data_ptr(),
                      mu.data_ptr(), sc.data_ptr(), pzl.data_ptr(), pzs.data_ptr(), K, B, n,
-                     lpx.data_ptr(), loss.data_ptr(), stream())
+                     lpx.data_ptr(), loss.data_ptr(), guard.ptr(x), stream())
         ctx.meta = (K, B, L, n, float(llik))
         ctx.save_for_backward(x, loc, scale, mu, sc, pzl, pzs)
         return loss

@@ -23,6 +23,8 @@ ROCm; "gloo" is used by the CPU-side tests of the process-group logic.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -33,19 +35,53 @@ def world():
     return 0, 1
 
 
+def env_world():
+    """(rank, world) from a launcher's environment (torchrun: RANK / WORLD_SIZE),
+    whether or not the process group exists yet."""
+    if dist.is_available() and dist.is_initialized():
+        return world()
+    ws = int(os.environ.get("WORLD_SIZE", "1") or 1)
+    return (int(os.environ.get("RANK", "0") or 0), ws) if ws > 1 else (0, 1)
+
+
+def init_from_env():
+    """Bring up the process group the launcher describes, if it is not up yet:
+    the cannon scripts never call init_process_group (training_util.py:17-53 has
+    no distributed code), so `torchrun --nproc-per-node N script.py` with the
+    script unchanged reaches here from training_step.  Backend "nccl" (RCCL over
+    xGMI) when the ranks drive GPUs, "gloo" otherwise.  Returns (rank, world)."""
+    if not dist.is_available() or dist.is_initialized():
+        return world()
+    rank, ws = env_world()
+    if ws <= 1:
+        return 0, 1
+    backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0") or 0))
+    dist.init_process_group(backend)
+    return world()
+
+
+def split_bounds(B, rank=None, world_size=None):
+    """[lo, hi) of rank's contiguous batch slice: sizes differ by at most one
+    (torch.tensor_split's rule: the first B % world ranks take one extra row)."""
+    if rank is None:
+        rank, world_size = world()
+    b, r = divmod(int(B), int(world_size))
+    lo = rank * b + min(rank, r)
+    return lo, lo + b + (1 if rank < r else 0)
+
+
 def shard(batch, rank=None, world_size=None):
-    """Contiguous slice [rank*b, (rank+1)*b) of every tensor of a (possibly
-    multimodal) batch; b = B // world (the remainder goes to the last rank)."""
+    """This rank's contiguous slice (split_bounds) of every tensor of a (possibly
+    multimodal) batch.  A rank can get an empty slice when B < world."""
     if rank is None:
         rank, world_size = world()
     if world_size == 1:
         return batch
 
     def cut(t):
-        B = t.shape[0]
-        b = B // world_size
-        lo = rank * b
-        hi = B if rank == world_size - 1 else lo + b
+        lo, hi = split_bounds(t.shape[0], rank, world_size)
         return t[lo:hi]
 
     if isinstance(batch, list):
@@ -54,12 +90,18 @@ def shard(batch, rank=None, world_size=None):
 
 
 def shard_fraction(B, rank=None, world_size=None):
-    """b_r / B for the contiguous split `shard` makes (the weight of this
-    rank's mean-objective gradient in the global mean)."""
-    if rank is None:
-        rank, world_size = world()
-    b = B // world_size
-    return ((B - rank * b) if rank == world_size - 1 else b) / B
+    """b_r / B for the split `shard` makes (the weight of this rank's
+    mean-objective gradient in the global mean)."""
+    lo, hi = split_bounds(B, rank, world_size)
+    return (hi - lo) / B
+
+
+def sync_parameters_once(module, src=0):
+    """broadcast_parameters the first time a module is trained data-parallel
+    (ranks seeded alike already agree; this makes it a guarantee)."""
+    if world()[1] > 1 and not getattr(module, "_vaesne_dp_synced", False):
+        broadcast_parameters(module, src)
+        module._vaesne_dp_synced = True
 
 
 def broadcast_parameters(module, src=0):

@@ -30,11 +30,29 @@ def _pz(model):
 def elbo(model, x, K=1, debug=False):
     """E_{p(x)}[ELBO]: mean_{k,b}(llik * sum_L log p(x|z)) - mean_b sum KL(q(z|x) || p(z))."""
     qz_x, px_z, _ = model(x, K)
+    if px_z.loc.device.type == "cpu":
+        return _elbo_host(model, x, K, qz_x, px_z, debug)
     pz_loc, pz_scale = _pz(model)
     loss = _ops.ElboFn.apply(x[0], float(model.llik_scaling), px_z.loc, px_z.scale, qz_x.loc,
                              qz_x.scale, pz_loc, pz_scale)
     if debug:
         print(f"elbo: {loss.item()}")
+    return loss
+
+
+def _elbo_host(model, x, K, qz_x, px_z, debug=False):
+    """elbo on host tensors — only the host-path image VAE (ImageVAE.HostImgVAE, BASELINE
+    config 1) produces those; every HIP model refuses host
+    tensors before reaching here.  losses.py:16-24 with torch's Laplace log_prob and
+    closed-form KL (torch/distributions/kl.py:331-338)."""
+    data = expand_first_dim(x[0], K)
+    lpx = px_z.log_prob(data).reshape(*px_z.batch_shape[:2], -1) * model.llik_scaling
+    kld = torch.distributions.kl_divergence(qz_x, model.pz(*model.pz_params))
+    if debug:
+        print(f"kl: {kld.sum((-1, -2)).mean()}, llk: {-lpx.sum(-1).mean()}")
+    loss = (lpx.sum(-1) - kld.sum((-1, -2))[None, :]).mean()
+    if not torch.isfinite(loss):
+        raise RuntimeError("elbo: non-finite loss")
     return loss
 
 

@@ -45,6 +45,16 @@ class _Branches:
             return contextlib.nullcontext()
         return torch.cuda.stream(self.side)
 
+    def to_side(self, *ts):
+        """tensors made on the main stream that the side branch reads"""
+        if self.side is not None:
+            _ops.used_on(self.side, *ts)
+
+    def to_main(self, *ts):
+        """tensors the side branch made that the main stream reads"""
+        if self.side is not None:
+            _ops.used_on(self.main, *ts)
+
     def __exit__(self, *exc):
         if self.side is not None:
             self.main.wait_stream(self.side)
@@ -94,18 +104,22 @@ class photospecMMVAE(nn.Module):
         side = _side_stream(x[0][0]) if n == 2 else None
         qz_xs, zss = [None] * n, [None] * n
         with _Branches(side) as br:
+            br.to_side(*x[0])
             for m, vae in enumerate(self.vaes):
                 with br.on(m):
                     qz_xs[m], zss[m] = vae.posterior(x[m], K=K)
+            br.to_main(qz_xs[0].loc, qz_xs[0].scale, zss[0])
         px_zs = _CellMatrix([[None for _ in range(n)] for _ in range(n)])
         if all(z.shape == zss[0].shape for z in zss):
             B = zss[0].shape[1]
             zcat = torch.cat(zss, dim=1)
             px_zs.merged = [None] * n
             with _Branches(side) as br:
+                br.to_side(zcat)
                 for d, vae in enumerate(self.vaes):
                     with br.on(d):
                         px_zs.merged[d] = vae.decode_params(zcat, x[d], groups=n)
+                br.to_main(*px_zs.merged[0])
             for d, vae in enumerate(self.vaes):
                 loc, scale = px_zs.merged[d]
                 for e in range(n):

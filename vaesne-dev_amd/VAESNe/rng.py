@@ -32,14 +32,40 @@ _queue: list = []
 _mode = "device"
 
 
+_MASK63 = (1 << 63) - 1
+
+
+def rank_seed(seed: int, rank: int) -> int:
+    """The device seed of data-parallel rank `rank` for a user seed: rank 0 keeps
+    it, other ranks fold their rank in (a 64-bit Weyl step), so ranks that all
+    called torch.manual_seed(0) — as every cannon script does, e.g.
+    ZTF_photospect.py:19 — still draw their own Laplace noise and dropout masks
+    (SURVEY.md §8(e)), while a single process is unchanged."""
+    return (int(seed) ^ ((int(rank) * 0x9E3779B97F4A7C15) & _MASK63)) & _MASK63
+
+
+def _rank() -> int:
+    from . import distributed as D
+    return D.env_world()[0]
+
+
 def _default_seed() -> int:
-    return int(torch.initial_seed()) & ((1 << 63) - 1)
+    return rank_seed(int(torch.initial_seed()) & _MASK63, _rank())
+
+
+def effective_seed() -> int:
+    """The seed the device streams use (created on first use)."""
+    global _seed
+    if _seed is None:
+        _seed = _default_seed()
+    return _seed
 
 
 def manual_seed(seed: int):
-    """Reset the device RNG of every device to `seed`, counter 0."""
+    """Reset the device RNG of every device to `seed` (folded with the
+    data-parallel rank, see rank_seed), counter 0."""
     global _seed, _call
-    _seed = int(seed) & ((1 << 63) - 1)
+    _seed = rank_seed(int(seed) & _MASK63, _rank())
     _call = 0
     for st in _states.values():
         st.copy_(torch.tensor([_seed, 0], dtype=torch.int64))
@@ -52,9 +78,7 @@ def state(device) -> torch.Tensor:
     key = device.index if device.index is not None else torch.cuda.current_device()
     st = _states.get(key)
     if st is None:
-        if _seed is None:
-            _seed = _default_seed()
-        st = torch.tensor([_seed, 0], dtype=torch.int64, device=torch.device("cuda", key))
+        st = torch.tensor([effective_seed(), 0], dtype=torch.int64, device=torch.device("cuda", key))
         _states[key] = st
     return st
 

@@ -277,6 +277,7 @@ def encoder_stack(blocks, x, context, context_mask=None):
     ctxs = [context] * len(blocks)
     if any(b.context_self_attn is not None for b in blocks):
         main = torch.cuda.current_stream() if _ctx_stream(context) is not None else None
+        kb = _ops.key_bias_of(context_mask)     # built on the main stream, shared by all paths
         evs = []
         for i, blk in enumerate(blocks):
             if blk.context_self_attn is None:
@@ -285,6 +286,11 @@ def encoder_stack(blocks, x, context, context_mask=None):
             cs = _ctx_stream(context, i)
             if cs is not None:
                 cs.wait_stream(main)
+                # tensors crossing streams are recorded on their consumer stream, so the
+                # caching allocator never hands their memory to the producer stream while
+                # the consumer may still read it (the B=16 step read a reused block as
+                # block i's context in the k|v weight gradient without this)
+                _ops.used_on(cs, context, kb)
             p = blk.dropout.p if blk.training else 0.0
             with torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext():
                 c, _ = blk.context_self_attn(context, context, context,
@@ -294,6 +300,7 @@ def encoder_stack(blocks, x, context, context_mask=None):
                     ev = torch.cuda.Event()
                     ev.record(cs)
                     evs.append(ev)
+                    _ops.used_on(main, ctxs[i])
                 else:
                     evs.append(None)
     else:
@@ -307,6 +314,7 @@ def encoder_stack(blocks, x, context, context_mask=None):
         ctx = ctxs[i]
         if evs[i] is not None:
             torch.cuda.current_stream().wait_event(evs[i])
+
         x1, q, kv = _ops.EncPreFn.apply(
             p, x, O, ctx, blk.self_attn.out_proj.weight, blk.self_attn.out_proj.bias,
             blk.layernorm1.weight, blk.layernorm1.bias,

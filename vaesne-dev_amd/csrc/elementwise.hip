@@ -88,16 +88,21 @@ __global__ __launch_bounds__(NT) void embed_bwd_kernel(const int64_t* __restrict
   }
 }
 
-// bottleneck [B, 2*Lz, Dz] -> mu [B, Lz*Dz], scale [B, Lz*Dz]
+// bottleneck [B, 2*Lz, Dz] -> mu [B, Lz*Dz], scale [B, Lz*Dz].  A non-finite mu or
+// scale sets nonfinite[0] = 1 (the reference stops there: PhotometricVAE.py:160-161).
 __global__ void latent_head_fwd_kernel(const float* __restrict__ bott, int B, int n,
-                                       float* __restrict__ mu, float* __restrict__ scale) {
+                                       float* __restrict__ mu, float* __restrict__ scale,
+                                       int* __restrict__ nonfinite) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)B * n) return;
   int64_t b = t / n;
   int j = (int)(t - b * n);
-  mu[t] = bott[b * 2 * n + j];
+  const float m = bott[b * 2 * n + j];
+  mu[t] = m;
   float x = bott[b * 2 * n + n + j];
-  scale[t] = x > 20.f ? x : log1pf(expf(x));
+  const float sc = x > 20.f ? x : log1pf(expf(x));
+  scale[t] = sc;
+  if (nonfinite && !(isfinite(m) && isfinite(sc))) nonfinite[0] = 1;
 }
 
 __global__ void latent_head_bwd_kernel(const float* __restrict__ bott, int B, int n,
@@ -192,6 +197,66 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   }
 }
 
+// Bright*VAE brightness head input (PhotometricVAE.py:321, SpectraVAE.py:311-312):
+// row r of the decoder batch: in[r, :Dz] = zs[r, token 0, :], in[r, Dz] = phase[r % period]
+// (spectra only; phase == null -> width Dz).
+__global__ void bright_in_fwd_kernel(const float* __restrict__ zs, int64_t zrow, int Dz,
+                                     const float* __restrict__ phase, int64_t period, int64_t R,
+                                     float* __restrict__ out) {
+  const int W = Dz + (phase ? 1 : 0);
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; t < R * W; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = t / W;
+    int j = (int)(t - r * W);
+    out[t] = j < Dz ? zs[r * zrow + j] : phase[r % period];
+  }
+}
+
+// its backward: dzs [R, zrow] = token-0 features from din, zero elsewhere
+__global__ void bright_in_bwd_kernel(const float* __restrict__ din, int W, int64_t zrow, int Dz,
+                                     int64_t R, float* __restrict__ dzs) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; t < R * zrow; t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = t / zrow;
+    int j = (int)(t - r * zrow);
+    dzs[t] = j < Dz ? din[r * W + j] : 0.f;
+  }
+}
+
+// out[r, l] = (loc[r, l] + bright[r]) - mean_l loc[r, :]   (PhotometricVAE.py:329,
+// SpectraVAE.py:319); one wave per row, fixed-order sum.
+constexpr int SHIFT_ROWS = 4;
+__global__ __launch_bounds__(64 * SHIFT_ROWS) void bright_shift_fwd_kernel(
+    const float* __restrict__ loc, const float* __restrict__ bright, int64_t R, int L,
+    float* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * SHIFT_ROWS + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  const float* x = loc + r * L;
+  float s = 0.f;
+  for (int l = lane; l < L; l += 64) s += x[l];
+  const float mean = wave_sum(s) / (float)L;
+  const float b = bright[r];
+  for (int l = lane; l < L; l += 64) out[r * L + l] = (x[l] + b) - mean;
+}
+
+// dloc[r, l] = g[r, l] - sum_l g[r, :] / L,  dbright[r] = sum_l g[r, :]
+__global__ __launch_bounds__(64 * SHIFT_ROWS) void bright_shift_bwd_kernel(
+    const float* __restrict__ g, int64_t R, int L, float* __restrict__ dloc,
+    float* __restrict__ dbright) {
+  const int64_t r = (int64_t)blockIdx.x * SHIFT_ROWS + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  const float* gr = g + r * L;
+  float s = 0.f;
+  for (int l = lane; l < L; l += 64) s += gr[l];
+  s = wave_sum(s);
+  const float m = s / (float)L;
+  if (dloc)
+    for (int l = lane; l < L; l += 64) dloc[r * L + l] = gr[l] - m;
+  if (dbright && lane == 0) dbright[r] = s;
+}
+
 __global__ void incr_kernel(float* step, int64_t* rng_state) {
   if (step) *step += 1.f;
   if (rng_state) rng_state[1] += 1;
@@ -276,10 +341,10 @@ VAESNE_API int vaesne_sum_leading(const float* in, int G, int F, float* out, int
 }
 
 VAESNE_API int vaesne_latent_head_fwd(const float* bott, int B, int n, float* mu, float* scale,
-                                      void* stream) {
+                                      int* nonfinite, void* stream) {
   if (B <= 0) return 0;
   hipLaunchKernelGGL(latent_head_fwd_kernel, dim3(blocks_for((int64_t)B * n)), dim3(NT), 0,
-                     (hipStream_t)stream, bott, B, n, mu, scale);
+                     (hipStream_t)stream, bott, B, n, mu, scale, nonfinite);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
@@ -325,6 +390,46 @@ VAESNE_API int vaesne_mask_scale(const uint8_t* mask, int64_t n, int K, float bi
   if (n <= 0) return 0;
   hipLaunchKernelGGL(mask_scale_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream,
                      mask, n, K, big, out);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_bright_input_fwd(const float* zs, int64_t zrow, int Dz, const float* phase,
+                                       int64_t period, int64_t R, float* out, void* stream) {
+  if (R <= 0) return 0;
+  if (Dz < 1 || zrow < Dz || (phase && period < 1)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bright_in_fwd_kernel, dim3(blocks_for(R * (Dz + 1), NT, 4096)), dim3(NT), 0,
+                     (hipStream_t)stream, zs, zrow, Dz, phase, period, R, out);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_bright_input_bwd(const float* din, int width, int64_t zrow, int Dz,
+                                       int64_t R, float* dzs, void* stream) {
+  if (R <= 0) return 0;
+  if (Dz < 1 || zrow < Dz || width < Dz) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bright_in_bwd_kernel, dim3(blocks_for(R * zrow, NT, 4096)), dim3(NT), 0,
+                     (hipStream_t)stream, din, width, zrow, Dz, R, dzs);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_bright_shift_fwd(const float* loc, const float* bright, int64_t R, int L,
+                                       float* out, void* stream) {
+  if (R <= 0) return 0;
+  if (L < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bright_shift_fwd_kernel, dim3((unsigned)((R + SHIFT_ROWS - 1) / SHIFT_ROWS)),
+                     dim3(64 * SHIFT_ROWS), 0, (hipStream_t)stream, loc, bright, R, L, out);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_bright_shift_bwd(const float* g, int64_t R, int L, float* dloc,
+                                       float* dbright, void* stream) {
+  if (R <= 0) return 0;
+  if (L < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bright_shift_bwd_kernel, dim3((unsigned)((R + SHIFT_ROWS - 1) / SHIFT_ROWS)),
+                     dim3(64 * SHIFT_ROWS), 0, (hipStream_t)stream, g, R, L, dloc, dbright);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }

@@ -89,7 +89,8 @@ __global__ __launch_bounds__(NT) void iwae_lw_kernel(IwaeArgs a, float* __restri
 
 // loss = sum_b LME_j lw[j, b]
 __global__ __launch_bounds__(NT) void lme_sum_fwd_kernel(const float* __restrict__ lw, int J,
-                                                         int B, float* __restrict__ loss) {
+                                                         int B, float* __restrict__ loss,
+                                                         int* __restrict__ nonfinite) {
   __shared__ float red[NT / 64];
   float acc = 0.f;
   for (int b = threadIdx.x; b < B; b += NT) {
@@ -100,7 +101,10 @@ __global__ __launch_bounds__(NT) void lme_sum_fwd_kernel(const float* __restrict
     acc += mx + logf(s) - logf((float)J);
   }
   acc = block_sum(acc, red);
-  if (threadIdx.x == 0) *loss = acc;
+  if (threadIdx.x == 0) {
+    *loss = acc;
+    if (nonfinite && !isfinite(acc)) nonfinite[1] = 1;
+  }
 }
 
 // dlw[j, b] = g * softmax_j(lw[:, b])
@@ -215,7 +219,8 @@ __device__ __forceinline__ float kl_lap(float mu, float sc, float pl, float ps) 
 }
 
 // loss = mean_{k,b} lpx - mean_b sum_j KL
-__global__ __launch_bounds__(NT) void elbo_loss_kernel(ElboArgs a, float* __restrict__ loss) {
+__global__ __launch_bounds__(NT) void elbo_loss_kernel(ElboArgs a, float* __restrict__ loss,
+                                                       int* __restrict__ nonfinite) {
   __shared__ float red[NT / 64];
   float s1 = 0.f;
   for (int i = threadIdx.x; i < a.K * a.B; i += NT) s1 += a.lpx[i];
@@ -226,7 +231,11 @@ __global__ __launch_bounds__(NT) void elbo_loss_kernel(ElboArgs a, float* __rest
     s2 += kl_lap(a.mu[i], a.sc[i], a.pz_loc[j], a.pz_scale[j]);
   }
   s2 = block_sum(s2, red);
-  if (threadIdx.x == 0) *loss = s1 / (float)(a.K * a.B) - s2 / (float)a.B;
+  if (threadIdx.x == 0) {
+    const float l = s1 / (float)(a.K * a.B) - s2 / (float)a.B;
+    *loss = l;
+    if (nonfinite && !isfinite(l)) nonfinite[1] = 1;
+  }
 }
 
 __global__ void elbo_dloc_kernel(ElboArgs a, const float* __restrict__ gout, float* dloc) {
@@ -324,9 +333,10 @@ VAESNE_API int vaesne_iwae_lw_bwd(const float* const* x, const float* llik, cons
   return 0;
 }
 
-VAESNE_API int vaesne_lme_sum_fwd(const float* lw, int J, int B, float* loss, void* stream) {
+VAESNE_API int vaesne_lme_sum_fwd(const float* lw, int J, int B, float* loss, int* nonfinite,
+                                  void* stream) {
   hipLaunchKernelGGL(lme_sum_fwd_kernel, dim3(1), dim3(NT), 0, (hipStream_t)stream, lw, J, B,
-                     loss);
+                     loss, nonfinite);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
@@ -342,13 +352,13 @@ VAESNE_API int vaesne_lme_sum_bwd(const float* lw, int J, int B, const float* go
 VAESNE_API int vaesne_elbo_fwd(const float* x, int L, float llik, const float* loc,
                                const float* scale, const float* mu, const float* sc,
                                const float* pz_loc, const float* pz_scale, int K, int B, int n,
-                               float* lpx, float* loss, void* stream) {
+                               float* lpx, float* loss, int* nonfinite, void* stream) {
   if (B <= 0 || K <= 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   ElboArgs a{x, llik, L, loc, scale, mu, sc, pz_loc, pz_scale, K, B, n, lpx};
   hipLaunchKernelGGL(elbo_lpx_kernel, dim3((unsigned)(K * B)), dim3(NT), 0, s, a);
   VAESNE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(elbo_loss_kernel, dim3(1), dim3(NT), 0, s, a, loss);
+  hipLaunchKernelGGL(elbo_loss_kernel, dim3(1), dim3(NT), 0, s, a, loss, nonfinite);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
