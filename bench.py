@@ -246,10 +246,18 @@ def roofline(device, B):
     bits = torch.empty(lib.attn_keep_bits_size(N, H, L, L), dtype=torch.uint8, device=device)
     b, d, s3 = qkv.data_ptr(), dqkv.data_ptr(), L * 3 * E
 
-    def fwd():
-        lib.attn_fwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E, kbias.data_ptr(), L,
-                     o.data_ptr(), L * E, E, lse.data_ptr(), N, H, L, L, dh, pd, st.data_ptr(), 7,
-                     bits.data_ptr(), None, _lib.stream())
+    def fwd_with(bits_in):
+        return lambda: lib.attn_fwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E,
+                                    kbias.data_ptr(), L, o.data_ptr(), L * E, E, lse.data_ptr(),
+                                    N, H, L, L, dh, pd, st.data_ptr(), 7, bits.data_ptr(), bits_in,
+                                    None, _lib.stream())
+
+    def gen():
+        lib.attn_keep_bits(N, H, L, L, pd, st.data_ptr(), 7, bits.data_ptr(), _lib.stream())
+
+    # the step's forward hashes its dropout decisions in-kernel (the pre-drawn bitmap
+    # variant, VAESNE_PREFETCH_DROPOUT=1, is timed beside it with its generator)
+    fwd = fwd_with(0)
 
     def bwd(fn):
         return lambda: fn(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E,
@@ -266,6 +274,12 @@ def roofline(device, B):
         t = time_kernel(fn, 20, device)
         res[name] = dict(kernel=kern, ms=t * 1e3, tflops=scores * fl / t / 1e12,
                          flops_per_launch=scores * fl)
+    if pd > 0:
+        res["keep_bits_gen"] = dict(kernel="attn_keep_bits_kernel",
+                                    ms=time_kernel(gen, 20, device) * 1e3,
+                                    note="draws the forward's keep bitmap ahead (off by default)")
+        res["fwd_bits_in"] = dict(kernel="attn_fwd_kernel<..., BITSIN> (reads the drawn bitmap)",
+                                  ms=time_kernel(fwd_with(1), 20, device) * 1e3)
         tr, src = _rocprof_avg_ms(kern)
         if tr is not None:
             res[name].update(ms_rocprof=tr, tflops_rocprof=scores * fl / (tr * 1e-3) / 1e12,

@@ -80,7 +80,8 @@ int vaesne_reduce_partials(const float* partial, int G, int F, float* out0, floa
  * lse [B,H,Lq] (log2 domain) is saved for the backward.  dh in {8, 16}.
  * Dropout (p_drop > 0): the forward draws the keep mask from the counter RNG
  * and stores it in keep_bits (1 bit per score, vaesne_attn_keep_bits_size
- * bytes); the backward reads it.
+ * bytes), or with bits_in = 1 reads it there (vaesne_attn_keep_bits made it);
+ * the backward reads it.
  * workspace (may be null): vaesne_attn_workspace(..., bwd) bytes.  Shapes whose
  * grid cannot fill the chip (the encoder's 983-token context self-attention,
  * B*H = 64) then run as key / query chunks with a fixed-order combine. */
@@ -92,7 +93,14 @@ int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, 
                     const float* kbias, int64_t kb_bs, float* o, int64_t o_bs, int64_t o_ls,
                     float* lse, int B, int H, int Lq, int Lk, int dh, float p_drop,
                     const int64_t* rng_state, uint32_t call_id, uint32_t* keep_bits,
-                    float* workspace, void* stream);
+                    int bits_in, float* workspace, void* stream);
+/* The keep bitmap a query-tiled forward (Lq > 16) with this shape, rng_state and
+ * call_id draws, generated ahead of it (bit-identical).  Data-independent, so it
+ * can run on a side stream before the attention's inputs exist (e.g. beside the
+ * latency-bound encoders); the forward then reads it with bits_in = 1 instead of
+ * hashing (its dropout VALU work falls by ~85 %), and the backward as usual. */
+int vaesne_attn_keep_bits(int B, int H, int Lq, int Lk, float p_drop, const int64_t* rng_state,
+                          uint32_t call_id, uint32_t* keep_bits, void* stream);
 /* Backward.  Query-tiled shapes read the forward's keep_bits; the few-query
  * path (Lq <= 16: the encoders' latent tokens, one fused key-parallel kernel)
  * re-derives the keep decisions from (rng_state, call_id), which must be the

@@ -508,3 +508,88 @@ def test_fused_encoder_stack_dropout_fwd_bwd_consistent():
     with torch.no_grad():
         fd = (f(x + eps * v)[1].item() - f(x - eps * v)[1].item()) / (2 * eps)
     assert abs(fd - dirn) < 2e-2 * abs(dirn) + 1e-3, (fd, dirn)
+
+
+def _fwd_raw(q, k, v, B, H, L_q, L_k, p, st, cid, bits, bits_in, ws=None):
+    """vaesne_attn_fwd on [B, L, E] q / k / v (separate tensors); returns (o, lse)."""
+    from VAESNe import _lib
+    E = q.shape[-1]
+    o = torch.empty(B, L_q, E, device=DEV)
+    lse = torch.empty(B, H, L_q, device=DEV)
+    rc = _lib.lib.attn_fwd(q.data_ptr(), L_q * E, E, k.data_ptr(), L_k * E, E, v.data_ptr(),
+                           L_k * E, E, None, L_k, o.data_ptr(), L_q * E, E, lse.data_ptr(), B, H,
+                           L_q, L_k, E // H, p, st.data_ptr(), cid, bits.data_ptr(), bits_in,
+                           None if ws is None else ws.data_ptr(), _lib.stream())
+    assert rc == 0
+    return o, lse
+
+
+@pytest.mark.parametrize("geo", [(0, 0), (256, 2), (128, 1), (64, 2)])
+@pytest.mark.parametrize("B,H,Lq,Lk,dh", [(3, 4, 982, 982, 8), (2, 4, 983, 983, 8),
+                                         (2, 4, 300, 77, 8), (5, 2, 17, 17, 8),
+                                         (2, 2, 260, 130, 16)])
+def test_keep_bits_generator_matches_forward_and_bits_in_forward(geo, B, H, Lq, Lk, dh):
+    """vaesne_attn_keep_bits draws the bitmap the hashing forward writes, word for
+    word; the forward reading it (bits_in=1) gives bit-identical o / lse."""
+    from VAESNe import _lib, rng
+    lib = _lib.lib
+    assert lib.attn_force_geometry(*geo) == 0
+    try:
+        E, p, cid = H * dh, 0.1, 9001
+        g = torch.Generator(device=DEV).manual_seed(Lq * 7 + Lk)
+        q, k, v = (torch.randn(B, n, E, device=DEV, generator=g) for n in (Lq, Lk, Lk))
+        st = rng.state(DEV)
+        n = lib.attn_keep_bits_size(B, H, Lq, Lk) // 4
+        bits_fwd = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+        bits_gen = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+        o0, l0 = _fwd_raw(q, k, v, B, H, Lq, Lk, p, st, cid, bits_fwd, 0)
+        assert lib.attn_keep_bits(B, H, Lq, Lk, p, st.data_ptr(), cid, bits_gen.data_ptr(),
+                                  _lib.stream()) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(bits_fwd, bits_gen)
+        o1, l1 = _fwd_raw(q, k, v, B, H, Lq, Lk, p, st, cid, bits_gen, 1)
+        assert torch.equal(o0, o1) and torch.equal(l0, l1)
+        # keep rate of the valid (query, key) bits
+        w = bits_gen.view(B * H, (Lk + 31) // 32, Lq).cpu().numpy().view(np.uint32)
+        bitsv = np.unpackbits(w.view(np.uint8), bitorder="little").reshape(B * H, -1, Lq, 32)
+        keep = bitsv.transpose(0, 2, 1, 3).reshape(B * H, Lq, -1)[:, :, :Lk]
+        rate = 1 - keep.mean()
+        assert abs(rate - p) < 5 * math.sqrt(p * (1 - p) / keep.size), rate
+    finally:
+        lib.attn_force_geometry(0, 0)
+
+
+def test_prefetched_decoder_bitmaps_give_the_hashing_result():
+    """decoder_stack with KeepBits prefetched on the side stream equals the
+    in-kernel hashing path for the same call ids (forward and every gradient)."""
+    from VAESNe import _ops, rng
+    from VAESNe.util_layers import _gen_stream, decoder_stack
+    blocks = _decoder_blocks(2, 3).to(DEV)
+    for b in blocks:     # attention-probability dropout only (the tails draw no ids)
+        b.train()
+        b.self_attn.dropout = 0.1
+    N, L, Lc = 6, 300, 5
+    x0 = torch.randn(N, L, 32, device=DEV)
+    ctx0 = torch.randn(N, Lc, 32, device=DEV)
+    mask = torch.rand(N, L, device=DEV) < 0.1
+    mask[:, 0] = False
+    outs = []
+    for pre in (False, True):
+        x = x0.clone().requires_grad_(True)
+        ctx = ctx0.clone().requires_grad_(True)
+        for b in blocks:
+            b.zero_grad()
+        rng._call = 500
+        keep = None
+        if pre:   # the call ids the hashing path draws for the two self-attentions: 501, 502
+            keep = [_ops.KeepBits(N, 4, L, L, 0.1, x.device, _gen_stream(x.device))
+                    for _ in range(2)]
+        y = decoder_stack(blocks, x, ctx, mask, keep=keep)
+        (y * torch.sin(torch.arange(y.numel(), device=DEV).view_as(y) * 1e-3)).sum().backward()
+        outs.append((y.detach(), x.grad, ctx.grad,
+                     [p.grad.clone() for b in blocks for p in b.parameters() if p.grad is not None]))
+    (y0, dx0, dc0, g0), (y1, dx1, dc1, g1) = outs
+    assert torch.equal(y0, y1)
+    assert torch.equal(dx0, dx1) and torch.equal(dc0, dc1)
+    for a, b in zip(g0, g1):
+        assert torch.equal(a, b)

@@ -35,7 +35,8 @@ class spectraTransformerDecoder(nn.Module):
         phase_embd = self.phase_embd_layer(phase[:, None])
         h = x
         bottleneck = torch.cat([self.contextfc(bottleneck), phase_embd], dim=1)
-        h = decoder_stack(self.transformerblocks, h, bottleneck, mask)
+        keep = self.__dict__.pop("_keep_prefetch", None)   # util_layers.prefetch_decoder_dropout
+        h = decoder_stack(self.transformerblocks, h, bottleneck, mask, keep=keep)
         return self.get_flux(x, h).squeeze(-1)   # get_flux(x + h)
 
 

@@ -10,7 +10,7 @@ from torch import nn
 from . import _ops
 from .SpectraLayers import spectraTransformerDecoder, spectraTransformerEncoder
 from .base_vae import VAE, check_laplace
-from .util_layers import MLP
+from .util_layers import MLP, prefetch_decoder_dropout
 
 
 class SpectraEnc(nn.Module):
@@ -76,6 +76,9 @@ class SpectraVAE(VAE):
 
     def forward(self, x, K=1):
         """SpectraVAE.py:148-165 -> (qz_x, px_z, zs)."""
+        # decoder dropout bitmaps drawn beside the encoder (util_layers.prefetch_decoder_dropout)
+        prefetch_decoder_dropout(self.dec.generativetransformer, K * x[1].shape[0],
+                                 x[1].shape[-1], x[1].device)
         qz_x, zs = self.posterior(x, K)
         px_z = self.decode(zs, x)
         return qz_x, px_z, zs

@@ -288,20 +288,59 @@ def _attn_ws(B, H, Lq, Lk, dh, bwd, dev):
     return _ws(n, dev) if n > 0 else None
 
 
-def _attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, kbias, B, H, Lq, Lk, dh, p, dev):
+class KeepBits:
+    """The dropout keep bitmap of one query-tiled attention forward (Lq > 16),
+    generated ahead of it (vaesne_attn_keep_bits) on `gen_stream`: it depends on
+    the RNG key and the shape only, so it can be drawn while the inputs are still
+    being computed (the decoders' self-attention bitmaps beside the latency-bound
+    encoders).  The forward then reads the bits instead of hashing them."""
+
+    def __init__(self, B, H, Lq, Lk, p, device, gen_stream=None):
+        self.shape = (int(B), int(H), int(Lq), int(Lk))
+        self.p = float(p)
+        self.st = rng.state(device)
+        self.cid = rng.next_call_id()
+        n = lib.attn_keep_bits_size(B, H, Lq, Lk)
+        self.bits = torch.empty((n + 3) // 4, dtype=torch.int32, device=device)
+        self.event = None
+        if gen_stream is not None:
+            gen_stream.wait_stream(torch.cuda.current_stream())
+            used_on(gen_stream, self.bits, self.st)
+            with torch.cuda.stream(gen_stream):
+                lib.attn_keep_bits(B, H, Lq, Lk, self.p, self.st.data_ptr(), self.cid,
+                                   self.bits.data_ptr(), stream())
+                self.event = torch.cuda.Event()
+                self.event.record(gen_stream)
+        else:
+            lib.attn_keep_bits(B, H, Lq, Lk, self.p, self.st.data_ptr(), self.cid,
+                               self.bits.data_ptr(), stream())
+
+    def take(self, B, H, Lq, Lk, p):
+        """Make the current stream wait for the bits; check they fit this launch."""
+        if self.shape != (B, H, Lq, Lk) or abs(self.p - float(p)) > 0:
+            raise RuntimeError(f"prefetched keep bits are for {self.shape}, p={self.p}; "
+                               f"launch is {(B, H, Lq, Lk)}, p={p}")
+        if self.event is not None:
+            torch.cuda.current_stream().wait_event(self.event)
+        return self.bits, self.st, self.cid
+
+
+def _attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, kbias, B, H, Lq, Lk, dh, p, dev, keep=None):
     E = H * dh
     o = torch.empty((B, Lq, E), dtype=torch.float32, device=dev)
     lse = torch.empty((B, H, Lq), dtype=torch.float32, device=dev)
     st = rng.state(dev) if p > 0 else None
-    cid = rng.next_call_id() if p > 0 else 0
+    cid = rng.next_call_id() if p > 0 and keep is None else 0
     bits = None
-    if p > 0:
+    if p > 0 and keep is not None:
+        bits, st, cid = keep.take(B, H, Lq, Lk, p)
+    elif p > 0:
         n = lib.attn_keep_bits_size(B, H, Lq, Lk)
         bits = torch.empty((n + 3) // 4, dtype=torch.int32, device=dev)
     ws = _attn_ws(B, H, Lq, Lk, dh, 0, dev)
     lib.attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, ptr(kbias), Lk, o.data_ptr(), Lq * E, E,
-                 lse.data_ptr(), B, H, Lq, Lk, dh, float(p), ptr(st), cid, ptr(bits), ptr(ws),
-                 stream())
+                 lse.data_ptr(), B, H, Lq, Lk, dh, float(p), ptr(st), cid, ptr(bits),
+                 int(keep is not None and p > 0), ptr(ws), stream())
     return o, lse, bits, st, cid
 
 
@@ -309,7 +348,7 @@ class SelfAttnFn(torch.autograd.Function):
     """Packed qkv [B, L, 3E] -> o [B, L, E] (self-attention, additive key bias)."""
 
     @staticmethod
-    def forward(ctx, qkv, kbias, H, p):
+    def forward(ctx, qkv, kbias, H, p, keep=None):
         _lib.require_device(qkv)
         qkv = qkv.contiguous()
         B, L, E3 = qkv.shape
@@ -318,7 +357,7 @@ class SelfAttnFn(torch.autograd.Function):
         base = qkv.data_ptr()
         o, lse, bits, st, cid = _attn_fwd(base, L * E3, E3, base + 4 * E, L * E3, E3,
                                           base + 8 * E, L * E3, E3, kbias, B, H, L, L, dh, p,
-                                          qkv.device)
+                                          qkv.device, keep)
         ctx.dims = (B, L, E, H, dh, float(p), cid)
         ctx.save_for_backward(qkv, kbias, o, lse, bits, st)
         return o
@@ -336,7 +375,7 @@ class SelfAttnFn(torch.autograd.Function):
                      d, L * E3, E3, d + 4 * E, L * E3, E3, d + 8 * E, L * E3, E3,
                      B, H, L, L, dh, p, ptr(st), cid, ptr(bits),
                      ptr(_attn_ws(B, H, L, L, dh, 1, qkv.device)), stream())
-        return dqkv, None, None, None
+        return dqkv, None, None, None, None
 
 
 class CrossAttnFn(torch.autograd.Function):
@@ -374,9 +413,11 @@ class CrossAttnFn(torch.autograd.Function):
         return dq, dkv, None, None, None
 
 
-def self_attention(qkv, mask, num_heads, p, kbias=None):
-    """mask: bool key_padding_mask (True = ignore) or None; kbias: a prebuilt key_bias."""
-    return SelfAttnFn.apply(qkv, _bias_of(mask, kbias), num_heads, float(p))
+def self_attention(qkv, mask, num_heads, p, kbias=None, keep=None):
+    """mask: bool key_padding_mask (True = ignore) or None; kbias: a prebuilt key_bias;
+    keep: a KeepBits prefetched for this launch (dropout only)."""
+    return SelfAttnFn.apply(qkv, _bias_of(mask, kbias), num_heads, float(p),
+                            keep if p > 0 else None)
 
 
 def cross_attention(q, kv, mask, num_heads, p, kbias=None):

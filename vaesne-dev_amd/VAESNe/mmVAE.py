@@ -8,6 +8,7 @@ import torch.distributions as dist
 import torch.nn as nn
 
 from . import _ops
+from .util_layers import prefetch_decoder_dropout
 
 
 _SIDE = {}
@@ -102,6 +103,15 @@ class photospecMMVAE(nn.Module):
         `px_zs.merged` lets the fused m_iwae read them in place."""
         n = len(self.vaes)
         side = _side_stream(x[0][0]) if n == 2 else None
+        merged = all((v.latent_len, v.latent_dim) == (self.vaes[0].latent_len,
+                                                       self.vaes[0].latent_dim) for v in self.vaes)
+        if merged:
+            # the decoders' dropout bitmaps only depend on the RNG key: draw them now,
+            # beside the latency-bound encoders (util_layers.prefetch_decoder_dropout)
+            B = x[0][0].shape[0]
+            for d, vae in enumerate(self.vaes):
+                prefetch_decoder_dropout(vae.dec.generativetransformer, K * n * B,
+                                         x[d][1].shape[-1], x[d][1].device)
         qz_xs, zss = [None] * n, [None] * n
         with _Branches(side) as br:
             br.to_side(*x[0])

@@ -197,7 +197,47 @@ def _fusable_decoder_block(blk):
             and all(ln.eps == 1e-5 for ln in (blk.layernorm1, blk.layernorm2, blk.layernorm3)))
 
 
-def decoder_stack(blocks, x, context, mask=None):
+_GEN_STREAMS = {}
+
+
+def _gen_stream(dev):
+    """Side stream the decoders' dropout bitmaps are drawn on (VAESNE_STREAMS=0: none)."""
+    if os.environ.get("VAESNE_STREAMS", "1") == "0":
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _GEN_STREAMS.get(idx)
+    if st is None:
+        st = _GEN_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return st
+
+
+def prefetch_decoder_dropout(decoder, N, L, device):
+    """Draw, ahead of the decoder's forward, the keep bitmaps of its blocks' masked
+    self-attention dropout (N sequences x L tokens) on a side stream, and hand them
+    to the decoder's next forward.  The bitmaps depend on the RNG key only, so at the
+    start of a step they can be drawn while the latency-bound encoders leave the chip
+    mostly idle, and the attention forwards read them instead of hashing (their
+    dropout VALU work falls by ~85 %, 27 % of the forward's VALU instructions).
+    OFF by default (VAESNE_PREFETCH_DROPOUT=1 enables it): measured on MI355X the
+    forward held the same time (0.63 ms: it runs power-limited, and with fewer VALU
+    instructions the chip clocks lower, 2.08 vs 2.28 GHz), while the generator's
+    0.19 ms per layer delayed the encoders, 12.8 vs 12.5 ms per step (profiles/r02_prefetch).
+    No-op outside training, without dropout, or for short sequences (L < 128)."""
+    blocks = list(getattr(decoder, "transformerblocks", []))
+    if (not blocks or not decoder.training or L < 128 or not device.type == "cuda"
+            or os.environ.get("VAESNE_PREFETCH_DROPOUT", "0") != "1"
+            or not all(_fusable_decoder_block(b) for b in blocks)):
+        return
+    gs = _gen_stream(device)
+    keep = []
+    for blk in blocks:
+        p = blk.self_attn.dropout
+        keep.append(_ops.KeepBits(N, blk.self_attn.num_heads, L, L, p, device, gs)
+                    if p > 0 else None)
+    decoder._keep_prefetch = keep
+
+
+def decoder_stack(blocks, x, context, mask=None, keep=None):
     """`for blk in blocks: x = blk(x, context, mask=mask)` for the decoders
     (SpectraLayers.py:61-62, PhotometricLayers.py:66-67).  With the reference's
     decoder shape (E 32, 4 heads, ff 32, no context self-attention) each block
@@ -215,10 +255,16 @@ def decoder_stack(blocks, x, context, mask=None):
     b0 = blocks[0].self_attn
     qkv = _ops.linear(x, b0.in_proj_weight, b0.in_proj_bias)
     kbias = _ops.key_bias(mask)          # one mask conversion for all layers
+    N = x.shape[0]
+    if keep is not None and (len(keep) != len(blocks) or any(
+            k is not None and k.shape != (N, blk.self_attn.num_heads, L, L)
+            for k, blk in zip(keep, blocks))):
+        keep = None      # prefetched for another shape: draw in the kernels
     for i, blk in enumerate(blocks):
         p_attn = blk.self_attn.dropout if blk.training else 0.0
         p = blk.dropout.p if blk.training else 0.0
-        O = _ops.self_attention(qkv, None, blk.self_attn.num_heads, p_attn, kbias=kbias)
+        O = _ops.self_attention(qkv, None, blk.self_attn.num_heads, p_attn, kbias=kbias,
+                                keep=None if keep is None else keep[i])
         nxt = blocks[i + 1].self_attn if i + 1 < len(blocks) else None
         x, qkv = _ops.DecTailFn.apply(
             L, p, x, O, context, blk.cross_attn.in_proj_weight, blk.cross_attn.in_proj_bias,

@@ -164,13 +164,37 @@ __device__ __forceinline__ void stage(float* dst, const float* __restrict__ src,
   }
 }
 
+// 0/1 float masks of the 4 bits of a nibble (bit j -> component j)
+__device__ __forceinline__ float4 nibble_mask(uint32_t i) {
+  return make_float4((float)(i & 1u), (float)((i >> 1) & 1u), (float)((i >> 2) & 1u),
+                     (float)((i >> 3) & 1u));
+}
+
 // ============================== forward ====================================
 // lane owns 2*NP queries: pair p = {i + (2p) NTT, i + (2p+1) NTT}
-template <int DH, int NTT, int NP, bool DROP>
+// BITSIN (with DROP): the keep bitmap was generated ahead by attn_keep_bits_kernel
+// (bit-identical to what this kernel's hashing path writes); the kernel reads it
+// instead of hashing: per 8 keys and query pair, the two rows' keep bytes are
+// bit-interleaved through an LDS spread table and each key pair's 4 decisions
+// become one LDS float4 mask (~40 VALU ops per 8-key x 4-query trip instead of
+// ~250 for the hash and decisions).
+template <int DH, int NTT, int NP, bool DROP, bool BITSIN = false>
 __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Ks[TK * DH];
   __shared__ __attribute__((aligned(16))) float Vs[TK * DH];
   __shared__ float Kb[TK];
+  __shared__ uint32_t Sp[BITSIN ? 256 : 1];              // byte -> bits at even positions
+  __shared__ __attribute__((aligned(16))) float4 Mn[BITSIN ? 16 : 1];   // nibble -> masks
+  if (BITSIN) {
+    for (int i = threadIdx.x; i < 256; i += NTT) {
+      uint32_t x = (uint32_t)i;
+      x = (x | (x << 4)) & 0x0f0fu;
+      x = (x | (x << 2)) & 0x3333u;
+      x = (x | (x << 1)) & 0x5555u;
+      Sp[i] = x;
+    }
+    if (threadIdx.x < 16) Mn[threadIdx.x] = nibble_mask(threadIdx.x);
+  }
   constexpr int R = 2 * NP;
   constexpr int QB = R * NTT;
   const int nqb = (a.Lq + QB - 1) / QB;
@@ -202,7 +226,7 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   }
   uint32_t rk[R];
   uint32_t skey = 0u;
-  if (DROP) {
+  if (DROP && !BITSIN) {
     skey = key_of(a.rng_state, a.call_id);
 #pragma unroll
     for (int u = 0; u < R; ++u) rk[u] = attn_row_key(skey, (uint32_t)((int64_t)bh * a.Lq + qc[u]));
@@ -224,6 +248,14 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
     uint32_t w[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) w[u] = 0u;
+    uint32_t wb[R][2];   // BITSIN: this tile's two keep words per row
+    if (DROP && BITSIN) {
+#pragma unroll
+      for (int t = 0; t < R; ++t) {
+        wb[t][0] = bitp[(int64_t)(kt >> 5) * a.Lq + qc[t]];
+        wb[t][1] = (kt >> 5) + 1 < a.nw ? bitp[(int64_t)((kt >> 5) + 1) * a.Lq + qc[t]] : 0u;
+      }
+    }
     for (int g0 = 0; g0 < kend; g0 += 8) {
       f2 s[NP][8];
       f2 x[NP];
@@ -266,6 +298,13 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int p = 0; p < NP; ++p)
         mu[p] = (f2){m[p].x == -INFINITY ? 0.f : m[p].x, m[p].y == -INFINITY ? 0.f : m[p].y};
+      uint32_t z[NP];   // BITSIN: rows (2p, 2p+1) keep bits of these 8 keys, interleaved
+      if (DROP && BITSIN) {
+        const int ws = g0 >> 5, sh = g0 & 31;
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+          z[p] = Sp[(wb[2 * p][ws] >> sh) & 0xffu] | (Sp[(wb[2 * p + 1][ws] >> sh) & 0xffu] << 1);
+      }
 #pragma unroll
       for (int u = 0; u < 8; u += 2) {
         f2 p0[NP], p1[NP];
@@ -275,7 +314,14 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
           p1[p] = ex2(s[p][u + 1] - mu[p]);
           l[p] += p0[p] + p1[p];
         }
-        if (DROP) {
+        if (DROP && BITSIN) {
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            const float4 mk = Mn[(z[p] >> (2 * u)) & 15u];
+            p0[p] *= (f2){mk.x, mk.y};
+            p1[p] *= (f2){mk.z, mk.w};
+          }
+        } else if (DROP) {
           const uint32_t kpm = attn_keypair_mix(skey, (uint32_t)((kt + g0 + u) >> 1));
           const int sh = (g0 + u) & 31;
           uint32_t kk[R];
@@ -303,7 +349,7 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
           }
         }
       }
-      if (DROP && (((g0 + 8) & 31) == 0 || g0 + 8 >= kend)) {
+      if (DROP && !BITSIN && (((g0 + 8) & 31) == 0 || g0 + 8 >= kend)) {
         const int word = (kt + g0) >> 5;
 #pragma unroll
         for (int t = 0; t < R; ++t) {
@@ -911,6 +957,42 @@ __global__ __launch_bounds__(SNT) void attn_bwd_smallq_kernel(AttnArgs a) {
   }
 }
 
+// The keep bitmap of a query-tiled forward launch, generated ahead of it:
+// bit-identical to what attn_fwd_kernel's hashing path writes for the same
+// (rng_state, call_id, shape) -- keys below round_up(Lk, 8) hashed, the rest 0.
+// lane = query (coalesced [word][query] stores), grid.y = word chunks.  Pure
+// integer VALU work with no data inputs, so it can run on a side stream while
+// the latency-bound encoders leave the chip idle (bits per layer: B*H*Lq*Lk).
+constexpr int GEN_NT = 256, GEN_WORDS = 8;
+__global__ __launch_bounds__(GEN_NT) void attn_keep_bits_kernel(int BH, int Lq, int Lk, int nw,
+                                                               uint32_t thr,
+                                                               const int64_t* rng_state,
+                                                               uint32_t call_id,
+                                                               uint32_t* __restrict__ bits) {
+  const int nqb = (Lq + GEN_NT - 1) / GEN_NT;
+  const int bh = blockIdx.x / nqb, qb = blockIdx.x - bh * nqb;
+  const int q = qb * GEN_NT + threadIdx.x;
+  if (bh >= BH) return;
+  const uint32_t skey = key_of(rng_state, call_id);
+  const uint32_t rk = attn_row_key(skey, (uint32_t)((int64_t)bh * Lq + min(q, Lq - 1)));
+  const int klim = (Lk + 7) & ~7;
+  const int w0 = blockIdx.y * GEN_WORDS, w1 = min(nw, w0 + GEN_WORDS);
+  uint32_t* out = bits + (int64_t)bh * nw * Lq + q;
+  for (int wd = w0; wd < w1; ++wd) {
+    uint32_t w = 0u;
+#pragma unroll 4
+    for (int j = 0; j < 32; j += 2) {
+      const int key = wd * 32 + j;
+      if (key < klim) {
+        const uint32_t kpm = attn_keypair_mix(skey, (uint32_t)(key >> 1));
+        const uint32_t hb = attn_pair_bits_mixed(rk, kpm);
+        w |= (((hb & 0xffffu) >= thr ? 1u : 0u) | ((hb >> 16) >= thr ? 2u : 0u)) << j;
+      }
+    }
+    if (q < Lq) out[(int64_t)wd * Lq] = w;
+  }
+}
+
 __global__ void mask_bias_kernel(const uint8_t* __restrict__ m, int64_t n, float* __restrict__ out) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < n) out[t] = m[t] ? -INFINITY : 0.f;
@@ -1091,7 +1173,7 @@ int64_t bwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sq, Split& sk
   }
 
 template <int DHV>
-int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s) {
+int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s, bool bits_in) {
   if (a.Lq <= 2 * SQ) {
     dim3 grid((unsigned)((int64_t)a.B * a.H), (unsigned)((a.Lq + SQ - 1) / SQ));
     if (p_drop > 0.f)
@@ -1116,7 +1198,9 @@ int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s) {
   VAESNE_GEO_SWITCH(g, {
     const int nqb = (a.Lq + 2 * NP * NTT - 1) / (2 * NP * NTT);
     dim3 grid((unsigned)((int64_t)a.B * a.H * nqb), (unsigned)sp.n);
-    if (p_drop > 0.f)
+    if (p_drop > 0.f && bits_in)
+      hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, true, true>), grid, dim3(NTT), 0, s, c);
+    else if (p_drop > 0.f)
       hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, true>), grid, dim3(NTT), 0, s, c);
     else
       hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, c);
@@ -1258,16 +1342,35 @@ VAESNE_API int64_t vaesne_attn_workspace(int B, int H, int Lq, int Lk, int dh, i
   return f * (int64_t)sizeof(float);
 }
 
+VAESNE_API int vaesne_attn_keep_bits(int B, int H, int Lq, int Lk, float p_drop,
+                                     const int64_t* rng_state, uint32_t call_id,
+                                     uint32_t* keep_bits, void* stream) {
+  if (B <= 0 || Lq <= 0) return 0;
+  if (Lk <= 0 || Lq <= 2 * SQ || p_drop <= 0.f || !keep_bits || !rng_state)
+    return (int)hipErrorInvalidValue;
+  const int nw = (Lk + 31) / 32;
+  const int64_t BH = (int64_t)B * H;
+  const dim3 grid((unsigned)(BH * ((Lq + GEN_NT - 1) / GEN_NT)),
+                  (unsigned)((nw + GEN_WORDS - 1) / GEN_WORDS));
+  hipLaunchKernelGGL(attn_keep_bits_kernel, grid, dim3(GEN_NT), 0, (hipStream_t)stream, (int)BH,
+                     Lq, Lk, nw, drop_thr16(p_drop), rng_state, call_id, keep_bits);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
 VAESNE_API int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k,
                                int64_t k_bs, int64_t k_ls, const float* v, int64_t v_bs,
                                int64_t v_ls, const float* kbias, int64_t kb_bs, float* o,
                                int64_t o_bs, int64_t o_ls, float* lse, int B, int H, int Lq,
                                int Lk, int dh, float p_drop, const int64_t* rng_state,
-                               uint32_t call_id, uint32_t* keep_bits, float* workspace,
-                               void* stream) {
+                               uint32_t call_id, uint32_t* keep_bits, int bits_in,
+                               float* workspace, void* stream) {
   if (B <= 0 || Lq <= 0) return 0;
   if (Lk <= 0 || (dh != 8 && dh != 16)) return (int)hipErrorInvalidValue;
   if (p_drop > 0.f && (!keep_bits || !rng_state)) return (int)hipErrorInvalidValue;
+  // a pre-generated bitmap is read by the query-tiled kernels (the few-query path
+  // never uses one)
+  if (bits_in && (Lq <= 2 * SQ || p_drop <= 0.f)) return (int)hipErrorInvalidValue;
   if (!aligned16(q, q_ls) || !aligned16(k, k_ls) || !aligned16(v, v_ls) || !aligned16(o, o_ls))
     return (int)hipErrorInvalidValue;
   AttnArgs a{};
@@ -1280,8 +1383,8 @@ VAESNE_API int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const
   a.bits = keep_bits;
   fill_common(a, B, H, Lq, Lk, dh, p_drop, rng_state, call_id);
   hipStream_t s = (hipStream_t)stream;
-  if (dh == 8) return launch_fwd<8>(a, p_drop, workspace, s);
-  return launch_fwd<16>(a, p_drop, workspace, s);
+  if (dh == 8) return launch_fwd<8>(a, p_drop, workspace, s, bits_in != 0);
+  return launch_fwd<16>(a, p_drop, workspace, s, bits_in != 0);
 }
 
 namespace {
