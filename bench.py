@@ -23,6 +23,7 @@ Rank 0 prints ONE JSON line (value = whole-job SN pairs/s).  Beside it:
                  max-rel errors of the latent mu / scale.
 """
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -100,9 +101,14 @@ class Step:
         model.train()
 
     def fwd_bwd(self):
+        try:
+            from VAESNe._defer import deferred
+        except ImportError:            # an older package under profiles/ab_pkg.sh
+            deferred = contextlib.nullcontext
         self.opt.zero_grad(set_to_none=True)
-        loss = -self.loss_fn(self.model, self.x)
-        loss.backward()
+        with deferred():   # parameter-gradient sums: one batched launch at the end of backward
+            loss = -self.loss_fn(self.model, self.x)
+            loss.backward()
         self.opt.pack_grads()
         self.loss.copy_(loss.detach())
 

@@ -31,6 +31,33 @@
 extern "C" {
 #endif
 
+/* ---- deferred parameter-gradient sums -------------------------------------
+ * Every parameter gradient is a fixed-order sum over per-workgroup partials.
+ * The entry points producing one take `defer` (nullable): null = launch the
+ * column sum now; a list = append the sum (partials, their row stride, groups,
+ * columns, output, accumulate flag) so that one vaesne_colsum_flush per backward
+ * pass finishes every pending sum in one or two launches (instead of one launch
+ * per parameter tensor).  The caller keeps the partials and outputs alive until
+ * the flush, orders the flush after every producer (streams), and reads no
+ * output before it.  A full list makes the producing call fail
+ * (hipErrorOutOfMemory): size `capacity` for a whole backward pass. */
+typedef struct vaesne_colsum_entry {
+  const float* partial;   /* [groups][ld] */
+  int64_t ld;
+  int groups;
+  int cols;               /* out[c] (+)= sum_g partial[g * ld + c], c < cols */
+  float* out;
+  int accum;
+} vaesne_colsum_entry;
+typedef struct vaesne_colsum_list {
+  vaesne_colsum_entry* entries;
+  int count;
+  int capacity;
+} vaesne_colsum_list;
+/* Launch every pending sum of `list` on `stream` (entries whose outputs overlap
+ * an earlier entry's are ordered after it) and empty the list. */
+int vaesne_colsum_flush(vaesne_colsum_list* list, void* stream);
+
 /* ---- token-wise linear layers ------------------------------------------
  * nn.Linear(K->N) (+ ReLU / exact GELU) on rows of a token matrix:
  * util_layers.py:9-18 (singlelayerMLP), :20-34 (MLP), :142-149 (sinusoidal
@@ -45,12 +72,13 @@ int vaesne_linear_fwd(const float* x, int64_t ldx, const float* x2, int64_t ldx2
 int vaesne_linear_bwd_data(const float* dy, int64_t lddy, const float* z, int64_t ldz, int act,
                            int64_t M, int N, const float* W, int K, float* dx, int64_t lddx,
                            int accum, void* stream);
-/* dW (+)= (dy*act'(z))^T (x [+ x2]),  db (+)= colsum(dy*act'(z)) */
+/* dW (+)= (dy*act'(z))^T (x [+ x2]),  db (+)= colsum(dy*act'(z)): MFMA partials per
+ * workgroup in `workspace`, then the fixed-order column sum (now, or deferred). */
 int64_t vaesne_linear_bwd_weight_workspace(int64_t M, int O, int I);
 int vaesne_linear_bwd_weight(const float* dy, int64_t lddy, const float* z, int64_t ldz, int act,
                              const float* x, int64_t ldx, const float* x2, int64_t ldx2,
                              int64_t M, int O, int I, float* dW, float* db, int accum,
-                             float* workspace, void* stream);
+                             float* workspace, vaesne_colsum_list* defer, void* stream);
 
 /* ---- post-LN residual join ------------------------------------------------
  * TransformerBlock: x = LayerNorm(x + Dropout(res))  util_layers.py:291,298,303,307
@@ -65,7 +93,8 @@ int vaesne_add_ln_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx
                       const float* mean, const float* rstd, float p_drop,
                       const int64_t* rng_state, uint32_t call_id, float* dx, int64_t lddx,
                       int accum_dx, float* dres, int64_t lddres, int accum_dres, float* dgamma,
-                      float* dbeta, int accum_param, float* workspace, void* stream);
+                      float* dbeta, int accum_param, float* workspace, vaesne_colsum_list* defer,
+                      void* stream);
 /* out0[f] (+)= sum_g partial[g*F+f] (f < split), out1 likewise (f >= split) */
 int vaesne_reduce_partials(const float* partial, int G, int F, float* out0, float* out1,
                            int split, int accum, void* stream);
@@ -149,7 +178,12 @@ int vaesne_attn_force_geometry(int nt, int np);
  * Wn/bn = next self in_proj [96, 32] / [96], null when not fused; qkv [M, 96]).
  * bwd: gflat = ONE device buffer receiving every parameter gradient of the
  * block at the offsets vaesne_dec_tail_grad_layout() reports (same order as w;
- * returns the buffer length, 8640 floats); y = the forward output; dqkv
+ * returns the buffer length, 10752 floats).  The Wq / bq regions span all 3E
+ * rows of the cross in_proj (3072 / 96 floats): the kernel fills rows [0, E),
+ * the caller's k | v projection gradient goes into rows [E, 3E) in place, so
+ * the whole in_proj gradient is one view (the block's column sums never write
+ * those rows, deferred or not).  dkvc is complete when the call's work ends.
+ * y = the forward output; dqkv
  * required iff Wn; workspace sized by vaesne_dec_tail_workspace.
  * drop_masks (nullable, p_drop > 0): uint32 [M][4] keep masks of the block's four
  * dropout sites, written by the forward and read by the backward instead of
@@ -163,7 +197,7 @@ int vaesne_dec_tail_bwd(const float* x, const float* O, const float* kvc, int M,
                         const float* const* w, float p_drop, const int64_t* rng_state,
                         uint32_t call_id, const float* y, const float* dy, const float* dqkv,
                         const uint32_t* drop_masks, float* dx, float* dO, float* dkvc,
-                        float* gflat, float* workspace, void* stream);
+                        float* gflat, float* workspace, vaesne_colsum_list* defer, void* stream);
 int vaesne_dec_tail_grad_layout(int* offsets);
 
 /* ---- encoder-block halves ------------------------------------------------------
@@ -177,8 +211,8 @@ int vaesne_dec_tail_grad_layout(int* offsets);
  *                  Drop(c Wo2^T + bo2)), FFN(GELU), y = LN3(x2 + Drop(f)),
  *                  q_or_qkv = y Wn^T + bn [M, 96] (when Wn, the next block's in_proj)
  * w: the 18-pointer array of vaesne_dec_tail_fwd (entries the mode does not use may
- * be null); gflat / its layout as vaesne_dec_tail_bwd (the other half's entries
- * are 0).  bwd: dy = d y; dq_or_dqkv = d q (PRE) or d qkv_next (POST, iff Wn);
+ * be null); gflat / its layout as vaesne_dec_tail_bwd (only the mode's own
+ * entries are written).  bwd: dy = d y; dq_or_dqkv = d q (PRE) or d qkv_next (POST, iff Wn);
  * dx = d x (PRE) / d x1 (POST); dO = d O (PRE) / d c (POST).  drop_masks: uint32
  * [M][4], required when p_drop > 0 (written by fwd, read by bwd).  Workspace sized
  * by vaesne_enc_block_workspace(M). */
@@ -190,7 +224,7 @@ int vaesne_enc_block_bwd(int mode, const float* x, const float* O, int M, const 
                          float p_drop, const int64_t* rng_state, uint32_t call_id,
                          const float* y, const float* dy, const float* dq_or_dqkv,
                          const uint32_t* drop_masks, float* dx, float* dO, float* gflat,
-                         float* workspace, void* stream);
+                         float* workspace, vaesne_colsum_list* defer, void* stream);
 
 /* ---- embeddings ------------------------------------------------------------
  * [sin(x*div) | cos(x*div)]: util_layers.py:125-129 (plain, 16 freqs) and
@@ -207,7 +241,7 @@ int vaesne_embed_fwd(const int64_t* idx, int64_t period, int64_t rows, const flo
 int64_t vaesne_embed_bwd_workspace(int64_t rows, int E, int nb);
 int vaesne_embed_bwd(const int64_t* idx, int64_t period, int64_t rows, const float* dout,
                      int64_t lddo, int E, int nb, float* dtable, int accum, float* workspace,
-                     void* stream);
+                     vaesne_colsum_list* defer, void* stream);
 /* out[f] (+)= sum_g in[g*F+f]: backward of x.repeat(B,1,1) (initbottleneck,
  * PhotometricLayers.py:137-138, SpectraLayers.py:134-135) */
 int vaesne_sum_leading(const float* in, int G, int F, float* out, int accum, void* stream);

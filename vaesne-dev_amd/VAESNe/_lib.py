@@ -34,11 +34,12 @@ SIGNATURES = {
     "vaesne_linear_bwd_data": (I32, [P, I64, P, I64, I32, I64, I32, P, I32, P, I64, I32, P]),
     "vaesne_linear_bwd_weight_workspace": (I64, [I64, I32, I32]),
     "vaesne_linear_bwd_weight": (I32, [P, I64, P, I64, I32, P, I64, P, I64, I64, I32, I32, P, P,
-                                       I32, P, P]),
+                                       I32, P, P, P]),
+    "vaesne_colsum_flush": (I32, [P, P]),
     "vaesne_add_ln_fwd": (I32, [P, I64, P, I64, I64, I32, P, P, F32, P, U32, P, I64, P, P, P]),
     "vaesne_add_ln_bwd_workspace": (I64, [I64, I32]),
     "vaesne_add_ln_bwd": (I32, [P, I64, P, I64, P, I64, I64, I32, P, P, P, F32, P, U32, P, I64,
-                                I32, P, I64, I32, P, P, I32, P, P]),
+                                I32, P, I64, I32, P, P, I32, P, P, P]),
     "vaesne_reduce_partials": (I32, [P, I32, I32, P, P, I32, I32, P]),
     "vaesne_mask_bias": (I32, [P, I64, P, P]),
     "vaesne_attn_keep_bits_size": (I64, [I32, I32, I32, I32]),
@@ -52,16 +53,17 @@ SIGNATURES = {
     "vaesne_dec_tail_workspace": (I64, [I32, I32, I32]),
     "vaesne_dec_tail_fwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P, P]),
     "vaesne_dec_tail_bwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P, P, P, P, P,
-                                  P, P, P]),
+                                  P, P, P, P]),
     "vaesne_dec_tail_grad_layout": (I32, [C.POINTER(I32)]),
     "vaesne_enc_block_workspace": (I64, [I32]),
     "vaesne_attn_force_geometry": (I32, [I32, I32]),
     "vaesne_enc_block_fwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P]),
-    "vaesne_enc_block_bwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P, P, P, P, P, P]),
+    "vaesne_enc_block_bwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P, P, P, P, P, P,
+                                   P]),
     "vaesne_sincos": (I32, [P, I64, I64, P, I32, P, I64, P]),
     "vaesne_embed_fwd": (I32, [P, I64, I64, P, I32, P, I64, P, I64, P]),
     "vaesne_embed_bwd_workspace": (I64, [I64, I32, I32]),
-    "vaesne_embed_bwd": (I32, [P, I64, I64, P, I64, I32, I32, P, I32, P, P]),
+    "vaesne_embed_bwd": (I32, [P, I64, I64, P, I64, I32, I32, P, I32, P, P, P]),
     "vaesne_sum_leading": (I32, [P, I32, I32, P, I32, P]),
     "vaesne_latent_head_fwd": (I32, [P, I32, I32, P, P, P, P]),
     "vaesne_latent_head_bwd": (I32, [P, I32, I32, P, P, P, P]),

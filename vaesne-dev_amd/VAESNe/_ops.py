@@ -11,7 +11,7 @@ import math
 
 import torch
 
-from . import _lib, guard, rng
+from . import _defer, _lib, guard, rng
 from ._lib import lib, ptr, stream
 
 ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
@@ -55,6 +55,8 @@ class LinearFn(torch.autograd.Function):
     def forward(ctx, x, W, b, act, x2, base):
         _lib.require_device(x, W, b, x2, base)
         _f32(x)
+        _defer.count_uses(W, b)
+        ctx.params = (W, b)
         lead = x.shape[:-1]
         K = x.shape[-1]
         N = W.shape[0]
@@ -96,9 +98,10 @@ class LinearFn(torch.autograd.Function):
             dW = torch.empty((N, K), dtype=torch.float32, device=dy.device)
             db = torch.empty((N,), dtype=torch.float32, device=dy.device) if ctx.has_b else None
             ws = _ws(lib.linear_bwd_weight_workspace(M, N, K), dy.device)
+            dfr = _defer.target(ctx.params, (dW, db), (ws,))
             lib.linear_bwd_weight(dy.data_ptr(), N, ptr(z), N, act, xr.data_ptr(), ctx.ldx,
                                   ptr(x2r), ctx.ldx2, M, N, K, dW.data_ptr(), ptr(db), 0,
-                                  ws.data_ptr(), s)
+                                  ws.data_ptr(), dfr, s)
         return (dx if ctx.needs_input_grad[0] else None, dW, db, None,
                 dx if ctx.needs_input_grad[4] else None,
                 dy.view(*ctx.xshape[:-1], N) if ctx.needs_input_grad[5] else None)
@@ -120,6 +123,8 @@ class InProjPairFn(torch.autograd.Function):
     def forward(ctx, query, key, W, b):
         _lib.require_device(query, key, W, b)
         _f32(query)
+        _defer.count_uses(W, b)
+        ctx.params = (W, b)
         E = W.shape[1]
         W = W.contiguous()
         b = b.contiguous() if b is not None else None
@@ -164,14 +169,15 @@ class InProjPairFn(torch.autograd.Function):
         if ng[2] or ng[3]:
             dW = torch.empty((3 * E, E), dtype=torch.float32, device=dev)
             db = torch.empty((3 * E,), dtype=torch.float32, device=dev) if has_b else None
-            ws = _ws(max(lib.linear_bwd_weight_workspace(Mq, E, E),
-                         lib.linear_bwd_weight_workspace(Mk, 2 * E, E)), dev)
+            ws = _ws(lib.linear_bwd_weight_workspace(Mq, E, E), dev)
+            ws2 = _ws(lib.linear_bwd_weight_workspace(Mk, 2 * E, E), dev)
+            dfr = _defer.target(ctx.params, (dW, db), (ws, ws2))
             dbp = ptr(db)
             lib.linear_bwd_weight(dq.data_ptr(), E, None, 0, 0, qr.data_ptr(), ldq, None, 0,
-                                  Mq, E, E, dW.data_ptr(), dbp, 0, ws.data_ptr(), s)
+                                  Mq, E, E, dW.data_ptr(), dbp, 0, ws.data_ptr(), dfr, s)
             lib.linear_bwd_weight(dkv.data_ptr(), 2 * E, None, 0, 0, kr.data_ptr(), ldk, None, 0,
                                   Mk, 2 * E, E, dW.data_ptr() + 4 * E * E,
-                                  None if dbp is None else dbp + 4 * E, 0, ws.data_ptr(), s)
+                                  None if dbp is None else dbp + 4 * E, 0, ws2.data_ptr(), dfr, s)
         return dquery, dkey, dW if ng[2] else None, db if ng[3] else None
 
 
@@ -187,6 +193,8 @@ class AddLNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, gamma, beta, p, eps):
         _lib.require_device(x, res, gamma, beta)
+        _defer.count_uses(gamma, beta)
+        ctx.params = (gamma, beta)
         if abs(eps - 1e-5) > 1e-12:
             raise RuntimeError("VAESNe LayerNorm kernel is built for eps=1e-5 (nn.LayerNorm default)")
         E = x.shape[-1]
@@ -215,10 +223,11 @@ class AddLNFn(torch.autograd.Function):
         dg = torch.empty_like(gamma)
         dbt = torch.empty_like(gamma)
         ws = _ws(lib.add_ln_bwd_workspace(M, E), dy.device)
+        dfr = _defer.target(ctx.params, (dg, dbt), (ws,))
         lib.add_ln_bwd(dy.data_ptr(), E, x.data_ptr(), E, res.data_ptr(), E, M, E,
                        gamma.data_ptr(), mean.data_ptr(), rstd.data_ptr(), float(ctx.p), ptr(st),
                        ctx.cid, dx.data_ptr(), E, 0, dres.data_ptr(), E, 0, dg.data_ptr(),
-                       dbt.data_ptr(), 0, ws.data_ptr(), stream())
+                       dbt.data_ptr(), 0, ws.data_ptr(), dfr, stream())
         return dx, dres, dg, dbt, None, None
 
 
@@ -444,6 +453,8 @@ class EmbedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, table, base):
         _lib.require_device(idx, table, base)
+        _defer.count_uses(table)
+        ctx.params = (table,)
         idx = idx.contiguous()
         if idx.dtype != torch.int64:
             idx = idx.long()
@@ -470,8 +481,9 @@ class EmbedFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dt = torch.empty((ctx.nb, ctx.E), dtype=torch.float32, device=dout.device)
             ws = _ws(lib.embed_bwd_workspace(n, ctx.E, ctx.nb), dout.device)
+            dfr = _defer.target(ctx.params, (dt,), (ws,))
             lib.embed_bwd(idx.data_ptr(), max(n, 1), n, dout.data_ptr(), ctx.E, ctx.E, ctx.nb,
-                          dt.data_ptr(), 0, ws.data_ptr(), stream())
+                          dt.data_ptr(), 0, ws.data_ptr(), dfr, stream())
         return None, dt, (dout if ctx.needs_input_grad[2] else None)
 
 
@@ -876,6 +888,8 @@ class DecTailFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, L, p, x, O, context, Wc, bc, *w16):
         _lib.require_device(x, O, context, Wc, bc)
+        ctx.params = w16[:4] + (Wc, bc) + w16[4:]       # C-ABI order (see w below)
+        _defer.count_uses(*ctx.params)
         x, O, context = x.contiguous(), O.contiguous(), context.contiguous()
         Wc, bc = Wc.contiguous(), bc.contiguous()
         E = 32
@@ -922,30 +936,33 @@ class DecTailFn(torch.autograd.Function):
         offs, total = _tail_layout()
         gflat = torch.empty(total, dtype=torch.float32, device=dev)
         ws = _ws(lib.dec_tail_workspace(M, L, Lc), dev)
+        Mc = context.shape[0] * Lc
+        wsk = _ws(lib.linear_bwd_weight_workspace(Mc, 2 * E, E), dev)
         s = stream()
+        ng = ctx.needs_input_grad
+        # every parameter gradient is a view of gflat; the full in_proj gradient
+        # too: rows [0, E) from the tail kernel, rows [E, 3E) written in place by
+        # the k|v projection's weight gradient
+        gall = [gflat[o:o + t.numel()].view_as(t) if t is not None else None
+                for t, o in zip(w, offs)]
+        gall[4] = gflat[offs[4]:offs[4] + 3 * E * E].view_as(w[4])
+        gall[5] = gflat[offs[5]:offs[5] + 3 * E]
+        need = [ng[7 + j] for j in range(4)] + [ng[5], ng[6]] + [ng[11 + j] for j in range(12)]
+        gout = [g if n else None for g, n in zip(gall, need)]
+        dfr = _defer.target(ctx.params, gout, (ws, wsk, gflat))
         lib.dec_tail_bwd(x.data_ptr(), O.data_ptr(), kvc.data_ptr(), M, L, Lc, _lib.ptr_array(w),
                          p, ptr(st), cid, y.data_ptr(), dy.data_ptr(), ptr(dqkv), ptr(masks),
                          dx.data_ptr(), dO.data_ptr(), dkvc.data_ptr(), gflat.data_ptr(),
-                         ws.data_ptr(), s)
-        Wc = w[4]
-        Mc = context.shape[0] * Lc
-        # full in_proj gradient: rows [0, E) from the tail, rows [E, 3E) from the k|v proj
-        dWc = torch.empty_like(Wc)
-        dbc = torch.empty_like(w[5])
-        lib.pack(_lib.ptr_array([dWc, dbc]), (C.c_int64 * 2)(offs[4], offs[5]),
-                 (C.c_int64 * 2)(E * E, E), 2, gflat.data_ptr(), 1, s)
-        wsk = _ws(lib.linear_bwd_weight_workspace(Mc, 2 * E, E), dev)
+                         ws.data_ptr(), dfr, s)
+        Wc, dWc, dbc = w[4], gall[4], gall[5]
         lib.linear_bwd_weight(dkvc.data_ptr(), 2 * E, None, 0, 0, context.data_ptr(), E, None, 0,
                               Mc, 2 * E, E, dWc.data_ptr() + 4 * E * E, dbc.data_ptr() + 4 * E, 0,
-                              wsk.data_ptr(), s)
+                              wsk.data_ptr(), dfr, s)
         dctx = torch.empty_like(context)
         lib.linear_bwd_data(dkvc.data_ptr(), 2 * E, None, 0, 0, Mc, 2 * E,
                             Wc.data_ptr() + 4 * E * E, E, dctx.data_ptr(), E, 0, s)
-        ng = ctx.needs_input_grad
-        gw = [gflat[o:o + t.numel()].view_as(t) if (t is not None and ng[7 + j]) else None
-              for j, (t, o) in enumerate(zip(w[:4] + w[6:], offs[:4] + offs[6:]))]
-        return (None, None, dx.view(xshape), dO, dctx, dWc if ng[5] else None,
-                dbc if ng[6] else None, *gw)
+        gw = gout[:4] + gout[6:]
+        return (None, None, dx.view(xshape), dO, dctx, gout[4], gout[5], *gw)
 
 
 # ---------------------------------------------------------------------------
@@ -963,6 +980,8 @@ class EncPreFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, p, x, O, context, Wo1, bo1, g1, be1, Wc, bc):
         _lib.require_device(x, O, context, Wo1, bo1, g1, be1, Wc, bc)
+        ctx.params = (Wo1, bo1, g1, be1, Wc, bc)
+        _defer.count_uses(*ctx.params)
         E = 32
         x, O, context = x.contiguous(), O.contiguous(), context.contiguous()
         w = [t.contiguous() for t in (Wo1, bo1, g1, be1, Wc, bc)]
@@ -1002,23 +1021,22 @@ class EncPreFn(torch.autograd.Function):
         gflat = torch.empty(total, dtype=torch.float32, device=dev)
         s = stream()
         ws = _ws(lib.enc_block_workspace(M), dev)
+        wsk = _ws(lib.linear_bwd_weight_workspace(Mc, 2 * E, E), dev)
+        Wc = w[4]
+        gw = [gflat[o:o + t.numel()].view_as(t) for t, o in zip(w[:4], offs[:4])]
+        dWc = gflat[offs[4]:offs[4] + 3 * E * E].view_as(Wc)
+        dbc = gflat[offs[5]:offs[5] + 3 * E]
+        dfr = _defer.target(ctx.params, gw + [dWc, dbc], (ws, wsk, gflat))
         lib.enc_block_bwd(1, x.data_ptr(), O.data_ptr(), M, _lib.ptr_array(w + [None] * 12),
                           p, ptr(st), cid, x1.data_ptr(), dx1.data_ptr(), dq.data_ptr(),
                           ptr(masks), dx.data_ptr(), dO.data_ptr(), gflat.data_ptr(),
-                          ws.data_ptr(), s)
-        Wc = w[4]
-        dWc = torch.empty_like(Wc)
-        dbc = torch.empty_like(w[5])
-        lib.pack(_lib.ptr_array([dWc, dbc]), (C.c_int64 * 2)(offs[4], offs[5]),
-                 (C.c_int64 * 2)(E * E, E), 2, gflat.data_ptr(), 1, s)
-        wsk = _ws(lib.linear_bwd_weight_workspace(Mc, 2 * E, E), dev)
+                          ws.data_ptr(), dfr, s)
         lib.linear_bwd_weight(dkv.data_ptr(), 2 * E, None, 0, 0, context.data_ptr(), E, None, 0,
                               Mc, 2 * E, E, dWc.data_ptr() + 4 * E * E, dbc.data_ptr() + 4 * E, 0,
-                              wsk.data_ptr(), s)
+                              wsk.data_ptr(), dfr, s)
         dctx = torch.empty_like(context)
         lib.linear_bwd_data(dkv.data_ptr(), 2 * E, None, 0, 0, Mc, 2 * E,
                             Wc.data_ptr() + 4 * E * E, E, dctx.data_ptr(), E, 0, s)
-        gw = [gflat[o:o + t.numel()].view_as(t) for t, o in zip(w[:4], offs[:4])]
         return (None, dx.view(xshape), dO, dctx.view(cshape), *gw, dWc, dbc)
 
 
@@ -1031,6 +1049,8 @@ class EncPostFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, p, x1, c, *w12):
         _lib.require_device(x1, c, *w12)
+        ctx.params = w12
+        _defer.count_uses(*w12)
         E = 32
         x1, c = x1.contiguous(), c.contiguous()
         w = [None if t is None else t.contiguous() for t in w12]
@@ -1068,11 +1088,12 @@ class EncPostFn(torch.autograd.Function):
         offs, total = _tail_layout()
         gflat = torch.empty(total, dtype=torch.float32, device=dev)
         ws = _ws(lib.enc_block_workspace(M), dev)
-        lib.enc_block_bwd(2, x1.data_ptr(), c.data_ptr(), M, _lib.ptr_array([None] * 6 + w),
-                          p, ptr(st), cid, y.data_ptr(), dy.data_ptr(), ptr(dqkv), ptr(masks),
-                          dx1.data_ptr(), dc.data_ptr(), gflat.data_ptr(), ws.data_ptr(),
-                          stream())
         ng = ctx.needs_input_grad
         gw = [gflat[o:o + t.numel()].view_as(t) if (t is not None and ng[3 + j]) else None
               for j, (t, o) in enumerate(zip(w, offs[6:]))]
+        dfr = _defer.target(ctx.params, gw, (ws, gflat))
+        lib.enc_block_bwd(2, x1.data_ptr(), c.data_ptr(), M, _lib.ptr_array([None] * 6 + w),
+                          p, ptr(st), cid, y.data_ptr(), dy.data_ptr(), ptr(dqkv), ptr(masks),
+                          dx1.data_ptr(), dc.data_ptr(), gflat.data_ptr(), ws.data_ptr(), dfr,
+                          stream())
         return (None, dx1.view(xshape), dc, *gw)

@@ -22,8 +22,8 @@ import math
 
 import torch
 
+from . import _defer, guard
 from . import distributed as D
-from . import guard
 from .losses import elbo
 from .optim import FusedAdamW
 
@@ -67,8 +67,10 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
                 if p.requires_grad:
                     p.grad = torch.zeros_like(p)
         else:
-            loss = -loss_fn(network, x)
-            loss.backward()
+            # parameter-gradient sums batched into one launch at the end of backward
+            with _defer.deferred():
+                loss = -loss_fn(network, x)
+                loss.backward()
         if ws > 1 and not isinstance(optimizer, FusedAdamW):
             D.allreduce_grads(network.parameters(), reduction, weight=w)
         optimizer.step()

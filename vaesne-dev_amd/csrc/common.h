@@ -189,4 +189,8 @@ int launch_colsum(const float* P, int G, int F, float* out0, float* out1, int sp
                   hipStream_t s);
 // same over columns [0, F) of rows with stride ld (P[g*ld + f]) -> out[f]
 int launch_colsum_strided(const float* P, int G, int F, int64_t ld, float* out, hipStream_t s);
+// out[f] (+)= sum_g P[g*ld + f], f < F: launched now (defer null) or appended to
+// `defer` for one batched vaesne_colsum_flush (include/vaesne_hip.h)
+int colsum_or_defer(vaesne_colsum_list* defer, const float* P, int64_t ld, int G, int F,
+                    float* out, int accum, hipStream_t s);
 }  // namespace vaesne

@@ -25,7 +25,8 @@
 // Backward: recompute the forward in registers, run the chain in reverse, and
 // accumulate every weight gradient dW = sum_t g_t x_t^T with MFMAs whose
 // contraction runs over the wave's 32 tokens (operands staged in LDS rows).
-// Per-workgroup partials -> fixed-order column sum (bitwise reproducible).
+// Per-workgroup partials -> fixed-order column sums (bitwise reproducible),
+// launched at once or deferred to the backward pass's batched flush.
 // Context (k, v) gradients are per sequence: a workgroup only ever covers
 // tokens of ONE sequence, so they accumulate in the same way.
 #include "common.h"
@@ -70,8 +71,8 @@ struct Tail {
   const float* dqkv;   // [M, 96] (if Wn)
   float* dx;           // [M, 32]
   float* dO;           // [M, 32]
-  float* wpart;        // [G][WPART]
-  float* cpart;        // [chunks][Nseq * Lc * 64]
+  float* wpart;        // [G][WPART] per-workgroup partials (gflat itself when G == 1)
+  float* dkvc;         // [Nseq, Lc, 64] context k | v gradients (written per sequence)
   int mode;            // MODE_FULL (decoder block tail) / MODE_PRE / MODE_POST (encoder halves)
 };
 
@@ -885,10 +886,14 @@ __global__ __launch_bounds__(NT) void enc_post_bwd_data(Tail a, float* __restric
 }
 
 // gradient partial layout per workgroup (floats)
-constexpr int OFF_WO1 = 0, OFF_WQ = 1024, OFF_WO2 = 2048, OFF_W1 = 3072, OFF_W2 = 4096,
-              OFF_WN = 5120, OFF_BO1 = 8192, OFF_BQ = 8224, OFF_BO2 = 8256, OFF_B1 = 8288,
-              OFF_B2 = 8320, OFF_BN = 8352, OFF_G1 = 8448, OFF_BE1 = 8480, OFF_G2 = 8512,
-              OFF_BE2 = 8544, OFF_G3 = 8576, OFF_BE3 = 8608, WPART = 8640;
+// gradient layout (slabs and gflat alike).  The cross in_proj region holds all
+// 3E rows [Wq; Wk; Wv] (and 3E biases): the tail writes rows [0, E), the
+// context k | v projection's weight gradient writes rows [E, 3E) in place, so
+// the whole in_proj gradient is one view of gflat.
+constexpr int OFF_WO1 = 0, OFF_WQ = 1024, OFF_WO2 = 4096, OFF_W1 = 5120, OFF_W2 = 6144,
+              OFF_WN = 7168, OFF_BO1 = 10240, OFF_BQ = 10272, OFF_BO2 = 10368, OFF_B1 = 10400,
+              OFF_B2 = 10432, OFF_BN = 10464, OFF_G1 = 10560, OFF_BE1 = 10592, OFF_G2 = 10624,
+              OFF_BE2 = 10656, OFF_G3 = 10688, OFF_BE3 = 10720, WPART = 10752;
 
 // acc[o][k] += sum_t G[t][o] X[t][k] over the wave's 32 tokens (rows r0..r0+31,
 // rows >= rmax contribute 0); operands read straight from L2 / HBM, all 32 loads
@@ -938,48 +943,44 @@ __global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __rest
   const bool next = a.Wn != nullptr;
   if (!next && job >= J_WN0 && job <= J_WN2) return;
   if (a.mode != MODE_FULL) {
-    // encoder halves: no context gradients; the other half's matrices are zero
+    // encoder halves: no context gradients; the other half's matrices are not
+    // computed (their gflat regions are neither summed nor written)
     if (job == J_K || job == J_V) return;
     const bool mine = a.mode == MODE_PRE ? (job == J_WO1 || job == J_WQ || job == J_LN)
                                          : !(job == J_WO1 || job == J_WQ);
-    if (!mine) {
-      const int mo = job == J_WO1 ? OFF_WO1 : job == J_WQ ? OFF_WQ : job == J_WO2 ? OFF_WO2
-                   : job == J_W1 ? OFF_W1 : job == J_W2 ? OFF_W2 : OFF_WN + 1024 * (job - J_WN0);
-      const int bo = job == J_WO1 ? OFF_BO1 : job == J_WQ ? OFF_BQ : job == J_WO2 ? OFF_BO2
-                   : job == J_W1 ? OFF_B1 : job == J_W2 ? OFF_B2 : OFF_BN + 32 * (job - J_WN0);
-      float* o = a.wpart + (int64_t)blockIdx.x * WPART;
-      for (int i = threadIdx.x; i < 1024; i += NT) o[mo + i] = 0.f;
-      if (threadIdx.x < 32) o[bo + threadIdx.x] = 0.f;
-      return;
-    }
+    if (!mine) return;
   }
   const int chunks = (a.L + a.chunk - 1) / a.chunk;
   const int seq = blockIdx.x / chunks, ch = blockIdx.x % chunks;
+  // context (k, v) gradients are per sequence: the sequence's first workgroup
+  // covers all its chunks and writes dkvc directly (no cross-workgroup sum)
+  const bool ctx_job = job == J_K || job == J_V;
+  if (ctx_job && ch != 0) return;
   const int64_t MS = (int64_t)a.M * E;
-  const float* G = nullptr;
+  const float* Gm = nullptr;
   const float* X = nullptr;
   int ldg = E;
   int boff = -1, moff = -1;
   switch (job) {
-    case J_WO1: G = scr + V_DA1 * MS; X = a.O; moff = OFF_WO1; boff = OFF_BO1; break;
-    case J_WQ: G = scr + V_DQ * MS; X = scr + V_X1 * MS; moff = OFF_WQ; boff = OFF_BQ; break;
+    case J_WO1: Gm = scr + V_DA1 * MS; X = a.O; moff = OFF_WO1; boff = OFF_BO1; break;
+    case J_WQ: Gm = scr + V_DQ * MS; X = scr + V_X1 * MS; moff = OFF_WQ; boff = OFF_BQ; break;
     case J_WO2:   // POST reads c straight from its input (no V_C copy)
-      G = scr + V_DA2 * MS; X = a.mode == MODE_POST ? a.O : scr + V_C * MS;
+      Gm = scr + V_DA2 * MS; X = a.mode == MODE_POST ? a.O : scr + V_C * MS;
       moff = OFF_WO2; boff = OFF_BO2; break;
-    case J_W1: G = scr + V_DF1 * MS; X = scr + V_X2 * MS; moff = OFF_W1; boff = OFF_B1; break;
-    case J_W2: G = scr + V_DF2 * MS; X = scr + V_GL * MS; moff = OFF_W2; boff = OFF_B2; break;
+    case J_W1: Gm = scr + V_DF1 * MS; X = scr + V_X2 * MS; moff = OFF_W1; boff = OFF_B1; break;
+    case J_W2: Gm = scr + V_DF2 * MS; X = scr + V_GL * MS; moff = OFF_W2; boff = OFF_B2; break;
     case J_WN0: case J_WN1: case J_WN2: {
       const int c = job - J_WN0;
-      G = a.dqkv + c * E; ldg = 3 * E; X = a.y; moff = OFF_WN + 1024 * c; boff = OFF_BN + 32 * c;
+      Gm = a.dqkv + c * E; ldg = 3 * E; X = a.y; moff = OFF_WN + 1024 * c; boff = OFF_BN + 32 * c;
       break;
     }
-    case J_K: G = scr + V_Q * MS; X = scr + V_DS * MS; break;
-    case J_V: G = scr + V_DC * MS; X = scr + V_PD * MS; break;
+    case J_K: Gm = scr + V_Q * MS; X = scr + V_DS * MS; break;
+    case J_V: Gm = scr + V_DC * MS; X = scr + V_PD * MS; break;
     default: break;
   }
-  const int t0 = ch * a.chunk, t1 = min(a.L, t0 + a.chunk);
+  const int t0 = ctx_job ? 0 : ch * a.chunk, t1 = ctx_job ? a.L : min(a.L, t0 + a.chunk);
   const int64_t base = (int64_t)seq * a.L, rmax = base + t1;
-  float* out = a.wpart + (int64_t)blockIdx.x * WPART;
+  float* out = a.wpart + (int64_t)blockIdx.x * WPART;   // == gflat when the grid is one workgroup
   if (job == J_LN) {
     const int voff[6] = {V_DLN1X, V_DLN1, V_DLN2X, V_DLN2, V_DLN3X, V_DLN3};
     const int ooff[6] = {OFF_G1, OFF_BE1, OFF_G2, OFF_BE2, OFF_G3, OFF_BE3};
@@ -997,7 +998,7 @@ __global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __rest
       float sum = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) sum += red[i * 256 + w * 64 + c] + red[i * 256 + w * 64 + 32 + c];
-      out[ooff[i] + c] = sum;
+      if (a.mode == MODE_FULL || (a.mode == MODE_PRE) == (i < 2)) out[ooff[i] + c] = sum;
     }
     return;
   }
@@ -1005,21 +1006,20 @@ __global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __rest
   float cs = 0.f;
 #pragma unroll 2
   for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32)
-    cs += wg_tile(G, ldg, X, E, base + tt, rmax, acc, lane);
+    cs += wg_tile(Gm, ldg, X, E, base + tt, rmax, acc, lane);
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[wave * 1024 + F(r, h) * 32 + (lane & 31)] = acc[r];
   __syncthreads();
-  if (job == J_K || job == J_V) {
+  if (ctx_job) {
     // acc[f = F(r,h)][j' = lane&31] is valid where (j' & 3) == f >> 3, j = j' >> 2 < Lc
-    const int nseq = a.M / a.L;
-    float* cp = a.cpart + ((int64_t)ch * nseq + seq) * a.Lc * 2 * E + (job == J_V ? E : 0);
+    float* dk = a.dkvc + (int64_t)seq * a.Lc * 2 * E + (job == J_V ? E : 0);
     for (int i = threadIdx.x; i < a.Lc * E; i += NT) {
       const int j = i / E, f = i % E;
       const int idx = f * 32 + 4 * j + (f >> 3);
       float sum = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) sum += red[w * 1024 + idx];
-      cp[j * 2 * E + f] = sum;
+      dk[j * 2 * E + f] = sum;
     }
     return;
   }
@@ -1034,6 +1034,37 @@ __global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __rest
     for (int w = 0; w < NW; ++w) sum += red[w * 64 + threadIdx.x] + red[w * 64 + 32 + threadIdx.x];
     out[boff + threadIdx.x] = sum;
   }
+}
+
+// column ranges of the gradient layout a mode produces (the k | v rows of the
+// cross in_proj are excluded: the caller's projection gradient owns them)
+int tail_ranges(int mode, int (&r)[3][2]) {
+  if (mode == MODE_PRE) {
+    r[0][0] = OFF_WO1; r[0][1] = OFF_WQ + 1024;
+    r[1][0] = OFF_BO1; r[1][1] = OFF_BQ + 32;
+    r[2][0] = OFF_G1;  r[2][1] = OFF_G1 + 64;
+  } else if (mode == MODE_POST) {
+    r[0][0] = OFF_WO2; r[0][1] = OFF_BO1;
+    r[1][0] = OFF_BO2; r[1][1] = OFF_G1;
+    r[2][0] = OFF_G2;  r[2][1] = WPART;
+  } else {
+    r[0][0] = 0;       r[0][1] = OFF_WQ + 1024;
+    r[1][0] = OFF_WO2; r[1][1] = OFF_BQ + 32;
+    r[2][0] = OFF_BO2; r[2][1] = WPART;
+  }
+  return 3;
+}
+
+int sum_tail(int mode, const float* wpart, int G, float* gflat, vaesne_colsum_list* defer,
+             hipStream_t s) {
+  int r[3][2];
+  const int n = tail_ranges(mode, r);
+  for (int k = 0; k < n; ++k) {
+    const int rc = colsum_or_defer(defer, wpart + r[k][0], WPART, G, r[k][1] - r[k][0],
+                                   gflat + r[k][0], 0, s);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 template <int LC, bool NEXT, bool DROP>
@@ -1094,8 +1125,7 @@ VAESNE_API int64_t vaesne_dec_tail_workspace(int M, int L, int Lc) {
   const int chunk = L <= 256 ? ((L + 127) / 128) * 128 : 512;
   const int chunks = (L + chunk - 1) / chunk;
   const int64_t G = (int64_t)(M / L) * chunks;
-  return (G * WPART + (int64_t)chunks * (M / L) * Lc * 2 * E + (int64_t)NVEC * M * E) *
-         (int64_t)sizeof(float);
+  return (G * WPART + (int64_t)NVEC * M * E) * (int64_t)sizeof(float);
 }
 
 VAESNE_API int vaesne_dec_tail_fwd(const float* x, const float* O, const float* kvc, int M, int L,
@@ -1111,14 +1141,14 @@ VAESNE_API int vaesne_dec_tail_fwd(const float* x, const float* O, const float* 
   return dispatch<true>(a, grid, nullptr, (hipStream_t)stream);
 }
 
-// gflat [8640]: every parameter gradient of the block in the layout of the
-// per-workgroup partials (see include/vaesne_hip.h); dkvc [Nseq, Lc, 64].
+// gflat [WPART]: every parameter gradient of the block in the layout of the
+// per-workgroup slabs (see include/vaesne_hip.h); dkvc [Nseq, Lc, 64].
 VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* kvc, int M, int L,
                                    int Lc, const float* const* w, float p_drop,
                                    const int64_t* rng, uint32_t call_id, const float* y,
                                    const float* dy, const float* dqkv, const uint32_t* drop_masks,
                                    float* dx, float* dO, float* dkvc, float* gflat,
-                                   float* workspace, void* stream) {
+                                   float* workspace, vaesne_colsum_list* defer, void* stream) {
   if (!shapes_ok(M, L, Lc)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   Tail a = make(x, O, kvc, M, L, Lc, w, p_drop, rng, call_id);
@@ -1128,17 +1158,13 @@ VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* 
   const int chunks = (L + a.chunk - 1) / a.chunk;
   const int grid = (M / L) * chunks;
   a.y = const_cast<float*>(y);
-  a.wpart = workspace;
-  a.cpart = workspace + (int64_t)grid * WPART;
-  float* scr = a.cpart + (int64_t)chunks * (M / L) * Lc * 2 * E;
-  int rc = dispatch<false>(a, grid, scr, s);
-  if (rc) return rc;
-  // fixed-order sums of the per-workgroup partials: all parameters in one pass
-  rc = launch_colsum(workspace, grid, WPART, gflat, nullptr, WPART, 0, s);
-  if (rc) return rc;
-  // context grads: sum over chunks -> dkvc [Nseq * Lc * 64]
-  return launch_colsum(a.cpart, chunks, (M / L) * Lc * 2 * E, dkvc, nullptr,
-                       (M / L) * Lc * 2 * E, 0, s);
+  a.dkvc = dkvc;
+  // one workgroup: its slab IS the gradient (no column sum)
+  a.wpart = grid == 1 ? gflat : workspace;
+  float* scr = workspace + (int64_t)grid * WPART;
+  const int rc = dispatch<false>(a, grid, scr, s);
+  if (rc || grid == 1) return rc;
+  return sum_tail(MODE_FULL, workspace, grid, gflat, defer, s);
 }
 
 VAESNE_API int64_t vaesne_enc_block_workspace(int M) {
@@ -1178,7 +1204,7 @@ VAESNE_API int vaesne_enc_block_bwd(int mode, const float* x, const float* O, in
                                     uint32_t call_id, const float* y, const float* dy,
                                     const float* dq_or_dqkv, const uint32_t* drop_masks,
                                     float* dx, float* dO, float* gflat, float* workspace,
-                                    void* stream) {
+                                    vaesne_colsum_list* defer, void* stream) {
   if (M <= 0 || (mode != MODE_PRE && mode != MODE_POST)) return (int)hipErrorInvalidValue;
   if (p_drop > 0.f && !drop_masks) return (int)hipErrorInvalidValue;
   Tail a = make(x, O, nullptr, M, M, 1, w, p_drop, rng, call_id);
@@ -1188,9 +1214,8 @@ VAESNE_API int vaesne_enc_block_bwd(int mode, const float* x, const float* O, in
   a.y = const_cast<float*>(y);
   if (!dq_or_dqkv && (mode == MODE_PRE || a.Wn)) return (int)hipErrorInvalidValue;
   const int grid = (M + a.chunk - 1) / a.chunk;
-  a.wpart = workspace;
-  a.cpart = workspace + (int64_t)grid * WPART;
-  float* scr = a.cpart + (int64_t)grid * 2 * E;   // vaesne_dec_tail_workspace(M, M, 1) layout
+  a.wpart = grid == 1 ? gflat : workspace;
+  float* scr = workspace + (int64_t)grid * WPART;   // vaesne_dec_tail_workspace(M, M, 1) layout
   hipStream_t s = (hipStream_t)stream;
   const bool drop = p_drop > 0.f, next = a.Wn != nullptr;
   if (mode == MODE_PRE) {
@@ -1206,7 +1231,8 @@ VAESNE_API int vaesne_enc_block_bwd(int mode, const float* x, const float* O, in
   VAESNE_CHECK_LAUNCH();
   hipLaunchKernelGGL(dec_tail_wgrad, dim3(grid, NJOB), dim3(NT), 0, s, a, (const float*)scr);
   VAESNE_CHECK_LAUNCH();
-  return launch_colsum(workspace, grid, WPART, gflat, nullptr, WPART, 0, s);
+  if (grid == 1) return 0;
+  return sum_tail(mode, workspace, grid, gflat, defer, s);
 }
 
 VAESNE_API int vaesne_dec_tail_grad_layout(int* offsets) {

@@ -314,7 +314,8 @@ VAESNE_API int64_t vaesne_embed_bwd_workspace(int64_t rows, int E, int nb) {
 
 VAESNE_API int vaesne_embed_bwd(const int64_t* idx, int64_t period, int64_t rows,
                                 const float* dout, int64_t lddo, int E, int nb, float* dtable,
-                                int accum, float* workspace, void* stream) {
+                                int accum, float* workspace, vaesne_colsum_list* defer,
+                                void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (E > NT || nb > 16 || nb < 1) return (int)hipErrorInvalidValue;
   int groups = NT / E;
@@ -331,7 +332,7 @@ VAESNE_API int vaesne_embed_bwd(const int64_t* idx, int64_t period, int64_t rows
     hipLaunchKernelGGL(embed_bwd_kernel<16>, dim3(G), dim3(NT), 0, s, idx, period, rows, dout,
                        lddo, E, nb, workspace);
   VAESNE_CHECK_LAUNCH();
-  return launch_colsum(workspace, G, nb * E, dtable, nullptr, nb * E, accum, s);
+  return colsum_or_defer(defer, workspace, (int64_t)nb * E, G, nb * E, dtable, accum, s);
 }
 
 // out[f] (+)= sum_g in[g*F + f]  (gradient of a broadcast / repeat over G)

@@ -204,7 +204,8 @@ VAESNE_API int vaesne_add_ln_bwd(const float* dy, int64_t lddy, const float* x, 
                                  float p_drop, const int64_t* rng_state, uint32_t call_id,
                                  float* dx, int64_t lddx, int accum_dx, float* dres,
                                  int64_t lddres, int accum_dres, float* dgamma, float* dbeta,
-                                 int accum_param, float* workspace, void* stream) {
+                                 int accum_param, float* workspace, vaesne_colsum_list* defer,
+                                 void* stream) {
   hipStream_t s = (hipStream_t)stream;
   int G = ln_grid(M);
   if (M <= 0) {
@@ -223,7 +224,9 @@ VAESNE_API int vaesne_add_ln_bwd(const float* dy, int64_t lddy, const float* x, 
     return (int)hipErrorInvalidValue;
   }
   VAESNE_CHECK_LAUNCH();
-  return launch_colsum(workspace, G, 2 * E, dgamma, dbeta, E, accum_param, s);
+  if (!defer) return launch_colsum(workspace, G, 2 * E, dgamma, dbeta, E, accum_param, s);
+  const int rc = colsum_or_defer(defer, workspace, 2 * E, G, E, dgamma, accum_param, s);
+  return rc ? rc : colsum_or_defer(defer, workspace + E, 2 * E, G, E, dbeta, accum_param, s);
 }
 
 // generic fixed-order partial-sum reduction (used by the host for other

@@ -359,7 +359,8 @@ VAESNE_API int64_t vaesne_linear_bwd_weight_workspace(int64_t M, int O, int I) {
 VAESNE_API int vaesne_linear_bwd_weight(const float* dy, int64_t lddy, const float* z, int64_t ldz,
                                         int act, const float* x, int64_t ldx, const float* x2,
                                         int64_t ldx2, int64_t M, int O, int I, float* dW,
-                                        float* db, int accum, float* workspace, void* stream) {
+                                        float* db, int accum, float* workspace,
+                                        vaesne_colsum_list* defer, void* stream) {
   if (O < 1 || O > MAXN || I < 1 || I > MAXK) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int F = O * I + O;
@@ -382,5 +383,7 @@ VAESNE_API int vaesne_linear_bwd_weight(const float* dy, int64_t lddy, const flo
     VAESNE_CHECK_LAUNCH();
     if (G == 1) return 0;   // written directly
   }
-  return launch_colsum(workspace, G, F, dW, db, O * I, accum, s);
+  if (!defer) return launch_colsum(workspace, G, F, dW, db, O * I, accum, s);
+  const int rc = colsum_or_defer(defer, workspace, F, G, O * I, dW, accum, s);
+  return rc ? rc : colsum_or_defer(defer, workspace + (int64_t)O * I, F, G, O, db, accum, s);
 }
