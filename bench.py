@@ -109,6 +109,12 @@ class Step:
         with deferred():   # parameter-gradient sums: one batched launch at the end of backward
             loss = -self.loss_fn(self.model, self.x)
             loss.backward()
+        # the VAEs keep their last posterior parameters (the reference's `_qz_x_params`),
+        # which would keep this step's autograd graph -- and its AccumulateGrad nodes,
+        # bound to this step's stream -- alive into the next (captured) step
+        for m in self.model.modules():
+            if getattr(m, "_qz_x_params", None) is not None:
+                m._qz_x_params = None
         self.opt.pack_grads()
         self.loss.copy_(loss.detach())
 

@@ -245,6 +245,11 @@ int vaesne_embed_bwd(const int64_t* idx, int64_t period, int64_t rows, const flo
 /* out[f] (+)= sum_g in[g*F+f]: backward of x.repeat(B,1,1) (initbottleneck,
  * PhotometricLayers.py:137-138, SpectraLayers.py:134-135) */
 int vaesne_sum_leading(const float* in, int G, int F, float* out, int accum, void* stream);
+/* out = srcs[0] + srcs[1] + ... + srcs[n-1] (n <= 16, fixed order): the
+ * gradient of an activation several ops read (the encoders' data tokens read by every
+ * block, a decoder input read by its first block and its head), one launch instead of
+ * autograd's n - 1 pairwise adds. */
+int vaesne_sum_n(const float* const* srcs, int n, int64_t numel, float* out, void* stream);
 
 /* ---- posterior, sampler, likelihood scale --------------------------------- */
 /* mu = b[:, :Lz], scale = softplus(b[:, Lz:])  PhotometricVAE.py:53-54, SpectraVAE.py:48-49.

@@ -107,9 +107,10 @@ def test_accumulating_and_shared_parameters_fall_back():
     with _defer.deferred():
         (lin(x).square().sum() + lin(2 * x).sum()).backward()   # the weight used twice
     xd = x.double().cpu()
-    ref_y = torch.nn.functional.linear(xd, lin.weight.double().cpu(), lin.bias.double().cpu())
+    ref_y = torch.nn.functional.linear(xd, lin.weight.detach().double().cpu(),
+                                       lin.bias.detach().double().cpu())
     gw = 2 * ref_y.T @ xd + torch.ones(5000, 32, dtype=torch.float64).T @ (2 * xd)
-    assert float((lin.weight.grad.double().cpu() - gw).abs().max() / gw.abs().max()) < 1e-5
+    assert float((lin.weight.grad.detach().double().cpu() - gw).abs().max() / gw.abs().max()) < 1e-5
 
 
 def test_parameter_also_used_by_a_torch_op_raises():

@@ -470,7 +470,10 @@ def test_fused_encoder_stack_matches_per_op(selfattn, B, T, Lc):
             for blk in blocks:
                 out = blk(out, cc, context_mask=mask)
         (out * go).sum().backward()
-        res.append([out, xx.grad, cc.grad] + [p.grad.clone() for p in blocks.parameters()])
+        # detached: the fused pass's graph (AccumulateGrad nodes bound to the context
+        # side streams) must not outlive it into the one-stream per-op pass
+        res.append([out.detach(), xx.grad, cc.grad] + [p.grad.clone() for p in blocks.parameters()])
+        del out
     names = ["out", "dx", "dcontext"] + [n for n, _ in blocks.named_parameters()]
     for n, a, b in zip(names, *res):
         assert _rel(a, b) < 2e-5, n

@@ -35,10 +35,11 @@ class photometricTransformerDecoder(nn.Module):
             mask = None
         # x = time_embd + band_embd (PhotometricLayers.py:62-64), the add fused in the gather
         x = _ops.embedding(band, self.bandembd.weight, base=self.sinusoidal_time_embd(time))
-        h = x
+        # x feeds the first block twice and the head: one gradient sum (_ops.fanout)
+        x_res, x_qkv, x_out = _ops.fanout(x, 3)
         bottleneck = self.contextfc(bottleneck)
-        h = decoder_stack(self.transformerblocks, h, bottleneck, mask)
-        return self.get_photo(x, h).squeeze(-1)   # get_photo(x + h)
+        h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, x_qkv=x_qkv)
+        return self.get_photo(x_out, h).squeeze(-1)   # get_photo(x + h)
 
 
 class photometricTransformerEncoder(nn.Module):
@@ -75,5 +76,6 @@ class photometricTransformerEncoder(nn.Module):
             tok = _ops.embedding(band, self.bandembd.weight,
                                  base=self.fluxfc(flux[:, :, None], base=self.time_embd(time)))
         x = _ops.repeat_batch(self.initbottleneck, flux.shape[0])
-        h = encoder_stack(self.transformerblocks, x, tok, context_mask=mask)
-        return self.bottleneckfc(x, h)   # bottleneckfc(x + h)
+        x_res, x_qkv, x_out = _ops.fanout(x, 3)
+        h = encoder_stack(self.transformerblocks, x_res, tok, context_mask=mask, x_qkv=x_qkv)
+        return self.bottleneckfc(x_out, h)   # bottleneckfc(x + h)

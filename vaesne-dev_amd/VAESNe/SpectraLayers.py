@@ -33,11 +33,12 @@ class spectraTransformerDecoder(nn.Module):
     def forward(self, wavelength, phase, bottleneck, mask=None):
         x = self.wavelength_embd_layer(wavelength)
         phase_embd = self.phase_embd_layer(phase[:, None])
-        h = x
+        # x feeds the first block twice and the head: one gradient sum (_ops.fanout)
+        x_res, x_qkv, x_out = _ops.fanout(x, 3)
         bottleneck = torch.cat([self.contextfc(bottleneck), phase_embd], dim=1)
         keep = self.__dict__.pop("_keep_prefetch", None)   # util_layers.prefetch_decoder_dropout
-        h = decoder_stack(self.transformerblocks, h, bottleneck, mask, keep=keep)
-        return self.get_flux(x, h).squeeze(-1)   # get_flux(x + h)
+        h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, keep=keep, x_qkv=x_qkv)
+        return self.get_flux(x_out, h).squeeze(-1)   # get_flux(x + h)
 
 
 class spectraTransformerEncoder(nn.Module):
@@ -78,5 +79,6 @@ class spectraTransformerEncoder(nn.Module):
             mask = torch.cat([mask, torch.zeros(mask.shape[0], 1, dtype=mask.dtype,
                                                 device=mask.device)], dim=1)
         x = _ops.repeat_batch(self.initbottleneck, context.shape[0])
-        h = encoder_stack(self.transformerblocks, x, context, context_mask=mask)
-        return self.bottleneckfc(x, h)   # bottleneckfc(x + h)
+        x_res, x_qkv, x_out = _ops.fanout(x, 3)
+        h = encoder_stack(self.transformerblocks, x_res, context, context_mask=mask, x_qkv=x_qkv)
+        return self.bottleneckfc(x_out, h)   # bottleneckfc(x + h)

@@ -65,6 +65,7 @@ SIGNATURES = {
     "vaesne_embed_bwd_workspace": (I64, [I64, I32, I32]),
     "vaesne_embed_bwd": (I32, [P, I64, I64, P, I64, I32, I32, P, I32, P, P, P]),
     "vaesne_sum_leading": (I32, [P, I32, I32, P, I32, P]),
+    "vaesne_sum_n": (I32, [PP, I32, I64, P, P]),
     "vaesne_latent_head_fwd": (I32, [P, I32, I32, P, P, P, P]),
     "vaesne_latent_head_bwd": (I32, [P, I32, I32, P, P, P, P]),
     "vaesne_uniform": (I32, [P, I64, P, U32, P]),

@@ -514,6 +514,35 @@ def repeat_batch(p, B):
     return RepeatFn.apply(p, int(B))
 
 
+class FanoutFn(torch.autograd.Function):
+    """n aliases of x for n consumers; the backward sums their gradients in ONE
+    launch (vaesne_sum_n) instead of autograd's n - 1 pairwise adds."""
+
+    @staticmethod
+    def forward(ctx, x, n):
+        ctx.n = n
+        return tuple(x.view_as(x) for _ in range(n))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        gs = [g.contiguous() for g in gs if g is not None]
+        if not gs:
+            return None, None
+        if len(gs) == 1:
+            return gs[0], None
+        out = torch.empty_like(gs[0])
+        lib.sum_n(_lib.ptr_array(gs), len(gs), out.numel(), out.data_ptr(), stream())
+        return out, None
+
+
+def fanout(x, n):
+    """n aliases of x whose gradients are summed by one kernel (x itself n times when
+    no gradient flows)."""
+    if n <= 1 or not (x.requires_grad and torch.is_grad_enabled()):
+        return (x,) * n
+    return FanoutFn.apply(x, int(n))
+
+
 # ---------------------------------------------------------------------------
 # posterior head, sampler, likelihood scale
 # ---------------------------------------------------------------------------

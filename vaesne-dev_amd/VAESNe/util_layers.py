@@ -237,13 +237,15 @@ def prefetch_decoder_dropout(decoder, N, L, device):
     decoder._keep_prefetch = keep
 
 
-def decoder_stack(blocks, x, context, mask=None, keep=None):
+def decoder_stack(blocks, x, context, mask=None, keep=None, x_qkv=None):
     """`for blk in blocks: x = blk(x, context, mask=mask)` for the decoders
     (SpectraLayers.py:61-62, PhotometricLayers.py:66-67).  With the reference's
     decoder shape (E 32, 4 heads, ff 32, no context self-attention) each block
     runs as: masked self-attention kernel -> ONE fused tail kernel (out_proj,
     LN1, cross-attention over the context tokens, LN2, FFN, LN3, and the next
-    block's in_proj).  Other shapes take the per-op path (TransformerBlock)."""
+    block's in_proj).  Other shapes take the per-op path (TransformerBlock).
+    `x_qkv` (optional): an alias of x (_ops.fanout) the first in-projection reads,
+    so the caller's single gradient sum for x covers that use too."""
     blocks = list(blocks)
     if not blocks or not all(_fusable_decoder_block(b) for b in blocks) or x.dim() != 3 \
             or context.shape[1] > 8:
@@ -253,7 +255,9 @@ def decoder_stack(blocks, x, context, mask=None, keep=None):
     E = 32
     L = x.shape[1]
     b0 = blocks[0].self_attn
-    qkv = _ops.linear(x, b0.in_proj_weight, b0.in_proj_bias)
+    qkv = _ops.linear(x if x_qkv is None else x_qkv, b0.in_proj_weight, b0.in_proj_bias)
+    # every block's cross-attention reads the context: one gradient sum for all
+    ctxs = _ops.fanout(context, len(blocks))
     kbias = _ops.key_bias(mask)          # one mask conversion for all layers
     N = x.shape[0]
     if keep is not None and (len(keep) != len(blocks) or any(
@@ -267,7 +271,7 @@ def decoder_stack(blocks, x, context, mask=None, keep=None):
                                 keep=None if keep is None else keep[i])
         nxt = blocks[i + 1].self_attn if i + 1 < len(blocks) else None
         x, qkv = _ops.DecTailFn.apply(
-            L, p, x, O, context, blk.cross_attn.in_proj_weight, blk.cross_attn.in_proj_bias,
+            L, p, x, O, ctxs[i], blk.cross_attn.in_proj_weight, blk.cross_attn.in_proj_bias,
             blk.self_attn.out_proj.weight, blk.self_attn.out_proj.bias,
             blk.layernorm1.weight, blk.layernorm1.bias,
             blk.cross_attn.out_proj.weight, blk.cross_attn.out_proj.bias,
@@ -303,7 +307,7 @@ def _fusable_encoder_block(blk):
             and all(ln.eps == 1e-5 for ln in (blk.layernorm1, blk.layernorm2, blk.layernorm3)))
 
 
-def encoder_stack(blocks, x, context, context_mask=None):
+def encoder_stack(blocks, x, context, context_mask=None, x_qkv=None):
     """`for blk in blocks: x = blk(x, context, context_mask=context_mask)` for the
     encoders (SpectraLayers.py:135-136, PhotometricLayers.py:141-143: unmasked
     latent tokens x, the ORIGINAL data tokens as every block's context).  With the
@@ -317,10 +321,15 @@ def encoder_stack(blocks, x, context, context_mask=None):
             x = blk(x, context, context_mask=context_mask)
         return x
     b0 = blocks[0].self_attn
+    # every block reads the ORIGINAL context (twice with a context self-attention:
+    # its in-projection and its residual): aliases whose gradients one kernel sums
+    uses = [2 if b.context_self_attn is not None else 1 for b in blocks]
+    cal = iter(_ops.fanout(context, sum(uses)))
+    cuse = [[next(cal) for _ in range(u)] for u in uses]
     # The context self-attention of every block reads the ORIGINAL context, so the
     # blocks' context paths are independent of each other and of the latent chain:
     # they run ahead on their own stream, one event per block for the join.
-    ctxs = [context] * len(blocks)
+    ctxs = [cu[0] for cu in cuse]
     if any(b.context_self_attn is not None for b in blocks):
         main = torch.cuda.current_stream() if _ctx_stream(context) is not None else None
         kb = _ops.key_bias_of(context_mask)     # built on the main stream, shared by all paths
@@ -336,12 +345,12 @@ def encoder_stack(blocks, x, context, context_mask=None):
                 # caching allocator never hands their memory to the producer stream while
                 # the consumer may still read it (the B=16 step read a reused block as
                 # block i's context in the k|v weight gradient without this)
-                _ops.used_on(cs, context, kb)
+                _ops.used_on(cs, context, *cuse[i], kb)
             p = blk.dropout.p if blk.training else 0.0
+            c_in, c_res = cuse[i]
             with torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext():
-                c, _ = blk.context_self_attn(context, context, context,
-                                             key_padding_mask=context_mask)
-                ctxs[i] = _ops.add_layernorm(context, c, blk.layernorm_context, p)
+                c, _ = blk.context_self_attn(c_in, c_in, c_in, key_padding_mask=context_mask)
+                ctxs[i] = _ops.add_layernorm(c_res, c, blk.layernorm_context, p)
                 if cs is not None:
                     ev = torch.cuda.Event()
                     ev.record(cs)
@@ -351,7 +360,7 @@ def encoder_stack(blocks, x, context, context_mask=None):
                     evs.append(None)
     else:
         evs = [None] * len(blocks)
-    qkv = _ops.linear(x, b0.in_proj_weight, b0.in_proj_bias)
+    qkv = _ops.linear(x if x_qkv is None else x_qkv, b0.in_proj_weight, b0.in_proj_bias)
     for i, blk in enumerate(blocks):
         p = blk.dropout.p if blk.training else 0.0
         pa = blk.self_attn.dropout if blk.training else 0.0

@@ -262,6 +262,32 @@ __global__ void incr_kernel(float* step, int64_t* rng_state) {
   if (rng_state) rng_state[1] += 1;
 }
 
+// out = g0 + g1 + ... (fixed order): the gradient of a tensor several ops read
+constexpr int SUM_MAX = 16;
+struct SumArgs {
+  const float* src[SUM_MAX];
+  int n;
+};
+template <bool VEC>
+__global__ void sum_n_kernel(SumArgs a, int64_t numel, float* __restrict__ out) {
+  const int64_t n4 = VEC ? numel / 4 : 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float4 s = reinterpret_cast<const float4*>(a.src[0])[i];
+    for (int k = 1; k < a.n; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(a.src[k])[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = s;
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < numel;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s = a.src[0][i];
+    for (int k = 1; k < a.n; ++k) s += a.src[k][i];
+    out[i] = s;
+  }
+}
+
 constexpr int PACK_MAX = 48;
 struct PackArgs {
   const float* src[PACK_MAX];
@@ -339,6 +365,28 @@ VAESNE_API int vaesne_embed_bwd(const int64_t* idx, int64_t period, int64_t rows
 VAESNE_API int vaesne_sum_leading(const float* in, int G, int F, float* out, int accum,
                                   void* stream) {
   return launch_colsum(in, G, F, out, nullptr, F, accum, (hipStream_t)stream);
+}
+
+VAESNE_API int vaesne_sum_n(const float* const* srcs, int n, int64_t numel, float* out,
+                            void* stream) {
+  if (n < 1 || n > SUM_MAX) return (int)hipErrorInvalidValue;
+  if (numel <= 0) return 0;
+  SumArgs a{};
+  a.n = n;
+  bool vec = ((uintptr_t)out & 15u) == 0;
+  for (int k = 0; k < n; ++k) {
+    if (!srcs[k]) return (int)hipErrorInvalidValue;
+    a.src[k] = srcs[k];
+    vec = vec && ((uintptr_t)srcs[k] & 15u) == 0;
+  }
+  if (vec)
+    hipLaunchKernelGGL(sum_n_kernel<true>, dim3(blocks_for((numel + 3) / 4, NT, 4096)), dim3(NT),
+                       0, (hipStream_t)stream, a, numel, out);
+  else
+    hipLaunchKernelGGL(sum_n_kernel<false>, dim3(blocks_for(numel, NT, 4096)), dim3(NT), 0,
+                       (hipStream_t)stream, a, numel, out);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
 }
 
 VAESNE_API int vaesne_latent_head_fwd(const float* bott, int B, int n, float* mu, float* scale,
