@@ -351,7 +351,13 @@ int vaesne_infonce_bwd(const float* nz, const float* nrm, const float* lse, int 
  * vaesne_step_advance (which also advances rng_state[1]), so the whole step can
  * be captured in a hipGraph. */
 int vaesne_adamw(float* p, const float* g, float* m, float* v, int64_t n, const float* step,
-                 float lr, float b1, float b2, float eps, float wd, void* stream);
+                 const int32_t* pidx, float lr, float b1, float b2, float eps, float wd,
+                 void* stream);
+/* per-parameter step counts (torch.optim.AdamW's state['step']): pidx [n] maps each
+ * element to its parameter and step[pidx[t]] is that parameter's count (pidx null: one
+ * count step[0] for all).  steps[i] += 1 for the parameters that have a gradient this
+ * step (active[i] != 0; active null: all). */
+int vaesne_adamw_steps_advance(float* steps, const uint8_t* active, int P, void* stream);
 int vaesne_step_advance(float* step, int64_t* rng_state, void* stream);
 /* gather (unpack=0) / scatter (unpack=1) `count` tensors to/from a flat buffer */
 int vaesne_pack(const float* const* srcs, const int64_t* offs, const int64_t* ns, int count,

@@ -5,9 +5,12 @@ flat fp32 parameter buffer on the device.
 * Parameters are re-bound as views into one flat buffer (module identity and
   state_dict keys unchanged), so the update is ONE HIP kernel launch and the
   gradient is ONE flat buffer — the unit the data-parallel all-reduce moves.
-* The step counter lives on the device, so a whole training step (forward,
+* The step counters live on the device, so a whole training step (forward,
   backward, pack, all-reduce, update) can be captured in one hipGraph.
-* Parameters whose .grad is None are skipped, as torch.optim.AdamW does.
+* As in torch.optim.AdamW, every parameter has its own step count, advanced only
+  when it has a gradient, and parameters whose .grad is None are skipped.
+* state_dict() / load_state_dict() use torch.optim.AdamW's format (per-parameter
+  "step", "exp_avg", "exp_avg_sq"), so checkpoints move between the two.
 """
 from __future__ import annotations
 
@@ -46,10 +49,13 @@ class FusedAdamW(torch.optim.Optimizer):
                     offs.append(o)
                     ns.append(p.numel())
                     o += p.numel()
+            pidx = torch.repeat_interleave(torch.arange(len(ps), dtype=torch.int32),
+                                           torch.tensor(ns, dtype=torch.int64)).to(dev)
             self._flat.append(dict(
                 params=ps, flat=flat, grad=torch.zeros_like(flat), m=torch.zeros_like(flat),
-                v=torch.zeros_like(flat), step=torch.zeros(1, dtype=torch.float32, device=dev),
-                offs=(C.c_int64 * len(ps))(*offs), ns=(C.c_int64 * len(ps))(*ns)))
+                v=torch.zeros_like(flat),
+                steps=torch.zeros(len(ps), dtype=torch.float32, device=dev), pidx=pidx,
+                active={}, offs=(C.c_int64 * len(ps))(*offs), ns=(C.c_int64 * len(ps))(*ns)))
 
     def flat_params(self, group=0):
         return self._flat[group]["flat"]
@@ -91,13 +97,81 @@ class FusedAdamW(torch.optim.Optimizer):
             if fl is None:
                 continue
             b1, b2 = group["betas"]
-            lib.step_advance(fl["step"].data_ptr(), None, stream())
+            lib.adamw_steps_advance(fl["steps"].data_ptr(), self._active(fl), len(fl["params"]),
+                                    stream())
             runs = self._runs(fl)
             for o, n in runs:
                 lib.adamw(fl["flat"].data_ptr() + 4 * o, fl["grad"].data_ptr() + 4 * o,
                           fl["m"].data_ptr() + 4 * o, fl["v"].data_ptr() + 4 * o, n,
-                          fl["step"].data_ptr(), float(group["lr"]), float(b1), float(b2),
+                          fl["steps"].data_ptr(), fl["pidx"].data_ptr() + 4 * o,
+                          float(group["lr"]), float(b1), float(b2),
                           float(group["eps"]), float(group["weight_decay"]), stream())
+
+    @staticmethod
+    def _active(fl):
+        """Device mask of the parameters with a gradient (None: all), cached per pattern;
+        built from pinned memory so a graph capture can record the copy."""
+        flags = tuple(p.grad is not None for p in fl["params"])
+        if all(flags):
+            return None
+        t = fl["active"].get(flags)
+        if t is None:
+            host = torch.tensor(flags, dtype=torch.uint8).pin_memory()
+            t = (host, host.to(fl["steps"].device, non_blocking=True))
+            fl["active"][flags] = t
+        return t[1].data_ptr()
+
+    # ---- torch.optim.AdamW-format state --------------------------------------
+    def state_dict(self):
+        state, groups, base = {}, [], 0
+        for group, fl in zip(self.param_groups, self._flat):
+            g = {k: v for k, v in group.items() if k != "params"}
+            g["params"] = list(range(base, base + len(group["params"])))
+            groups.append(g)
+            if fl is not None:
+                steps = fl["steps"].cpu()
+                index = {id(p): i for i, p in enumerate(group["params"])}
+                for j, (p, o, n) in enumerate(zip(fl["params"], fl["offs"], fl["ns"])):
+                    if float(steps[j]) == 0.0:
+                        continue        # never updated: no state, as in torch
+                    state[base + index[id(p)]] = {
+                        "step": steps[j].clone(),
+                        "exp_avg": fl["m"][o:o + n].view_as(p).clone(),
+                        "exp_avg_sq": fl["v"][o:o + n].view_as(p).clone()}
+            base += len(group["params"])
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, state_dict):
+        groups = state_dict["param_groups"]
+        if len(groups) != len(self.param_groups):
+            raise ValueError("loaded state dict has a different number of parameter groups")
+        st = state_dict["state"]
+        for group, saved, fl in zip(self.param_groups, groups, self._flat):
+            if len(saved["params"]) != len(group["params"]):
+                raise ValueError("loaded state dict contains a parameter group that doesn't "
+                                 "match the size of optimizer's group")
+            for k, v in saved.items():
+                if k != "params":
+                    group[k] = v
+            if fl is None:
+                continue
+            where = {id(p): j for j, p in enumerate(fl["params"])}
+            steps = torch.zeros(len(fl["params"]), dtype=torch.float32)
+            with torch.no_grad():
+                for p, key in zip(group["params"], saved["params"]):
+                    j = where.get(id(p))
+                    if j is None:
+                        continue
+                    o, n = fl["offs"][j], fl["ns"][j]
+                    s = st.get(key, st.get(str(key)))
+                    if s is None:
+                        fl["m"][o:o + n].zero_()
+                        fl["v"][o:o + n].zero_()
+                        continue
+                    steps[j] = float(s["step"])
+                    fl["m"][o:o + n].copy_(s["exp_avg"].reshape(-1))
+                    fl["v"][o:o + n].copy_(s["exp_avg_sq"].reshape(-1))
+            fl["steps"].copy_(steps)
 
     @staticmethod
     def _runs(fl):

@@ -174,17 +174,28 @@ __global__ void mask_scale_kernel(const uint8_t* __restrict__ mask, int64_t n, i
 
 // torch.optim.AdamW single-tensor arithmetic (torch/optim/adamw.py ->
 // adam.py _single_tensor_adam with decoupled decay): step counter on device.
+// pidx (nullable): element t belongs to parameter pidx[t], whose step count is
+// step[pidx[t]] (torch.optim.AdamW keeps one step per parameter); else one step
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                              float* __restrict__ m, float* __restrict__ v, int64_t n,
-                             const float* __restrict__ step, float lr, float b1, float b2,
-                             float eps, float wd) {
+                             const float* __restrict__ step, const int32_t* __restrict__ pidx,
+                             float lr, float b1, float b2, float eps, float wd) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const float st = *step;
-  const float bc1 = 1.f - powf(b1, st);
-  const float bc2 = 1.f - powf(b2, st);
-  const float step_size = lr / bc1;
-  const float bc2s = sqrtf(bc2);
+  float st = pidx ? -1.f : step[0];
+  float step_size = 0.f, bc2s = 0.f;
+  if (!pidx) {
+    step_size = lr / (1.f - powf(b1, st));
+    bc2s = sqrtf(1.f - powf(b2, st));
+  }
   for (; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+    if (pidx) {
+      const float sp = step[pidx[t]];
+      if (sp != st) {   // parameters are runs of elements: recompute on a change only
+        st = sp;
+        step_size = lr / (1.f - powf(b1, st));
+        bc2s = sqrtf(1.f - powf(b2, st));
+      }
+    }
     float w = p[t] * (1.f - lr * wd);
     float gg = g[t];
     float mm = m[t];
@@ -257,6 +268,11 @@ __global__ __launch_bounds__(64 * SHIFT_ROWS) void bright_shift_bwd_kernel(
   if (dbright && lane == 0) dbright[r] = s;
 }
 
+__global__ void steps_advance_kernel(float* __restrict__ steps, const uint8_t* __restrict__ active,
+                                     int P) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < P && (!active || active[i])) steps[i] += 1.f;
+}
 __global__ void incr_kernel(float* step, int64_t* rng_state) {
   if (step) *step += 1.f;
   if (rng_state) rng_state[1] += 1;
@@ -484,11 +500,20 @@ VAESNE_API int vaesne_bright_shift_bwd(const float* g, int64_t R, int L, float* 
 }
 
 VAESNE_API int vaesne_adamw(float* p, const float* g, float* m, float* v, int64_t n,
-                            const float* step, float lr, float b1, float b2, float eps, float wd,
-                            void* stream) {
+                            const float* step, const int32_t* pidx, float lr, float b1, float b2,
+                            float eps, float wd, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(adamw_kernel, dim3(blocks_for(n, NT, 4096)), dim3(NT), 0,
-                     (hipStream_t)stream, p, g, m, v, n, step, lr, b1, b2, eps, wd);
+                     (hipStream_t)stream, p, g, m, v, n, step, pidx, lr, b1, b2, eps, wd);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_adamw_steps_advance(float* steps, const uint8_t* active, int P,
+                                          void* stream) {
+  if (P <= 0) return 0;
+  hipLaunchKernelGGL(steps_advance_kernel, dim3((P + NT - 1) / NT), dim3(NT), 0,
+                     (hipStream_t)stream, steps, active, P);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
