@@ -199,6 +199,12 @@ int vaesne_dec_tail_bwd(const float* x, const float* O, const float* kvc, int M,
                         const uint32_t* drop_masks, float* dx, float* dO, float* dkvc,
                         float* gflat, float* workspace, vaesne_colsum_list* defer, void* stream);
 int vaesne_dec_tail_grad_layout(int* offsets);
+/* Test / tuning hook: the decoder-tail backward for sequences of >= 256 tokens runs as
+ * ONE fused kernel per sequence (data gradients and weight-gradient contractions, no
+ * per-token scratch); path 1 forces it for every length, 2 forces the two-kernel path
+ * (data kernel + scratch + weight-gradient kernel), 0 restores the automatic choice.
+ * Process-wide; not for use while launches are in flight. */
+int vaesne_dec_tail_force_path(int path);
 
 /* ---- encoder-block halves ------------------------------------------------------
  * An encoder TransformerBlock (util_layers.py:285-309 as called by

@@ -399,6 +399,51 @@ def test_fused_decoder_tail_dropout_fwd_bwd_consistent():
     assert (o1 - o2).abs().max().item() > 1e-3
 
 
+@pytest.mark.parametrize("L,Lc,store", [(982, 5, True), (300, 4, False), (57, 8, True)])
+def test_decoder_tail_fused_backward_matches_two_kernel_path(L, Lc, store):
+    """The fused per-sequence tail backward (no per-token scratch) against the
+    data-kernel + scratch + weight-gradient-kernel path on the same draws: every
+    gradient, with dropout (stored masks and re-hashed), a fused next in_proj
+    (blocks 0..n-2) and a last block."""
+    from VAESNe import _lib, _ops, rng
+    from VAESNe.util_layers import decoder_stack
+    blocks = _decoder_blocks(3, L + Lc).to(DEV)
+    for b in blocks:
+        b.dropout.p = 0.1
+        b.self_attn.dropout = 0.1
+        b.cross_attn.dropout = 0.1
+    blocks.train()
+    g = torch.Generator().manual_seed(L + Lc)
+    N = 4
+    x = torch.randn(N, L, 32, generator=g).to(DEV)
+    ctx = torch.randn(N, Lc, 32, generator=g).to(DEV)
+    mask = _rand_mask(N, L, 0.1, g).to(DEV)
+    go = torch.randn(N, L, 32, generator=g).to(DEV)
+    res = []
+    old = _ops.STORE_TAIL_MASKS
+    try:
+        _ops.STORE_TAIL_MASKS = store
+        for path in (1, 2):
+            _lib.lib.dec_tail_force_path(path)
+            blocks.zero_grad(set_to_none=True)
+            rng._call = 700
+            xx = x.clone().requires_grad_(True)
+            cc = ctx.clone().requires_grad_(True)
+            out = decoder_stack(blocks, xx, cc, mask)
+            (out * go).sum().backward()
+            torch.cuda.synchronize()
+            res.append([out.detach(), xx.grad, cc.grad] + [p.grad.clone() for p in blocks.parameters()])
+    finally:
+        _lib.lib.dec_tail_force_path(0)
+        _ops.STORE_TAIL_MASKS = old
+    names = ["out", "dx", "dcontext"] + [n for n, _ in blocks.named_parameters()]
+    assert torch.equal(res[0][0], res[1][0])
+    for n, a, b in zip(names, *res):
+        if n.endswith("in_proj_bias"):   # the key slice is analytically zero (shift invariance)
+            a, b = torch.cat([a[:32], a[64:]]), torch.cat([b[:32], b[64:]])
+        assert _rel(a, b) < 1e-5, n
+
+
 def test_fused_decoder_tail_stored_masks_match_rehash():
     """The tail backward reading the forward's stored dropout masks gives the
     same gradients as re-hashing them from the counter RNG.  The two paths are

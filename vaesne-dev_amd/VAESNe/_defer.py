@@ -39,7 +39,7 @@ class List(C.Structure):
 
 
 CAPACITY = 2048
-_MAX_ENTRIES_PER_CALL = 3        # vaesne_*_bwd append at most 3 sums per call
+_MAX_ENTRIES_PER_CALL = 8        # vaesne_*_bwd append at most 7 sums per call
 
 
 class _State:

@@ -55,6 +55,7 @@ SIGNATURES = {
     "vaesne_dec_tail_bwd": (I32, [P, P, P, I32, I32, I32, PP, F32, P, U32, P, P, P, P, P, P, P,
                                   P, P, P, P]),
     "vaesne_dec_tail_grad_layout": (I32, [C.POINTER(I32)]),
+    "vaesne_dec_tail_force_path": (I32, [I32]),
     "vaesne_enc_block_workspace": (I64, [I32]),
     "vaesne_attn_force_geometry": (I32, [I32, I32]),
     "vaesne_enc_block_fwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P]),

@@ -936,10 +936,10 @@ __device__ __forceinline__ float cs_tile(const float* G, int ldg, int64_t r0, in
 // wave keeps occupancy high so the streamed operand loads overlap.
 enum Job { J_WO1 = 0, J_WQ, J_WO2, J_W1, J_W2, J_WN0, J_WN1, J_WN2, J_K, J_V, J_LN, NJOB };
 
-__global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __restrict__ scr) {
+__global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __restrict__ scr, int job0) {
   __shared__ float red[NW * 1024];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
-  const int job = blockIdx.y;
+  const int job = blockIdx.y + job0;
   const bool next = a.Wn != nullptr;
   if (!next && job >= J_WN0 && job <= J_WN2) return;
   if (a.mode != MODE_FULL) {
@@ -1036,6 +1036,390 @@ __global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __rest
   }
 }
 
+// ======================= fused backward (long sequences) =====================
+// One workgroup per sequence runs dec_tail_bwd_data's chain per 32-token tile and
+// does every weight-gradient contraction in place, instead of writing 19
+// per-token scratch vectors (~2.4 KB per token, ~0.6 GB per spectra layer) for
+// dec_tail_wgrad to read back: each vector is transposed through a per-wave LDS
+// tile into the MFMA operand layout (lane = feature, k = token) and contracted
+// into accumulators that live for the whole sequence (7 matrices x 16 plus 11
+// column sums per lane: one wave per SIMD, 512 registers).  The workgroup's
+// partials go to the usual partial row / column sums; the context k | v gradient
+// is complete per workgroup and written directly.  The next block's in_proj
+// gradient (dqkv^T y: inputs only) stays with dec_tail_wgrad's jobs.
+constexpr int LT = 33;        // LDS tile row stride (floats)
+constexpr int TILE = 32 * LT;
+
+// token-major tile: lane (t, h) stores its feature-layout values of token t
+__device__ __forceinline__ void put_fl(float* tile, const float (&v)[16], int lane, bool valid) {
+  const int t = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) tile[t * LT + F(r, h)] = valid ? v[r] : 0.f;
+}
+// rows whose half h holds columns [16h, 16h + 16) in order (cross-attention ds / pd)
+__device__ __forceinline__ void put_half(float* tile, const float (&v)[16], int lane, bool valid) {
+  const int t = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) tile[t * LT + 16 * h + k] = valid ? v[k] : 0.f;
+}
+// MFMA operand layout: lane (c, h) reads column c of tokens 2s + h
+__device__ __forceinline__ void get_op(const float* tile, float (&o)[16], int lane) {
+  const int c = lane & 31, h = lane >> 5;
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int s = 0; s < 16; ++s) o[s] = tile[(2 * s + h) * LT + c];
+}
+__device__ __forceinline__ void contract(f16v& acc, const float (&g)[16], const float (&x)[16],
+                                         float& cs) {
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    cs += g[s];
+    acc = mfma(g[s], x[s], acc);
+  }
+}
+__device__ __forceinline__ void colsum_tile(float* tile, const float (&v)[16], int lane, bool valid,
+                                            float& cs) {
+  put_fl(tile, v, lane, valid);
+  float o[16];
+  get_op(tile, o, lane);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) cs += o[s];
+  asm volatile("" ::: "memory");
+}
+// operand-layout rows of a global [rows][ld] matrix (columns col0 + c), zero past rmax
+__device__ __forceinline__ void get_glob(const float* p, int ld, int col0, int64_t r0,
+                                         int64_t rmax, float (&o)[16], int lane) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int64_t t = min(r0 + 2 * s + h, rmax - 1);
+    o[s] = p[t * ld + col0 + c];
+  }
+#pragma unroll
+  for (int s = 0; s < 16; ++s) o[s] = r0 + 2 * s + h < rmax ? o[s] : 0.f;
+}
+
+template <int LC, bool NEXT, bool DROP, bool MASKS>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void dec_tail_bwd_fused(Tail a) {
+  __shared__ Smem S;
+  __shared__ float Lt[NW][6 * TILE];   // per wave: X1, C / dC, X2, GL, Q, transient
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int seq = blockIdx.x;
+  stage_all(S, a, NEXT);
+  for (int i = threadIdx.x; i < a.Lc * 2 * E; i += NT) S.kv[i] = a.kvc[(int64_t)seq * a.Lc * 2 * E + i];
+  __syncthreads();
+  float* tX1 = Lt[wave];
+  float* tC = tX1 + TILE;
+  float* tX2 = tC + TILE;
+  float* tGL = tX2 + TILE;
+  float* tQ = tGL + TILE;
+  float* tT = tQ + TILE;
+  const uint32_t key = DROP ? key_of(a.rng, a.call_id) : 0u;
+  const float scale = 0.35355339059327373f;
+  const float ik = DROP ? a.inv_keep : 1.f;
+  f16v aWO1 = {}, aWQ = {}, aWO2 = {}, aW1 = {}, aW2 = {}, aK = {}, aV = {};
+  float cBO1 = 0.f, cBQ = 0.f, cBO2 = 0.f, cB1 = 0.f, cB2 = 0.f;
+  float cG1 = 0.f, cBE1 = 0.f, cG2 = 0.f, cBE2 = 0.f, cG3 = 0.f, cBE3 = 0.f;
+  const int64_t base = (int64_t)seq * a.L, rend = base + a.L;
+  for (int tt = wave * 32; tt < a.L; tt += NW * 32) {
+    const int tok = tt + (lane & 31);
+    const bool valid = tok < a.L;
+    const int64_t row = base + (valid ? tok : a.L - 1);
+    const int64_t r0 = base + tt;
+    // ---------------- forward recompute -----------------
+    float xh1[16], xh2[16], xh3[16], f1[16], q[16];
+    float rs1, rs2, rs3;
+    uint32_t km, k0 = 0xffffffffu, k1 = 0xffffffffu, k2 = 0xffffffffu;
+    constexpr bool have = DROP && MASKS;
+    if (have) {
+      const uint4 mw = *reinterpret_cast<const uint4*>(a.masks + row * 4);
+      const int sh = 16 * h;
+      k0 = (mw.x >> sh) & 0xffffu;
+      k1 = (mw.y >> sh) & 0xffffu;
+      k2 = (mw.z >> sh) & 0xffffu;
+      km = mw.w;
+    }
+    {
+      float v[16], t[16], c[16], p[H][LC];
+      load_row(a.O, row, h, t);
+      mv(S.Wo1, S.bo1, t, v, lane);
+      load_row(a.x, row, h, t);
+      if (DROP && have) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] *= ((k0 >> r) & 1u) ? a.inv_keep : 0.f;
+      } else if (DROP) {
+        float sc[16];
+        drop_res(site_key(key, 0), row, h, a.thr, a.inv_keep, sc);
+        k0 = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; k0 |= (sc[r] != 0.f ? 1u : 0u) << r; }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] += t[r];
+      layernorm(v, rs1, xh1);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t[r] = fmaf(xh1[r], S.g1[F(r, h)], S.be1[F(r, h)]);   // x1
+      put_fl(tX1, t, lane, valid);
+      mv(S.Wq, S.bq, t, q, lane);
+      put_fl(tQ, q, lane, valid);
+      cross_fwd<LC>(S.kv, a.Lc, q, h, site_key(key, 3), row, DROP, a.thr, a.inv_keep, p, km, c,
+                    have);
+      put_fl(tC, c, lane, valid);
+      mv(S.Wo2, S.bo2, c, v, lane);
+      if (DROP && have) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] *= ((k1 >> r) & 1u) ? a.inv_keep : 0.f;
+      } else if (DROP) {
+        float sc[16];
+        drop_res(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
+        k1 = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; k1 |= (sc[r] != 0.f ? 1u : 0u) << r; }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] += t[r];
+      layernorm(v, rs2, xh2);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t[r] = fmaf(xh2[r], S.g2[F(r, h)], S.be2[F(r, h)]);   // x2
+      put_fl(tX2, t, lane, valid);
+      mv(S.W1, S.b1, t, f1, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = gelu(f1[r]);
+      put_fl(tGL, v, lane, valid);
+      mv(S.W2, S.b2, v, v, lane);
+      if (DROP && have) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] *= ((k2 >> r) & 1u) ? a.inv_keep : 0.f;
+      } else if (DROP) {
+        float sc[16];
+        drop_res(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
+        k2 = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; k2 |= (sc[r] != 0.f ? 1u : 0u) << r; }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] += t[r];
+      layernorm(v, rs3, xh3);
+    }
+    float go[16], xo[16];
+    // ---------------- backward -----------------
+    float d[16];
+    load_row(a.dy, row, h, d);
+    if (NEXT) {   // (the next block's in_proj gradient reads only inputs: dec_tail_wgrad)
+      f16v acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = d[r];
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) {
+        float g3[16];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          float4 t = *reinterpret_cast<const float4*>(a.dqkv + row * 3 * E + cc * E + 8 * g4 + 4 * h);
+          g3[4 * g4] = t.x; g3[4 * g4 + 1] = t.y; g3[4 * g4 + 2] = t.z; g3[4 * g4 + 3] = t.w;
+        }
+        mvt(S.Wn + cc * E * LP, g3, acc, lane);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) d[r] = acc[r];
+    }
+    float t[16];
+    // LN3
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = d[r] * xh3[r];
+    colsum_tile(tT, d, lane, valid, cBE3);
+    colsum_tile(tT, t, lane, valid, cG3);
+    layernorm_bwd(d, xh3, S.g3, rs3, h, d);                 // dv3 (residual into x2)
+    // FFN
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = ((k2 >> r) & 1u) ? d[r] * ik : 0.f;   // df2
+    put_fl(tT, t, lane, valid);
+    get_op(tT, go, lane);
+    get_op(tGL, xo, lane);
+    contract(aW2, go, xo, cB2);
+    asm volatile("" ::: "memory");
+    {
+      f16v acc = {};
+      mvt(S.W2, t, acc, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t[r] = acc[r] * gelu_erf_grad(f1[r]);   // df1
+    }
+    put_fl(tT, t, lane, valid);
+    get_op(tT, go, lane);
+    get_op(tX2, xo, lane);
+    contract(aW1, go, xo, cB1);
+    asm volatile("" ::: "memory");
+    {
+      f16v acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = d[r];
+      mvt(S.W1, t, acc, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) d[r] = acc[r];                        // dx2
+    }
+    // LN2
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = d[r] * xh2[r];
+    colsum_tile(tT, d, lane, valid, cBE2);
+    colsum_tile(tT, t, lane, valid, cG2);
+    layernorm_bwd(d, xh2, S.g2, rs2, h, d);                 // dv2 (residual into x1)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = ((k1 >> r) & 1u) ? d[r] * ik : 0.f;   // da2
+    put_fl(tT, t, lane, valid);
+    get_op(tT, go, lane);
+    get_op(tC, xo, lane);
+    contract(aWO2, go, xo, cBO2);
+    asm volatile("" ::: "memory");
+    float dc[16];
+    {
+      f16v acc = {};
+      mvt(S.Wo2, t, acc, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dc[r] = acc[r];
+    }
+    put_fl(tC, dc, lane, valid);        // C is consumed: the slot now holds dC
+    // cross attention backward (dq -> t)
+    {
+      float dsv[16], pdv[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) { dsv[k] = 0.f; pdv[k] = 0.f; }
+#pragma unroll
+      for (int hd = 0; hd < H; ++hd) {
+        float dp[LC], ph[LC];
+        cross_probs<LC>(S.kv, a.Lc, q, h, hd, ph);
+        float Dsum = 0.f;
+#pragma unroll
+        for (int j = 0; j < LC; ++j) {
+          float part = 0.f;
+          if (j < a.Lc) {
+            const float* vj = S.kv + j * 2 * E + E + 8 * hd + 4 * h;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) part = fmaf(dc[4 * hd + i], vj[i], part);
+          }
+          part = xsum32(part);
+          const bool kp = (km >> (hd * LCMAX + j)) & 1u;
+          dp[j] = (j < a.Lc && kp) ? part * ik : 0.f;
+          if ((j >> 2) == h) pdv[4 * (j & 3) + hd] = (j < a.Lc && kp) ? ph[j] * ik : 0.f;
+          Dsum = fmaf(ph[j], dp[j], Dsum);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[4 * hd + i] = 0.f;
+#pragma unroll
+        for (int j = 0; j < LC; ++j) {
+          const float ds = j < a.Lc ? ph[j] * (dp[j] - Dsum) * scale : 0.f;
+          if ((j >> 2) == h) dsv[4 * (j & 3) + hd] = ds;
+          if (j < a.Lc) {
+            const float* kj = S.kv + j * 2 * E + 8 * hd + 4 * h;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) t[4 * hd + i] = fmaf(ds, kj[i], t[4 * hd + i]);
+          }
+        }
+      }
+      float unused = 0.f;
+      // dk part: acc[f][j'] += q[t][f] ds[t][j'];  dv part: dC[t][f] pd[t][j']
+      put_half(tT, dsv, lane, valid);
+      get_op(tQ, go, lane);
+      get_op(tT, xo, lane);
+      contract(aK, go, xo, unused);
+      asm volatile("" ::: "memory");
+      put_half(tT, pdv, lane, valid);
+      get_op(tC, go, lane);
+      get_op(tT, xo, lane);
+      contract(aV, go, xo, unused);
+      asm volatile("" ::: "memory");
+    }
+    put_fl(tT, t, lane, valid);         // dq
+    get_op(tT, go, lane);
+    get_op(tX1, xo, lane);
+    contract(aWQ, go, xo, cBQ);
+    asm volatile("" ::: "memory");
+    {
+      f16v acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = d[r];
+      mvt(S.Wq, t, acc, lane);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) d[r] = acc[r];                        // dx1
+    }
+    // LN1
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = d[r] * xh1[r];
+    colsum_tile(tT, d, lane, valid, cBE1);
+    colsum_tile(tT, t, lane, valid, cG1);
+    layernorm_bwd(d, xh1, S.g1, rs1, h, d);                 // dv1 = dx
+    if (valid) store_row(a.dx, row, E, 0, h, d);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) t[r] = ((k0 >> r) & 1u) ? d[r] * ik : 0.f;   // da1
+    put_fl(tT, t, lane, valid);
+    get_op(tT, go, lane);
+    get_glob(a.O, E, 0, r0, rend, xo, lane);
+    contract(aWO1, go, xo, cBO1);
+    asm volatile("" ::: "memory");
+    {
+      f16v acc = {};
+      mvt(S.Wo1, t, acc, lane);
+      float dO[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dO[r] = acc[r];
+      if (valid) store_row(a.dO, row, E, 0, h, dO);
+    }
+  }
+  // ---------------- workgroup sums -----------------
+  __syncthreads();
+  constexpr int RS = 1024 + 64;                  // per-wave stride of the reduction rows
+  float* red = &Lt[0][0];                         // [NW][RS] (reuses the tiles)
+  float* out = a.wpart + (int64_t)seq * WPART;
+  auto flush_job = [&](const f16v& acc, float cs, int moff, int boff) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave * RS + F(r, h) * 32 + (lane & 31)] = acc[r];
+    red[wave * RS + 1024 + lane] = cs;             // lanes 32..63: the other half's rows
+    __syncthreads();
+    for (int i = threadIdx.x; i < 1024; i += NT)
+      out[moff + i] = ((red[i] + red[RS + i]) + red[2 * RS + i]) + red[3 * RS + i];
+    if (threadIdx.x < 32) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w)
+        sum += red[w * RS + 1024 + threadIdx.x] + red[w * RS + 1024 + 32 + threadIdx.x];
+      out[boff + threadIdx.x] = sum;
+    }
+    __syncthreads();
+  };
+  flush_job(aWO1, cBO1, OFF_WO1, OFF_BO1);
+  flush_job(aWQ, cBQ, OFF_WQ, OFF_BQ);
+  flush_job(aWO2, cBO2, OFF_WO2, OFF_BO2);
+  flush_job(aW1, cB1, OFF_W1, OFF_B1);
+  flush_job(aW2, cB2, OFF_W2, OFF_B2);
+  {   // LayerNorm vectors: [g1 b1 | g2 b2 | g3 b3]
+    const float cl[6] = {cG1, cBE1, cG2, cBE2, cG3, cBE3};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) red[wave * RS + i * 64 + lane] = cl[i];
+    __syncthreads();
+    if (threadIdx.x < 6 * 32) {
+      const int i = threadIdx.x / 32, c = threadIdx.x % 32;
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) sum += red[w * RS + i * 64 + c] + red[w * RS + i * 64 + 32 + c];
+      out[OFF_G1 + i * 32 + c] = sum;
+    }
+    __syncthreads();
+  }
+  // context k | v gradients of this sequence: acc[f = F(r,h)][j' = lane&31] is valid
+  // where (j' & 3) == f >> 3, j = j' >> 2 < Lc
+  for (int kv = 0; kv < 2; ++kv) {
+    const f16v& acc = kv ? aV : aK;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave * RS + F(r, h) * 32 + (lane & 31)] = acc[r];
+    __syncthreads();
+    float* dk = a.dkvc + (int64_t)seq * a.Lc * 2 * E + (kv ? E : 0);
+    for (int i = threadIdx.x; i < a.Lc * E; i += NT) {
+      const int j = i / E, f = i % E;
+      const int idx = f * 32 + 4 * j + (f >> 3);
+      dk[j * 2 * E + f] = ((red[idx] + red[RS + idx]) + red[2 * RS + idx]) + red[3 * RS + idx];
+    }
+    __syncthreads();
+  }
+}
+
 // column ranges of the gradient layout a mode produces (the k | v rows of the
 // cross in_proj are excluded: the caller's projection gradient owns them)
 int tail_ranges(int mode, int (&r)[3][2]) {
@@ -1082,9 +1466,44 @@ int launch_bwd(const Tail& a, int grid, float* scr, hipStream_t s) {
     hipLaunchKernelGGL((dec_tail_bwd_data<LC, NEXT, DROP, true>), dim3(grid), dim3(NT), 0, s, a,
                        scr);
   VAESNE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(dec_tail_wgrad, dim3(grid, NJOB), dim3(NT), 0, s, a, (const float*)scr);
+  hipLaunchKernelGGL(dec_tail_wgrad, dim3(grid, NJOB), dim3(NT), 0, s, a, (const float*)scr, 0);
   VAESNE_CHECK_LAUNCH();
   return 0;
+}
+
+template <int LC, bool NEXT, bool DROP>
+int launch_fused(const Tail& a, int grid, hipStream_t s) {
+  if (DROP && !a.masks)
+    hipLaunchKernelGGL((dec_tail_bwd_fused<LC, NEXT, DROP, false>), dim3(grid), dim3(NT), 0, s, a);
+  else
+    hipLaunchKernelGGL((dec_tail_bwd_fused<LC, NEXT, DROP, true>), dim3(grid), dim3(NT), 0, s, a);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+int dispatch_fused(const Tail& a, int grid, hipStream_t s) {
+  const bool next = a.Wn != nullptr, drop = a.p_drop > 0.f;
+#define VAESNE_FUSED_CASE(LCV)                                                  \
+  if (next && drop) return launch_fused<LCV, true, true>(a, grid, s);           \
+  if (next) return launch_fused<LCV, true, false>(a, grid, s);                  \
+  if (drop) return launch_fused<LCV, false, true>(a, grid, s);                  \
+  return launch_fused<LCV, false, false>(a, grid, s);
+  if (a.Lc <= 4) { VAESNE_FUSED_CASE(4) }
+  VAESNE_FUSED_CASE(8)
+#undef VAESNE_FUSED_CASE
+}
+
+// long sequences take the fused backward (VAESNE_TAIL_FUSED=0, or
+// vaesne_dec_tail_force_path(2): the two-kernel path; force_path(1): fused always)
+int g_tail_path = 0;
+bool use_fused(int L) {
+  static const bool env_off = [] {
+    const char* e = getenv("VAESNE_TAIL_FUSED");
+    return e && e[0] == '0';
+  }();
+  if (g_tail_path == 1) return true;
+  if (g_tail_path == 2 || env_off) return false;
+  return L >= 256;
 }
 
 template <bool FWD>
@@ -1155,10 +1574,39 @@ VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* 
   a.masks = p_drop > 0.f ? const_cast<uint32_t*>(drop_masks) : nullptr;
   a.dy = dy; a.dqkv = dqkv; a.dx = dx; a.dO = dO;
   if (a.Wn && !dqkv) return (int)hipErrorInvalidValue;
-  const int chunks = (L + a.chunk - 1) / a.chunk;
-  const int grid = (M / L) * chunks;
   a.y = const_cast<float*>(y);
   a.dkvc = dkvc;
+  if (use_fused(L)) {   // one workgroup per sequence, no scratch
+    const int nseq = M / L;
+    a.wpart = workspace;
+    int rc = dispatch_fused(a, nseq, s);
+    if (rc) return rc;
+    // the next block's in_proj gradient: dec_tail_wgrad's WN jobs (inputs only) into
+    // a second partial area, one row per (sequence, chunk)
+    const int chunks = (L + a.chunk - 1) / a.chunk;
+    float* wn = workspace + (int64_t)nseq * WPART;
+    if (a.Wn) {
+      Tail b = a;
+      b.wpart = wn;
+      hipLaunchKernelGGL(dec_tail_wgrad, dim3(nseq * chunks, 3), dim3(NT), 0, s, b,
+                         (const float*)nullptr, (int)J_WN0);
+      VAESNE_CHECK_LAUNCH();
+    }
+    // fused rows: everything but the in_proj-of-next regions (and the k|v rows)
+    const int fr[5][2] = {{0, OFF_WQ + 1024}, {OFF_WO2, OFF_WN}, {OFF_BO1, OFF_BQ + 32},
+                          {OFF_BO2, OFF_BN}, {OFF_G1, WPART}};
+    for (int k = 0; k < 5; ++k) {
+      rc = colsum_or_defer(defer, workspace + fr[k][0], WPART, nseq, fr[k][1] - fr[k][0],
+                           gflat + fr[k][0], 0, s);
+      if (rc) return rc;
+    }
+    if (!a.Wn) return 0;
+    rc = colsum_or_defer(defer, wn + OFF_WN, WPART, nseq * chunks, 3 * 1024, gflat + OFF_WN, 0, s);
+    return rc ? rc : colsum_or_defer(defer, wn + OFF_BN, WPART, nseq * chunks, 96, gflat + OFF_BN,
+                                     0, s);
+  }
+  const int chunks = (L + a.chunk - 1) / a.chunk;
+  const int grid = (M / L) * chunks;
   // one workgroup: its slab IS the gradient (no column sum)
   a.wpart = grid == 1 ? gflat : workspace;
   float* scr = workspace + (int64_t)grid * WPART;
@@ -1229,10 +1677,16 @@ VAESNE_API int vaesne_enc_block_bwd(int mode, const float* x, const float* O, in
     else hipLaunchKernelGGL((enc_post_bwd_data<false, false>), dim3(grid), dim3(NT), 0, s, a, scr);
   }
   VAESNE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(dec_tail_wgrad, dim3(grid, NJOB), dim3(NT), 0, s, a, (const float*)scr);
+  hipLaunchKernelGGL(dec_tail_wgrad, dim3(grid, NJOB), dim3(NT), 0, s, a, (const float*)scr, 0);
   VAESNE_CHECK_LAUNCH();
   if (grid == 1) return 0;
   return sum_tail(mode, workspace, grid, gflat, defer, s);
+}
+
+VAESNE_API int vaesne_dec_tail_force_path(int path) {
+  if (path < 0 || path > 2) return (int)hipErrorInvalidValue;
+  g_tail_path = path;
+  return 0;
 }
 
 VAESNE_API int vaesne_dec_tail_grad_layout(int* offsets) {
