@@ -524,6 +524,38 @@ def test_fused_encoder_stack_matches_per_op(selfattn, B, T, Lc):
         assert _rel(a, b) < 2e-5, n
 
 
+@pytest.mark.parametrize("B,Lc,defer", [(16, 983, False), (3, 70, True)])
+def test_merged_context_paths_match_per_block(B, Lc, defer, monkeypatch):
+    """The blocks' context self-attention paths batch-stacked into one attention
+    launch (util_layers._merged_context_paths, VAESNE_CTX_MERGE) against one path
+    per block: outputs and every gradient (cfg-5 shape: 4 blocks, 983 tokens)."""
+    from VAESNe import _defer
+    from VAESNe.util_layers import encoder_stack
+    blocks = _encoder_blocks(4, B + Lc + 1, True).to(DEV)
+    blocks.train()
+    g = torch.Generator().manual_seed(Lc + 1)
+    x = torch.randn(B, 8, 32, generator=g).to(DEV)
+    ctx = torch.randn(B, Lc, 32, generator=g).to(DEV)
+    mask = _rand_mask(B, Lc, 0.05, g).to(DEV)
+    go = torch.randn(B, 8, 32, generator=g).to(DEV)
+    res = []
+    for merge in ("1", "0"):
+        monkeypatch.setenv("VAESNE_CTX_MERGE", merge)
+        blocks.zero_grad(set_to_none=True)
+        xx = x.clone().requires_grad_(True)
+        cc = ctx.clone().requires_grad_(True)
+        with _defer.deferred(defer):
+            out = encoder_stack(blocks, xx, cc, context_mask=mask)
+            (out * go).sum().backward()
+        torch.cuda.synchronize()
+        res.append([out.detach(), xx.grad, cc.grad] + [p.grad.clone() for p in blocks.parameters()])
+        del out
+    names = ["out", "dx", "dcontext"] + [n for n, _ in blocks.named_parameters()]
+    assert len(names) == len(res[0]) and any("context_self_attn" in n for n in names)
+    for n, a, b in zip(names, *res):
+        assert _rel(a, b) < 1e-5, n
+
+
 def test_fused_encoder_stack_dropout_fwd_bwd_consistent():
     """With dropout on, the encoder halves' backward replays the forward's masks:
     a directional finite difference matches <grad, v>."""

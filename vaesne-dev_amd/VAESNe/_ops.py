@@ -186,6 +186,102 @@ def in_proj_pair(query, key, weight, bias):
     return InProjPairFn.apply(query, key, weight, bias)
 
 
+class GroupLinearFn(torch.autograd.Function):
+    """G token-wise linears with their own (W_g, b_g), stacked batch-major, one
+    launch per group: the encoder blocks' context self-attention projections
+    (util_layers.py:297, once per block on the same context), so the G attention
+    cores run as ONE launch over G*B sequences (util_layers.encoder_stack).
+      shared:     x [*, K]    -> y [G, *, N],          y[g] = x W_g^T + b_g
+      not shared: x [G, *, K] -> (y_0, .., y_{G-1}),   y_g [*, N] = x[g] W_g^T + b_g
+    Parameter gradients are per group (deferred sums as LinearFn's)."""
+
+    @staticmethod
+    def forward(ctx, x, shared, *wb):
+        G = len(wb) // 2
+        Ws, bs = wb[0::2], wb[1::2]
+        _lib.require_device(x, *wb)
+        _f32(x)
+        _defer.count_uses(*wb)
+        ctx.params = wb
+        N, K = Ws[0].shape
+        if any(W.shape != (N, K) for W in Ws) or x.shape[-1] != K:
+            raise RuntimeError("GroupLinearFn: every W_g must be [N, K] with K = x.shape[-1]")
+        if not shared and x.shape[0] != G:
+            raise RuntimeError("GroupLinearFn: stacked input must be [G, *, K]")
+        x = x.contiguous()
+        lead = x.shape[:-1] if shared else x.shape[1:-1]
+        M = math.prod(lead)
+        Wc = [W.contiguous() for W in Ws]
+        dev = x.device
+        s = stream()
+        if shared:
+            y = torch.empty((G, M, N), dtype=torch.float32, device=dev)
+            outs = [y.data_ptr() + 4 * g * M * N for g in range(G)]
+        else:
+            ys = [torch.empty((M, N), dtype=torch.float32, device=dev) for _ in range(G)]
+            outs = [t.data_ptr() for t in ys]
+        for g in range(G):
+            xp = x.data_ptr() + (0 if shared else 4 * g * M * K)
+            lib.linear_fwd(xp, K, None, 0, M, K, Wc[g].data_ptr(), ptr(bs[g]), N, outs[g], N,
+                           None, 0, 0, 0, s)
+        ctx.meta = (G, M, K, N, bool(shared), x.shape, tuple(b is not None for b in bs))
+        ctx.save_for_backward(x, *Wc)
+        if shared:
+            return y.view(G, *lead, N)
+        return tuple(t.view(*lead, N) for t in ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        x, *Wc = ctx.saved_tensors
+        G, M, K, N, shared, xshape, has_b = ctx.meta
+        ng = ctx.needs_input_grad
+        dev = x.device
+        s = stream()
+        if shared:
+            dy = dys[0].contiguous()
+            dyp = [dy.data_ptr() + 4 * g * M * N for g in range(G)]
+            keep = [dy]
+        else:
+            keep = [None if d is None else d.contiguous() for d in dys]
+            dyp = [None if d is None else d.data_ptr() for d in keep]
+        dx = None
+        if ng[0]:
+            if shared:
+                dx = torch.empty((M, K), dtype=torch.float32, device=dev)
+                for g in range(G):   # dx = sum_g dy[g] W_g, in group order
+                    lib.linear_bwd_data(dyp[g], N, None, 0, 0, M, N, Wc[g].data_ptr(), K,
+                                        dx.data_ptr(), K, int(g > 0), s)
+            else:
+                dx = torch.empty((G, M, K), dtype=torch.float32, device=dev)
+                for g in range(G):
+                    if dyp[g] is None:
+                        dx[g].zero_()
+                    else:
+                        lib.linear_bwd_data(dyp[g], N, None, 0, 0, M, N, Wc[g].data_ptr(), K,
+                                            dx.data_ptr() + 4 * g * M * K, K, 0, s)
+            dx = dx.view(xshape)
+        grads = [None] * (2 * G)
+        for g in range(G):
+            if dyp[g] is None or not (ng[2 + 2 * g] or ng[3 + 2 * g]):
+                continue
+            dW = torch.empty((N, K), dtype=torch.float32, device=dev)
+            db = torch.empty((N,), dtype=torch.float32, device=dev) if has_b[g] else None
+            ws = _ws(lib.linear_bwd_weight_workspace(M, N, K), dev)
+            dfr = _defer.target(ctx.params[2 * g:2 * g + 2], (dW, db), (ws,))
+            xp = x.data_ptr() + (0 if shared else 4 * g * M * K)
+            lib.linear_bwd_weight(dyp[g], N, None, 0, 0, xp, K, None, 0, M, N, K, dW.data_ptr(),
+                                  ptr(db), 0, ws.data_ptr(), dfr, s)
+            grads[2 * g] = dW if ng[2 + 2 * g] else None
+            grads[2 * g + 1] = db if ng[3 + 2 * g] else None
+        return (dx, None, *grads)
+
+
+def group_linear(x, weights, biases, shared):
+    """GroupLinearFn: `shared` -> y [G, *, N]; else x [G, *, K] -> G outputs."""
+    wb = [t for pair in zip(weights, biases) for t in pair]
+    return GroupLinearFn.apply(x, bool(shared), *wb)
+
+
 # ---------------------------------------------------------------------------
 # residual + dropout + LayerNorm
 # ---------------------------------------------------------------------------
@@ -278,6 +374,27 @@ _KBIAS_CACHE = []
 def key_bias_of(mask):
     """The (cached) additive key bias of a key_padding_mask, or None."""
     return None if mask is None else _bias_of(mask, None)
+
+
+def key_bias_rep(mask, G):
+    """The key bias of a [B, L] mask for G batch-stacked copies of its sequences
+    ([G*B, L]; cached like key_bias_of), or None."""
+    if mask is None:
+        return None
+    if G == 1:
+        return key_bias_of(mask)
+    for ent in _KBIAS_REP_CACHE:
+        if ent[0] is mask and ent[1] == mask._version and ent[2] == G \
+                and ent[3].device == mask.device:
+            return ent[3]
+    kb = key_bias_of(mask).repeat(G, 1)
+    _KBIAS_REP_CACHE.append((mask, mask._version, G, kb))
+    if len(_KBIAS_REP_CACHE) > 8:
+        _KBIAS_REP_CACHE.pop(0)
+    return kb
+
+
+_KBIAS_REP_CACHE = []
 
 
 def used_on(stream, *ts):

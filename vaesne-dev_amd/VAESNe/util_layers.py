@@ -307,6 +307,97 @@ def _fusable_encoder_block(blk):
             and all(ln.eps == 1e-5 for ln in (blk.layernorm1, blk.layernorm2, blk.layernorm3)))
 
 
+def _context_paths(blocks, context, context_mask):
+    """Per-block context paths (x = LN(c + Drop(SelfAttn(c))) of each block with a
+    context self-attention; the plain context otherwise) -> (ctxs, events).
+    Every block reads the ORIGINAL context (twice with a context self-attention:
+    its in-projection and its residual): aliases whose gradients one kernel sums.
+    The paths are independent of each other and of the latent chain, so they run
+    ahead on their own streams, one event per block for the join."""
+    uses = [2 if b.context_self_attn is not None else 1 for b in blocks]
+    cal = iter(_ops.fanout(context, sum(uses)))
+    cuse = [[next(cal) for _ in range(u)] for u in uses]
+    ctxs = [cu[0] for cu in cuse]
+    evs = [None] * len(blocks)
+    if not any(b.context_self_attn is not None for b in blocks):
+        return ctxs, evs
+    main = torch.cuda.current_stream() if _ctx_stream(context) is not None else None
+    kb = _ops.key_bias_of(context_mask)     # built on the main stream, shared by all paths
+    for i, blk in enumerate(blocks):
+        if blk.context_self_attn is None:
+            continue
+        cs = _ctx_stream(context, i)
+        if cs is not None:
+            cs.wait_stream(main)
+            # tensors crossing streams are recorded on their consumer stream, so the
+            # caching allocator never hands their memory to the producer stream while
+            # the consumer may still read it (the B=16 step read a reused block as
+            # block i's context in the k|v weight gradient without this)
+            _ops.used_on(cs, context, *cuse[i], kb)
+        p = blk.dropout.p if blk.training else 0.0
+        c_in, c_res = cuse[i]
+        with torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext():
+            c, _ = blk.context_self_attn(c_in, c_in, c_in, key_padding_mask=context_mask)
+            ctxs[i] = _ops.add_layernorm(c_res, c, blk.layernorm_context, p)
+            if cs is not None:
+                evs[i] = torch.cuda.Event()
+                evs[i].record(cs)
+                _ops.used_on(main, ctxs[i])
+    return ctxs, evs
+
+
+def _mergeable_context_paths(blocks, context):
+    if len(blocks) < 2 or os.environ.get("VAESNE_CTX_MERGE", "1") == "0":
+        return False
+    m0 = blocks[0].context_self_attn
+    if m0 is None or context.dim() != 3:
+        return False
+    for b in blocks:
+        m = b.context_self_attn
+        if (m is None or m.num_heads != m0.num_heads or m.dropout != m0.dropout
+                or m.in_proj_bias is None or m.out_proj.bias is None
+                or not m.batch_first or m.embed_dim != context.shape[-1]):
+            return False
+    return True
+
+
+def _merged_context_paths(blocks, context, context_mask):
+    """The G blocks' context paths as one batch-stacked path: the G in-projections
+    write [G, B, L, 3E] (GroupLinearFn), ONE attention launch runs all G*B
+    sequences (G x the workgroups of a per-block launch, which at B=16 x 983 tokens
+    fills half the chip at best), the G out-projections read their slices back,
+    then each block's residual + LayerNorm.  Per block the arithmetic is the
+    per-block path's (util_layers.py:297-298); only the dropout draws come from one
+    RNG call instead of G.  One stream, one event for the join."""
+    G = len(blocks)
+    B, L, E = context.shape
+    mhas = [b.context_self_attn for b in blocks]
+    H = mhas[0].num_heads
+    pa = mhas[0].dropout if blocks[0].training else 0.0
+    cal = _ops.fanout(context, 1 + G)      # the in-projections' input + G residuals
+    cs = _ctx_stream(context, 0)
+    main = torch.cuda.current_stream() if cs is not None else None
+    kb = _ops.key_bias_rep(context_mask, G)
+    if cs is not None:
+        cs.wait_stream(main)
+        _ops.used_on(cs, context, *cal, kb)
+    ev = None
+    with torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext():
+        qkv = _ops.group_linear(cal[0], [m.in_proj_weight for m in mhas],
+                                [m.in_proj_bias for m in mhas], shared=True)
+        o = _ops.self_attention(qkv.view(G * B, L, 3 * E), None, H, pa, kbias=kb)
+        cs_ = _ops.group_linear(o.view(G, B, L, E), [m.out_proj.weight for m in mhas],
+                                [m.out_proj.bias for m in mhas], shared=False)
+        ctxs = [_ops.add_layernorm(cal[1 + i], cs_[i], blk.layernorm_context,
+                                   blk.dropout.p if blk.training else 0.0)
+                for i, blk in enumerate(blocks)]
+        if cs is not None:
+            ev = torch.cuda.Event()
+            ev.record(cs)
+            _ops.used_on(main, *ctxs)
+    return ctxs, [ev] + [None] * (G - 1)
+
+
 def encoder_stack(blocks, x, context, context_mask=None, x_qkv=None):
     """`for blk in blocks: x = blk(x, context, context_mask=context_mask)` for the
     encoders (SpectraLayers.py:135-136, PhotometricLayers.py:141-143: unmasked
@@ -314,52 +405,18 @@ def encoder_stack(blocks, x, context, context_mask=None, x_qkv=None):
     reference's shape each block runs as: latent self-attention core -> PRE
     (out_proj, LN1, cross q) + context k|v projection -> cross-attention core ->
     POST (out_proj, LN2, FFN, LN3 and the next block's in_proj).  The optional
-    context self-attention (spectra `selfattn`) stays on its per-op path."""
+    context self-attention (spectra `selfattn`) runs ahead of the latent chain:
+    batch-stacked over the blocks (_merged_context_paths) or per block."""
     blocks = list(blocks)
     if not blocks or not all(_fusable_encoder_block(b) for b in blocks) or x.dim() != 3:
         for blk in blocks:
             x = blk(x, context, context_mask=context_mask)
         return x
     b0 = blocks[0].self_attn
-    # every block reads the ORIGINAL context (twice with a context self-attention:
-    # its in-projection and its residual): aliases whose gradients one kernel sums
-    uses = [2 if b.context_self_attn is not None else 1 for b in blocks]
-    cal = iter(_ops.fanout(context, sum(uses)))
-    cuse = [[next(cal) for _ in range(u)] for u in uses]
-    # The context self-attention of every block reads the ORIGINAL context, so the
-    # blocks' context paths are independent of each other and of the latent chain:
-    # they run ahead on their own stream, one event per block for the join.
-    ctxs = [cu[0] for cu in cuse]
-    if any(b.context_self_attn is not None for b in blocks):
-        main = torch.cuda.current_stream() if _ctx_stream(context) is not None else None
-        kb = _ops.key_bias_of(context_mask)     # built on the main stream, shared by all paths
-        evs = []
-        for i, blk in enumerate(blocks):
-            if blk.context_self_attn is None:
-                evs.append(None)
-                continue
-            cs = _ctx_stream(context, i)
-            if cs is not None:
-                cs.wait_stream(main)
-                # tensors crossing streams are recorded on their consumer stream, so the
-                # caching allocator never hands their memory to the producer stream while
-                # the consumer may still read it (the B=16 step read a reused block as
-                # block i's context in the k|v weight gradient without this)
-                _ops.used_on(cs, context, *cuse[i], kb)
-            p = blk.dropout.p if blk.training else 0.0
-            c_in, c_res = cuse[i]
-            with torch.cuda.stream(cs) if cs is not None else contextlib.nullcontext():
-                c, _ = blk.context_self_attn(c_in, c_in, c_in, key_padding_mask=context_mask)
-                ctxs[i] = _ops.add_layernorm(c_res, c, blk.layernorm_context, p)
-                if cs is not None:
-                    ev = torch.cuda.Event()
-                    ev.record(cs)
-                    evs.append(ev)
-                    _ops.used_on(main, ctxs[i])
-                else:
-                    evs.append(None)
+    if _mergeable_context_paths(blocks, context):
+        ctxs, evs = _merged_context_paths(blocks, context, context_mask)
     else:
-        evs = [None] * len(blocks)
+        ctxs, evs = _context_paths(blocks, context, context_mask)
     qkv = _ops.linear(x if x_qkv is None else x_qkv, b0.in_proj_weight, b0.in_proj_bias)
     for i, blk in enumerate(blocks):
         p = blk.dropout.p if blk.training else 0.0
