@@ -232,6 +232,55 @@ int vaesne_enc_block_bwd(int mode, const float* x, const float* O, int M, const 
                          const uint32_t* drop_masks, float* dx, float* dO, float* gflat,
                          float* workspace, vaesne_colsum_list* defer, void* stream);
 
+/* ---- fused encoder latent chain -------------------------------------------------
+ * Every TransformerBlock of an encoder's latent side in ONE forward and ONE backward
+ * launch: photometricTransformerEncoder / spectraTransformerEncoder's block loop
+ * (PhotometricLayers.py:141-142, SpectraLayers.py:135-136 -> util_layers.py:285-309
+ * with x = the T = 2 * latent_len bottleneck tokens, context = the data tokens; the
+ * optional context self-attention runs before, as its own ops).  Replaces, per block,
+ * vaesne_attn_fwd / bwd (latent self-attention and cross-attention cores, the
+ * few-query kernels) and vaesne_enc_block_fwd / bwd (PRE / POST halves).  One
+ * workgroup per sequence; groups (at most 2 per launch) are independent encoders
+ * run side by side.  Per group:
+ *   w[blk][18]: self_attn.in_proj_weight [96,32], in_proj_bias [96], out_proj W / b,
+ *     layernorm1 w / b, cross_attn.in_proj_weight [96,32] (rows [0,32) = Wq are read
+ *     here), cross_attn.in_proj_bias [96], cross out_proj W / b, layernorm2 w / b,
+ *     ffn[0] W / b, ffn[2] W / b, layernorm3 w / b (E = 32, 4 heads, ff 32, eps 1e-5)
+ *   kv[blk]: [B, Lk, 64] the block's projected context k | v (in_proj rows [32, 96))
+ *   kbias: [B, Lk] additive key bias (0 / -inf: vaesne_mask_bias) with row stride
+ *     kbias_bs, or null; call_id[blk] = {self-attn, PRE residual, cross-attn, POST
+ *     residual} dropout streams (the per-op path's ids give bit-identical masks)
+ *   x0 [B, T, 32] chain input, y [B, T, 32] output, save [B][nb][save_blk] activations
+ *   (fwd writes, bwd reads); bwd: dy [B, T, 32] -> dx0 [B, T, 32], dkv[blk] [B, Lk, 64],
+ *   per-sequence partials wpart [B][nb * pblk] and their column sums into gflat
+ *   [nb * pblk] (now, or appended to `defer`): every gradient of the 18 tensors per
+ *   block in vaesne_enc_chain_layout's offsets EXCEPT the k | v rows of the cross
+ *   in_proj weight / bias (rows [32, 96)), which the caller's context-projection
+ *   weight gradient writes in place.  T <= 8, nb <= VAESNE_ENC_CHAIN_MAXB. */
+#define VAESNE_ENC_CHAIN_MAXB 6
+typedef struct vaesne_enc_chain_group {
+  const float* w[VAESNE_ENC_CHAIN_MAXB][18];
+  const float* kv[VAESNE_ENC_CHAIN_MAXB];
+  float* dkv[VAESNE_ENC_CHAIN_MAXB];
+  uint32_t call_id[VAESNE_ENC_CHAIN_MAXB][4];
+  int B, T, Lk, nb;
+  float p_attn, p_res, p_cross;
+  const int64_t* rng;
+  const float* kbias;
+  int64_t kbias_bs;
+  const float* x0;
+  float* y;
+  float* save;
+  const float* dy;
+  float* dx0;
+  float* wpart;
+  float* gflat;
+} vaesne_enc_chain_group;
+int vaesne_enc_chain_layout(int* save_blk, int* pblk, int* offsets);
+int vaesne_enc_chain_fwd(int G, const vaesne_enc_chain_group* groups, void* stream);
+int vaesne_enc_chain_bwd(int G, const vaesne_enc_chain_group* groups,
+                         vaesne_colsum_list* defer, void* stream);
+
 /* ---- embeddings ------------------------------------------------------------
  * [sin(x*div) | cos(x*div)]: util_layers.py:125-129 (plain, 16 freqs) and
  * :142-146 (MLP form, 32 freqs).  x is read at index r % period, so the

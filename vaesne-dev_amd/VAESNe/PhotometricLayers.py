@@ -6,10 +6,10 @@ PhotometricLayers.py; forward passes run on the HIP kernels.
 import torch
 from torch import nn
 
-from . import _ops
+from . import _chain, _ops
 from .util_layers import (MLP, Linear, SinusoidalMLPPositionalEmbedding,
                           SinusoidalPositionalEmbedding, TransformerBlock, decoder_stack,
-                          singlelayerMLP, encoder_stack)
+                          singlelayerMLP, encoder_stack_steps)
 
 
 class photometricTransformerDecoder(nn.Module):
@@ -67,6 +67,11 @@ class photometricTransformerEncoder(nn.Module):
             self.LCfc = None
 
     def forward(self, flux, time, band, mask=None):
+        return _chain.drive([self.steps(flux, time, band, mask)])[0]
+
+    def steps(self, flux, time, band, mask=None):
+        """forward as a generator (VAESNe._chain.drive): yields the fused latent chain's
+        work item so several encoders' chains can share one launch."""
         if self.concat:
             tok = self.LCfc(torch.cat([self.fluxfc(flux[:, :, None]),
                                        self.time_embd(time),
@@ -77,5 +82,6 @@ class photometricTransformerEncoder(nn.Module):
                                  base=self.fluxfc(flux[:, :, None], base=self.time_embd(time)))
         x = _ops.repeat_batch(self.initbottleneck, flux.shape[0])
         x_res, x_qkv, x_out = _ops.fanout(x, 3)
-        h = encoder_stack(self.transformerblocks, x_res, tok, context_mask=mask, x_qkv=x_qkv)
+        h = yield from encoder_stack_steps(self.transformerblocks, x_res, tok, context_mask=mask,
+                                           x_qkv=x_qkv)
         return self.bottleneckfc(x_out, h)   # bottleneckfc(x + h)

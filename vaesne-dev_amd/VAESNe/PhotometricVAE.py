@@ -8,7 +8,7 @@ import torch
 import torch.distributions as dist
 from torch import nn
 
-from . import _ops
+from . import _chain, _ops
 from .PhotometricLayers import photometricTransformerDecoder, photometricTransformerEncoder
 from .base_vae import VAE, check_laplace
 from .util_layers import MLP
@@ -28,7 +28,10 @@ class PhotometricEnc(nn.Module):
         self.latent_len = latent_len
 
     def forward(self, flux, time, band, mask=None):
-        bottleneck = self.inference_transformer(flux, time, band, mask)
+        return _chain.drive([self.steps(flux, time, band, mask)])[0]
+
+    def steps(self, flux, time, band, mask=None):
+        bottleneck = yield from self.inference_transformer.steps(flux, time, band, mask)
         return _ops.latent_head(bottleneck, self.latent_len)
 
 
@@ -84,8 +87,13 @@ class PhotometricVAE(VAE):
 
     def posterior(self, x, K=1):
         """Encoder -> q(z|x) and K reparameterised draws (PhotometricVAE.py:158-163)."""
+        return _chain.drive([self.posterior_steps(x, K)])[0]
+
+    def posterior_steps(self, x, K=1):
+        """posterior as a generator (VAESNe._chain.drive: several VAEs' encoder chains
+        in one launch)."""
         flux, time, band, mask = x
-        self._qz_x_params = self.enc(flux, time, band, mask)
+        self._qz_x_params = yield from self.enc.steps(flux, time, band, mask)
         qz_x = self._dist(self.qz_x, *self._qz_x_params)
         zs = _ops.laplace_rsample(*self._qz_x_params, K)
         return qz_x, zs

@@ -8,10 +8,10 @@ SpectraLayers.py; forward passes run on the HIP kernels.  The decoder's
 import torch
 from torch import nn
 
-from . import _ops
+from . import _chain, _ops
 from .util_layers import (MLP, Linear, SinusoidalMLPPositionalEmbedding,
                           SinusoidalPositionalEmbedding, TransformerBlock, decoder_stack,
-                          singlelayerMLP, encoder_stack)
+                          singlelayerMLP, encoder_stack_steps)
 
 
 class spectraTransformerDecoder(nn.Module):
@@ -66,6 +66,10 @@ class spectraTransformerEncoder(nn.Module):
         self.phase_embd_layer = SinusoidalMLPPositionalEmbedding(model_dim)
 
     def forward(self, wavelength, flux, phase, mask=None):
+        return _chain.drive([self.steps(wavelength, flux, phase, mask)])[0]
+
+    def steps(self, wavelength, flux, phase, mask=None):
+        """forward as a generator (VAESNe._chain.drive), see photometricTransformerEncoder."""
         if self.concat:
             flux_embd = self.spectrafc(torch.cat([self.flux_embd(flux[:, :, None]),
                                                   self.wavelength_embd_layer(wavelength)], dim=-1))
@@ -80,5 +84,6 @@ class spectraTransformerEncoder(nn.Module):
                                                 device=mask.device)], dim=1)
         x = _ops.repeat_batch(self.initbottleneck, context.shape[0])
         x_res, x_qkv, x_out = _ops.fanout(x, 3)
-        h = encoder_stack(self.transformerblocks, x_res, context, context_mask=mask, x_qkv=x_qkv)
+        h = yield from encoder_stack_steps(self.transformerblocks, x_res, context,
+                                           context_mask=mask, x_qkv=x_qkv)
         return self.bottleneckfc(x_out, h)   # bottleneckfc(x + h)

@@ -7,7 +7,7 @@ import torch
 import torch.distributions as dist
 from torch import nn
 
-from . import _ops
+from . import _chain, _ops
 from .SpectraLayers import spectraTransformerDecoder, spectraTransformerEncoder
 from .base_vae import VAE, check_laplace
 from .util_layers import MLP, prefetch_decoder_dropout
@@ -26,8 +26,11 @@ class SpectraEnc(nn.Module):
         self.latent_len = latent_len
 
     def forward(self, flux, wavelength, phase, mask=None):
+        return _chain.drive([self.steps(flux, wavelength, phase, mask)])[0]
+
+    def steps(self, flux, wavelength, phase, mask=None):
         # NB argument order into the encoder is the reference's (see SpectraLayers)
-        bottleneck = self.inference_transformer(flux, wavelength, phase, mask)
+        bottleneck = yield from self.inference_transformer.steps(flux, wavelength, phase, mask)
         return _ops.latent_head(bottleneck, self.latent_len)
 
 
@@ -85,8 +88,12 @@ class SpectraVAE(VAE):
 
     def posterior(self, x, K=1):
         """Encoder -> q(z|x) and K reparameterised draws (SpectraVAE.py:149-152)."""
+        return _chain.drive([self.posterior_steps(x, K)])[0]
+
+    def posterior_steps(self, x, K=1):
+        """posterior as a generator (VAESNe._chain.drive)."""
         flux, wavelength, phase, mask = x
-        self._qz_x_params = self.enc(flux, wavelength, phase, mask)
+        self._qz_x_params = yield from self.enc.steps(flux, wavelength, phase, mask)
         qz_x = self._dist(self.qz_x, *self._qz_x_params)
         zs = _ops.laplace_rsample(*self._qz_x_params, K)
         return qz_x, zs

@@ -96,11 +96,12 @@ def _deferrable(p) -> bool:
             and not getattr(p, "_post_accumulate_grad_hooks", None))
 
 
-def target(params, outputs, keep=()):
+def target(params, outputs, keep=(), entries=_MAX_ENTRIES_PER_CALL):
     """Backward side: the list to append this op's sums to (a ctypes pointer), or
     None to launch them now.  `params[i]` receives `outputs[i]` (None entries
-    skipped); `keep` = the partial buffers the sums read."""
-    if _S.depth == 0 or _S.clist.count + _MAX_ENTRIES_PER_CALL > CAPACITY:
+    skipped); `keep` = the partial buffers the sums read; `entries` = the most sums
+    the op appends."""
+    if _S.depth == 0 or _S.clist.count + entries > CAPACITY:
         return None
     pairs = [(p, o) for p, o in zip(params, outputs) if p is not None and o is not None]
     if not pairs or not all(_deferrable(p) for p, _ in pairs):

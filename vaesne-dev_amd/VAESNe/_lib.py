@@ -61,6 +61,9 @@ SIGNATURES = {
     "vaesne_enc_block_fwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P]),
     "vaesne_enc_block_bwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P, P, P, P, P, P,
                                    P]),
+    "vaesne_enc_chain_layout": (I32, [P, P, P]),
+    "vaesne_enc_chain_fwd": (I32, [I32, P, P]),
+    "vaesne_enc_chain_bwd": (I32, [I32, P, P, P]),
     "vaesne_sincos": (I32, [P, I64, I64, P, I32, P, I64, P]),
     "vaesne_embed_fwd": (I32, [P, I64, I64, P, I32, P, I64, P, I64, P]),
     "vaesne_embed_bwd_workspace": (I64, [I64, I32, I32]),

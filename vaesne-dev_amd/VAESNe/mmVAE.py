@@ -7,7 +7,7 @@ import torch
 import torch.distributions as dist
 import torch.nn as nn
 
-from . import _ops
+from . import _chain, _ops
 from .util_layers import prefetch_decoder_dropout
 
 
@@ -113,20 +113,32 @@ class photospecMMVAE(nn.Module):
                 prefetch_decoder_dropout(vae.dec.generativetransformer, K * n * B,
                                          x[d][1].shape[-1], x[d][1].device)
         qz_xs, zss = [None] * n, [None] * n
-        with _Branches(side) as br:
-            br.to_side(*x[0])
-            for m, vae in enumerate(self.vaes):
-                with br.on(m):
-                    qz_xs[m], zss[m] = vae.posterior(x[m], K=K)
-            br.to_main(qz_xs[0].loc, qz_xs[0].scale, zss[0])
+        if os.environ.get("VAESNE_ENC_GROUP", "0") == "1" and \
+                all(hasattr(v, "posterior_steps") for v in self.vaes):
+            # both encoders on this stream, their fused latent chains in ONE launch
+            # (a captured graph runs side-stream branches one after the other anyway)
+            res = _chain.drive([vae.posterior_steps(x[m], K=K) for m, vae in enumerate(self.vaes)])
+            for m in range(n):
+                qz_xs[m], zss[m] = res[m]
+        else:
+            with _Branches(side) as br:
+                br.to_side(*x[0])
+                for m, vae in enumerate(self.vaes):
+                    with br.on(m):
+                        qz_xs[m], zss[m] = vae.posterior(x[m], K=K)
+                br.to_main(qz_xs[0].loc, qz_xs[0].scale, zss[0])
         px_zs = _CellMatrix([[None for _ in range(n)] for _ in range(n)])
         if all(z.shape == zss[0].shape for z in zss):
             B = zss[0].shape[1]
             zcat = torch.cat(zss, dim=1)
             px_zs.merged = [None] * n
+            order = list(range(n))
+            if os.environ.get("VAESNE_DEC_ORDER", "") == "rev":
+                order.reverse()       # the long spectra decoder issued first
             with _Branches(side) as br:
                 br.to_side(zcat)
-                for d, vae in enumerate(self.vaes):
+                for d in order:
+                    vae = self.vaes[d]
                     with br.on(d):
                         px_zs.merged[d] = vae.decode_params(zcat, x[d], groups=n)
                 br.to_main(*px_zs.merged[0])

@@ -22,7 +22,7 @@ import os
 import torch
 from torch import nn
 
-from . import _ops
+from . import _chain, _ops
 
 
 class Linear(nn.Linear):
@@ -402,21 +402,48 @@ def encoder_stack(blocks, x, context, context_mask=None, x_qkv=None):
     """`for blk in blocks: x = blk(x, context, context_mask=context_mask)` for the
     encoders (SpectraLayers.py:135-136, PhotometricLayers.py:141-143: unmasked
     latent tokens x, the ORIGINAL data tokens as every block's context).  With the
-    reference's shape each block runs as: latent self-attention core -> PRE
-    (out_proj, LN1, cross q) + context k|v projection -> cross-attention core ->
-    POST (out_proj, LN2, FFN, LN3 and the next block's in_proj).  The optional
-    context self-attention (spectra `selfattn`) runs ahead of the latent chain:
-    batch-stacked over the blocks (_merged_context_paths) or per block."""
+    reference's shape the latent side of all blocks is ONE fused chain launch
+    (VAESNe._chain; VAESNE_ENC_CHAIN=0 selects the per-block path: latent
+    self-attention core -> PRE (out_proj, LN1, cross q) + context k|v projection ->
+    cross-attention core -> POST (out_proj, LN2, FFN, LN3, next in_proj)).  The
+    optional context self-attention (spectra `selfattn`) runs ahead of the latent
+    chain: batch-stacked over the blocks (_merged_context_paths) or per block."""
+    return _chain.drive([encoder_stack_steps(blocks, x, context, context_mask, x_qkv)])[0]
+
+
+def encoder_stack_steps(blocks, x, context, context_mask=None, x_qkv=None):
+    """encoder_stack as a generator (VAESNe._chain.drive): runs everything up to the
+    fused latent chain, yields the chain's work item (or None when the blocks take
+    the per-op path), receives the chain output and returns it.  Driving several
+    encoders' generators together launches their chains as ONE kernel."""
     blocks = list(blocks)
     if not blocks or not all(_fusable_encoder_block(b) for b in blocks) or x.dim() != 3:
+        yield None
         for blk in blocks:
             x = blk(x, context, context_mask=context_mask)
         return x
-    b0 = blocks[0].self_attn
+    chain = _chain.fusable(blocks, x) and os.environ.get("VAESNE_ENC_CHAIN", "1") != "0"
+    if chain and not any(b.context_self_attn is not None for b in blocks):
+        # every block reads the original context: one input, its gradient summed in the op
+        spec = _chain.make_spec(blocks, context_mask, shared=True)
+        return (yield (spec, x, [context], blocks))
     if _mergeable_context_paths(blocks, context):
         ctxs, evs = _merged_context_paths(blocks, context, context_mask)
     else:
         ctxs, evs = _context_paths(blocks, context, context_mask)
+    if chain:
+        for ev in evs:
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
+        spec = _chain.make_spec(blocks, context_mask, shared=False)
+        return (yield (spec, x, ctxs, blocks))
+    yield None
+    return _encoder_stack_ops(blocks, x, context_mask, x_qkv, ctxs, evs)
+
+
+def _encoder_stack_ops(blocks, x, context_mask, x_qkv, ctxs, evs):
+    """The per-block encoder path (PRE / cross-attention / POST launches)."""
+    b0 = blocks[0].self_attn
     qkv = _ops.linear(x if x_qkv is None else x_qkv, b0.in_proj_weight, b0.in_proj_bias)
     for i, blk in enumerate(blocks):
         p = blk.dropout.p if blk.training else 0.0

@@ -35,9 +35,14 @@ def _deps_mtime():
     return max(os.path.getmtime(p) for p in paths)
 
 
-def _compile(src):
-    obj = os.path.join(OBJDIR, os.path.basename(src)[:-4] + ".o")
-    cmd = [HIPCC, "-c", *CFLAGS, "-o", obj, src]
+def _compile(src, extra=(), obj=None):
+    obj = obj or os.path.join(OBJDIR, os.path.basename(src)[:-4] + ".o")
+    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hdrs.append(os.path.join(ROOT, "include", "vaesne_hip.h"))
+    if not extra and os.path.exists(obj) and \
+            os.path.getmtime(obj) >= max(os.path.getmtime(p) for p in [src] + hdrs):
+        return obj          # object newer than its source and every header
+    cmd = [HIPCC, "-c", *CFLAGS, *extra, "-o", obj, src]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
@@ -63,6 +68,23 @@ def build(force=False, verbose=True):
     if verbose:
         print(f"[vaesne] built {LIB}")
     return LIB
+
+
+def build_profile_lib(out):
+    """A variant of the library whose fused encoder-chain kernels record per-phase
+    timestamps (VAESNE_CHAIN_PROFILE; tools/chain_phases.py).  Not the product."""
+    os.makedirs(OBJDIR, exist_ok=True)
+    srcs = sources()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(_compile, srcs))
+    prof = _compile(os.path.join(CSRC, "enc_chain.hip"), extra=["-DVAESNE_CHAIN_PROFILE"],
+                    obj=os.path.join(OBJDIR, "enc_chain_prof.o"))
+    objs = [prof if o.endswith("enc_chain.o") else o for o in objs]
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", out, *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    return out
 
 
 if __name__ == "__main__":
