@@ -232,6 +232,40 @@ int vaesne_enc_block_bwd(int mode, const float* x, const float* O, int M, const 
                          const uint32_t* drop_masks, float* dx, float* dO, float* gflat,
                          float* workspace, vaesne_colsum_list* defer, void* stream);
 
+/* ---- grouped linears ------------------------------------------------------------
+ * G <= 8 independent token-wise linears of ONE shape in one launch (the encoder blocks'
+ * context self-attention in / out projections and context k | v projections: one per
+ * block, util_layers.py:297,301; GroupLinearFn / the fused encoder chain).
+ *   fwd:      y[M, N] (+)= x[M, K] W[N, K]^T + b        (accum: add into y)
+ *   bwd_data: y[M, K] (+)= x[M, N] W[N, K]               (x = dy, y = dx)
+ *   bwd_weight: dW[O, I] = dy^T x, db[O] = colsum(dy) per group, all groups M rows;
+ *     workspace sized by vaesne_linear_bwd_weight_group_workspace; sums now or deferred. */
+typedef struct vaesne_linear_group {
+  const float* x;
+  int64_t ldx;
+  const float* W;
+  const float* b;
+  float* y;
+  int64_t ldy;
+  int64_t M;
+  int accum;
+} vaesne_linear_group;
+typedef struct vaesne_wgrad_group {
+  const float* dy;
+  int64_t lddy;
+  const float* x;
+  int64_t ldx;
+  float* dW;
+  float* db;
+} vaesne_wgrad_group;
+int vaesne_linear_fwd_group(int G, const vaesne_linear_group* groups, int K, int N, void* stream);
+int vaesne_linear_bwd_data_group(int G, const vaesne_linear_group* groups, int K, int N,
+                                 void* stream);
+int64_t vaesne_linear_bwd_weight_group_workspace(int G, int64_t M, int O, int I);
+int vaesne_linear_bwd_weight_group(int G, const vaesne_wgrad_group* groups, int64_t M, int O,
+                                   int I, float* workspace, vaesne_colsum_list* defer,
+                                   void* stream);
+
 /* ---- fused encoder latent chain -------------------------------------------------
  * Every TransformerBlock of an encoder's latent side in ONE forward and ONE backward
  * launch: photometricTransformerEncoder / spectraTransformerEncoder's block loop

@@ -30,11 +30,16 @@ class photometricTransformerDecoder(nn.Module):
         self.get_photo = singlelayerMLP(model_dim, 1)
         self.donotmask = donotmask
 
-    def forward(self, time, band, bottleneck, mask=None):
+    def forward(self, time, band, bottleneck, mask=None, repeat=1):
+        """`repeat` > 1: time / band hold the B distinct rows of the N = repeat * B
+        sequences (PhotometricVAE.py:190-193 expand): the embedding runs on the B rows
+        and is broadcast (its gradient summed over the copies)."""
         if self.donotmask:
             mask = None
         # x = time_embd + band_embd (PhotometricLayers.py:62-64), the add fused in the gather
         x = _ops.embedding(band, self.bandembd.weight, base=self.sinusoidal_time_embd(time))
+        if repeat > 1:
+            x = _ops.repeat_batch(x, repeat).reshape(repeat * x.shape[0], *x.shape[1:])
         # x feeds the first block twice and the head: one gradient sum (_ops.fanout)
         x_res, x_qkv, x_out = _ops.fanout(x, 3)
         bottleneck = self.contextfc(bottleneck)

@@ -44,11 +44,11 @@ class PhotometricDec(nn.Module):
         self.generativetransformer = photometricTransformerDecoder(
             latent_dim, num_bands, model_dim, num_heads, ff_dim, num_layers, dropout, selfattn)
 
-    def pxz(self, time, band, z, mask=None):
-        return self.generativetransformer(time, band, z, mask)
+    def pxz(self, time, band, z, mask=None, repeat=1):
+        return self.generativetransformer(time, band, z, mask, repeat=repeat)
 
-    def forward(self, time, band, z, mask=None):
-        x_rec = self.pxz(time, band, z, mask)
+    def forward(self, time, band, z, mask=None, repeat=1):
+        x_rec = self.pxz(time, band, z, mask, repeat=repeat)
         if mask is None:
             var = torch.ones_like(x_rec)
         else:
@@ -119,8 +119,9 @@ class PhotometricVAE(VAE):
         K = zs.shape[0]
         B, L = time.shape
         rep = lambda t: t.unsqueeze(0).unsqueeze(0).expand(K, groups, B, L).reshape(-1, L)
-        loc, scale = self.dec(rep(time), rep(band), zs.reshape(-1, zs.shape[-2], zs.shape[-1]),
-                              None if mask is None else rep(mask))
+        # the time / band embedding runs once per distinct light curve (repeat = K * groups)
+        loc, scale = self.dec(time, band, zs.reshape(-1, zs.shape[-2], zs.shape[-1]),
+                              None if mask is None else rep(mask), repeat=K * groups)
         return loc.reshape(K, groups * B, L), scale.reshape(K, groups * B, L)
 
     def reconstruct(self, x, K=1):

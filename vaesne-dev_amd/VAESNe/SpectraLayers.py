@@ -30,8 +30,14 @@ class spectraTransformerDecoder(nn.Module):
         self.contextfc = MLP(bottleneck_dim, model_dim, [model_dim])
         self.get_flux = singlelayerMLP(model_dim, 1)
 
-    def forward(self, wavelength, phase, bottleneck, mask=None):
+    def forward(self, wavelength, phase, bottleneck, mask=None, repeat=1):
+        """`repeat` > 1: wavelength holds the B distinct rows of the N = repeat * B
+        sequences (the decoders' K-sample / two-latent expand, SpectraVAE.py:189-192):
+        the embedding MLP runs on the B rows and is broadcast (its gradient is the
+        sum over the copies), the rest of the decoder on N."""
         x = self.wavelength_embd_layer(wavelength)
+        if repeat > 1:
+            x = _ops.repeat_batch(x, repeat).reshape(repeat * x.shape[0], *x.shape[1:])
         phase_embd = self.phase_embd_layer(phase[:, None])
         # x feeds the first block twice and the head: one gradient sum (_ops.fanout)
         x_res, x_qkv, x_out = _ops.fanout(x, 3)

@@ -43,11 +43,11 @@ class SpectraDec(nn.Module):
         self.generativetransformer = spectraTransformerDecoder(
             latent_dim, model_dim, num_heads, ff_dim, num_layers, dropout, selfattn)
 
-    def pxz(self, wavelength, phase, z, mask=None):
-        return self.generativetransformer(wavelength, phase, z, mask)
+    def pxz(self, wavelength, phase, z, mask=None, repeat=1):
+        return self.generativetransformer(wavelength, phase, z, mask, repeat=repeat)
 
-    def forward(self, wavelength, phase, z, mask=None):
-        x_rec = self.pxz(wavelength, phase, z, mask)
+    def forward(self, wavelength, phase, z, mask=None, repeat=1):
+        x_rec = self.pxz(wavelength, phase, z, mask, repeat=repeat)
         if mask is None:
             var = torch.ones_like(x_rec)
         else:
@@ -125,10 +125,11 @@ class SpectraVAE(VAE):
         K = zs.shape[0]
         B, L = wavelength.shape
         rep = lambda t: t.unsqueeze(0).unsqueeze(0).expand(K, groups, B, L).reshape(-1, L)
-        loc, scale = self.dec(rep(wavelength),
+        # the wavelength embedding runs once per distinct spectrum (repeat = K * groups)
+        loc, scale = self.dec(wavelength,
                               phase.unsqueeze(0).unsqueeze(0).expand(K, groups, B).reshape(-1),
                               zs.reshape(-1, zs.shape[-2], zs.shape[-1]),
-                              None if mask is None else rep(mask))
+                              None if mask is None else rep(mask), repeat=K * groups)
         return loc.reshape(K, groups * B, L), scale.reshape(K, groups * B, L)
 
     def generate(self, N, x):

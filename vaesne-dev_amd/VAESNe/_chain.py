@@ -23,6 +23,7 @@ import ctypes as C
 import torch
 
 from . import _defer, _lib, rng
+from . import _ops
 from ._ops import _ws, key_bias_of
 from ._lib import lib, ptr, stream
 
@@ -131,6 +132,7 @@ class EncChainFn(torch.autograd.Function):
         per = []
         pos = 0
         outs = []
+        kv_rows = []
         for gi, sp in enumerate(specs):
             nb = sp.nb
             x0 = flat[pos]
@@ -149,12 +151,11 @@ class EncChainFn(torch.autograd.Function):
                 raise RuntimeError("EncChainFn: every context must be [B, Lk, 32]")
             dev = x0.device
             kv = torch.empty((nb, B, Lk, 2 * E), dtype=torch.float32, device=dev)
-            for blk in range(nb):
+            for blk in range(nb):      # the k | v projections: one grouped launch below
                 c = ctxs[0 if sp.shared else blk]
                 Wc, bc = params[18 * blk + 6], params[18 * blk + 7]
-                lib.linear_fwd(c.data_ptr(), E, None, 0, B * Lk, E, Wc.data_ptr() + 4 * E * E,
-                               bc.data_ptr() + 4 * E, 2 * E, kv[blk].data_ptr(), 2 * E, None, 0,
-                               0, 0, s)
+                kv_rows.append((c.data_ptr(), E, Wc.data_ptr() + 4 * E * E, bc.data_ptr() + 4 * E,
+                                kv[blk].data_ptr(), 2 * E, B * Lk, 0))
             y = torch.empty((B, T, E), dtype=torch.float32, device=dev)
             save = torch.empty((B, nb, save_blk), dtype=torch.float32, device=dev)
             st = rng.state(dev) if any(p > 0 for p in sp.probs) else None
@@ -174,6 +175,9 @@ class EncChainFn(torch.autograd.Function):
             g.x0, g.y, g.save = x0.data_ptr(), y.data_ptr(), save.data_ptr()
             per.append((sp, B, T, Lk, nctx, ctxs, params, kv, save, st, kb, x0.shape))
             outs.append(y)
+        for i in range(0, len(kv_rows), 8):
+            chunk = kv_rows[i:i + 8]
+            lib.linear_fwd_group(len(chunk), _ops.lin_groups(chunk), E, 2 * E, s)
         lib.enc_chain_fwd(G, groups, s)
         ctx.per = [(sp, B, T, Lk, nctx, xs) for sp, B, T, Lk, nctx, _, _, _, _, _, _, xs in per]
         tensors = []
@@ -216,8 +220,8 @@ class EncChainFn(torch.autograd.Function):
             need_p = ng[pos_in + 1 + nctx:pos_in + 1 + nctx + 18 * nb]
             all_params += params
             all_out += [gv if n else None for gv, n in zip(gviews, need_p)]
-            wsk = [_ws(lib.linear_bwd_weight_workspace(B * Lk, 2 * E, E), dev) for _ in range(nb)]
-            keep += [wpart, gflat] + wsk
+            wsk = _ws(lib.linear_bwd_weight_group_workspace(nb, B * Lk, 2 * E, E), dev)
+            keep += [wpart, gflat, wsk]
             g = groups[gi]
             for blk in range(nb):
                 for j in range(18):
@@ -239,35 +243,36 @@ class EncChainFn(torch.autograd.Function):
             work.append((sp, B, Lk, nctx, ctxs, params, dkv, gflat, gviews, wsk, dx0, dy))
             pos_in += 1 + nctx + 18 * nb
         dfr = _defer.target(all_params, all_out, keep, entries=sum(
-            4 * w[0].nb + 2 for w in work) + 2)
+            5 * w[0].nb + 2 for w in work) + 2)
         lib.enc_chain_bwd(G, groups, dfr, s)
         grads = []
         for sp, B, Lk, nctx, ctxs, params, dkv, gflat, gviews, wsk, dx0, dy in work:
             nb = sp.nb
             M = B * Lk
-            for blk in range(nb):
+            rows = []
+            for blk in range(nb):       # k | v projection weight gradients, in place in gflat
                 c = ctxs[0 if sp.shared else blk]
                 o = blk * pblk + offs[6]
-                lib.linear_bwd_weight(dkv[blk].data_ptr(), 2 * E, None, 0, 0, c.data_ptr(), E,
-                                      None, 0, M, 2 * E, E, gflat.data_ptr() + 4 * (o + E * E),
-                                      gflat.data_ptr() + 4 * (blk * pblk + offs[7] + E), 0,
-                                      wsk[blk].data_ptr(), dfr, s)
+                rows.append((dkv[blk].data_ptr(), 2 * E, c.data_ptr(), E,
+                             gflat.data_ptr() + 4 * (o + E * E),
+                             gflat.data_ptr() + 4 * (blk * pblk + offs[7] + E)))
+            lib.linear_bwd_weight_group(nb, _ops.wgt_groups(rows), M, 2 * E, E, wsk.data_ptr(),
+                                        dfr, s)
             if sp.shared:
+                # dctx = sum_blk dkv_blk Wkv_blk: per-block products in one launch, then one
+                # fixed-order sum over the blocks
+                part = torch.empty((nb, M, E), dtype=torch.float32, device=kv.device)
+                rows = [(dkv[blk].data_ptr(), 2 * E, params[18 * blk + 6].data_ptr() + 4 * E * E,
+                         None, part[blk].data_ptr(), E, M, 0) for blk in range(nb)]
+                lib.linear_bwd_data_group(nb, _ops.lin_groups(rows), E, 2 * E, s)
                 dctx = torch.empty_like(ctxs[0])
-                for blk in range(nb):   # dctx = sum_blk dkv_blk Wkv_blk, in block order
-                    Wc = params[18 * blk + 6]
-                    lib.linear_bwd_data(dkv[blk].data_ptr(), 2 * E, None, 0, 0, M, 2 * E,
-                                        Wc.data_ptr() + 4 * E * E, E, dctx.data_ptr(), E,
-                                        int(blk > 0), s)
+                lib.sum_leading(part.data_ptr(), nb, M * E, dctx.data_ptr(), 0, s)
                 dctxs = [dctx]
             else:
-                dctxs = []
-                for blk in range(nb):
-                    Wc = params[18 * blk + 6]
-                    d = torch.empty_like(ctxs[blk])
-                    lib.linear_bwd_data(dkv[blk].data_ptr(), 2 * E, None, 0, 0, M, 2 * E,
-                                        Wc.data_ptr() + 4 * E * E, E, d.data_ptr(), E, 0, s)
-                    dctxs.append(d)
+                dctxs = [torch.empty_like(ctxs[blk]) for blk in range(nb)]
+                rows = [(dkv[blk].data_ptr(), 2 * E, params[18 * blk + 6].data_ptr() + 4 * E * E,
+                         None, dctxs[blk].data_ptr(), E, M, 0) for blk in range(nb)]
+                lib.linear_bwd_data_group(nb, _ops.lin_groups(rows), E, 2 * E, s)
             grads += [dx0] + dctxs + gviews
         out = [None]
         for i, gr in enumerate(grads):

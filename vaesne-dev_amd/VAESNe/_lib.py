@@ -61,6 +61,10 @@ SIGNATURES = {
     "vaesne_enc_block_fwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P]),
     "vaesne_enc_block_bwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P, P, P, P, P, P,
                                    P]),
+    "vaesne_linear_fwd_group": (I32, [I32, P, I32, I32, P]),
+    "vaesne_linear_bwd_data_group": (I32, [I32, P, I32, I32, P]),
+    "vaesne_linear_bwd_weight_group_workspace": (I64, [I32, I64, I32, I32]),
+    "vaesne_linear_bwd_weight_group": (I32, [I32, P, I64, I32, I32, P, P, P]),
     "vaesne_enc_chain_layout": (I32, [P, P, P]),
     "vaesne_enc_chain_fwd": (I32, [I32, P, P]),
     "vaesne_enc_chain_bwd": (I32, [I32, P, P, P]),

@@ -186,11 +186,39 @@ def in_proj_pair(query, key, weight, bias):
     return InProjPairFn.apply(query, key, weight, bias)
 
 
+class LinGroup(C.Structure):
+    """vaesne_linear_group (include/vaesne_hip.h)"""
+    _fields_ = [("x", C.c_void_p), ("ldx", C.c_int64), ("W", C.c_void_p), ("b", C.c_void_p),
+                ("y", C.c_void_p), ("ldy", C.c_int64), ("M", C.c_int64), ("accum", C.c_int)]
+
+
+class WgtGroup(C.Structure):
+    """vaesne_wgrad_group"""
+    _fields_ = [("dy", C.c_void_p), ("lddy", C.c_int64), ("x", C.c_void_p), ("ldx", C.c_int64),
+                ("dW", C.c_void_p), ("db", C.c_void_p)]
+
+
+def lin_groups(rows):
+    """rows: (x_ptr, ldx, W_ptr, b_ptr, y_ptr, ldy, M, accum) per group -> ctypes array"""
+    arr = (LinGroup * len(rows))()
+    for g, r in zip(arr, rows):
+        g.x, g.ldx, g.W, g.b, g.y, g.ldy, g.M, g.accum = r
+    return arr
+
+
+def wgt_groups(rows):
+    arr = (WgtGroup * len(rows))()
+    for g, r in zip(arr, rows):
+        g.dy, g.lddy, g.x, g.ldx, g.dW, g.db = r
+    return arr
+
+
 class GroupLinearFn(torch.autograd.Function):
-    """G token-wise linears with their own (W_g, b_g), stacked batch-major, one
-    launch per group: the encoder blocks' context self-attention projections
-    (util_layers.py:297, once per block on the same context), so the G attention
-    cores run as ONE launch over G*B sequences (util_layers.encoder_stack).
+    """G token-wise linears with their own (W_g, b_g), stacked batch-major, ONE
+    launch for all groups (vaesne_linear_*_group): the encoder blocks' context
+    self-attention projections (util_layers.py:297, once per block on the same
+    context), so the G attention cores run as ONE launch over G*B sequences
+    (util_layers.encoder_stack).
       shared:     x [*, K]    -> y [G, *, N],          y[g] = x W_g^T + b_g
       not shared: x [G, *, K] -> (y_0, .., y_{G-1}),   y_g [*, N] = x[g] W_g^T + b_g
     Parameter gradients are per group (deferred sums as LinearFn's)."""
@@ -208,22 +236,22 @@ class GroupLinearFn(torch.autograd.Function):
             raise RuntimeError("GroupLinearFn: every W_g must be [N, K] with K = x.shape[-1]")
         if not shared and x.shape[0] != G:
             raise RuntimeError("GroupLinearFn: stacked input must be [G, *, K]")
+        if G > 8:
+            raise RuntimeError("GroupLinearFn: at most 8 groups per launch")
         x = x.contiguous()
         lead = x.shape[:-1] if shared else x.shape[1:-1]
         M = math.prod(lead)
         Wc = [W.contiguous() for W in Ws]
         dev = x.device
-        s = stream()
         if shared:
             y = torch.empty((G, M, N), dtype=torch.float32, device=dev)
             outs = [y.data_ptr() + 4 * g * M * N for g in range(G)]
         else:
             ys = [torch.empty((M, N), dtype=torch.float32, device=dev) for _ in range(G)]
             outs = [t.data_ptr() for t in ys]
-        for g in range(G):
-            xp = x.data_ptr() + (0 if shared else 4 * g * M * K)
-            lib.linear_fwd(xp, K, None, 0, M, K, Wc[g].data_ptr(), ptr(bs[g]), N, outs[g], N,
-                           None, 0, 0, 0, s)
+        rows = [(x.data_ptr() + (0 if shared else 4 * g * M * K), K, Wc[g].data_ptr(), ptr(bs[g]),
+                 outs[g], N, M, 0) for g in range(G)]
+        lib.linear_fwd_group(G, lin_groups(rows), K, N, stream())
         ctx.meta = (G, M, K, N, bool(shared), x.shape, tuple(b is not None for b in bs))
         ctx.save_for_backward(x, *Wc)
         if shared:
@@ -240,39 +268,38 @@ class GroupLinearFn(torch.autograd.Function):
         if shared:
             dy = dys[0].contiguous()
             dyp = [dy.data_ptr() + 4 * g * M * N for g in range(G)]
-            keep = [dy]
         else:
-            keep = [None if d is None else d.contiguous() for d in dys]
-            dyp = [None if d is None else d.data_ptr() for d in keep]
+            keep = [torch.zeros((M, N), dtype=torch.float32, device=dev) if d is None
+                    else d.contiguous() for d in dys]
+            dyp = [d.data_ptr() for d in keep]
         dx = None
         if ng[0]:
             if shared:
+                # dx = sum_g dy[g] W_g, in group order (accumulating launches)
                 dx = torch.empty((M, K), dtype=torch.float32, device=dev)
-                for g in range(G):   # dx = sum_g dy[g] W_g, in group order
+                for g in range(G):
                     lib.linear_bwd_data(dyp[g], N, None, 0, 0, M, N, Wc[g].data_ptr(), K,
                                         dx.data_ptr(), K, int(g > 0), s)
             else:
                 dx = torch.empty((G, M, K), dtype=torch.float32, device=dev)
-                for g in range(G):
-                    if dyp[g] is None:
-                        dx[g].zero_()
-                    else:
-                        lib.linear_bwd_data(dyp[g], N, None, 0, 0, M, N, Wc[g].data_ptr(), K,
-                                            dx.data_ptr() + 4 * g * M * K, K, 0, s)
+                rows = [(dyp[g], N, Wc[g].data_ptr(), None, dx.data_ptr() + 4 * g * M * K, K, M, 0)
+                        for g in range(G)]
+                lib.linear_bwd_data_group(G, lin_groups(rows), K, N, s)
             dx = dx.view(xshape)
         grads = [None] * (2 * G)
-        for g in range(G):
-            if dyp[g] is None or not (ng[2 + 2 * g] or ng[3 + 2 * g]):
-                continue
-            dW = torch.empty((N, K), dtype=torch.float32, device=dev)
-            db = torch.empty((N,), dtype=torch.float32, device=dev) if has_b[g] else None
-            ws = _ws(lib.linear_bwd_weight_workspace(M, N, K), dev)
-            dfr = _defer.target(ctx.params[2 * g:2 * g + 2], (dW, db), (ws,))
-            xp = x.data_ptr() + (0 if shared else 4 * g * M * K)
-            lib.linear_bwd_weight(dyp[g], N, None, 0, 0, xp, K, None, 0, M, N, K, dW.data_ptr(),
-                                  ptr(db), 0, ws.data_ptr(), dfr, s)
-            grads[2 * g] = dW if ng[2 + 2 * g] else None
-            grads[2 * g + 1] = db if ng[3 + 2 * g] else None
+        if any(ng[2:]):
+            dWs = [torch.empty((N, K), dtype=torch.float32, device=dev) for _ in range(G)]
+            dbs = [torch.empty((N,), dtype=torch.float32, device=dev) if has_b[g] else None
+                   for g in range(G)]
+            ws = _ws(lib.linear_bwd_weight_group_workspace(G, M, N, K), dev)
+            outs = [t for pair in zip(dWs, dbs) for t in pair]
+            dfr = _defer.target(ctx.params, outs, (ws,), entries=2 * G + 2)
+            rows = [(dyp[g], N, x.data_ptr() + (0 if shared else 4 * g * M * K), K,
+                     dWs[g].data_ptr(), ptr(dbs[g])) for g in range(G)]
+            lib.linear_bwd_weight_group(G, wgt_groups(rows), M, N, K, ws.data_ptr(), dfr, s)
+            for g in range(G):
+                grads[2 * g] = dWs[g] if ng[2 + 2 * g] else None
+                grads[2 * g + 1] = dbs[g] if ng[3 + 2 * g] else None
         return (dx, None, *grads)
 
 

@@ -611,19 +611,30 @@ __global__ __launch_bounds__(NT) void enc_chain_bwd_kernel(Args args) {
       float dqa[DH];
 #pragma unroll
       for (int d = 0; d < DH; ++d) dqa[d] = 0.f;
+      // this lane's k | v row slices of the next tile are loaded while the current
+      // tile is computed
+      float4 pk0, pk1, pv0, pv1;
+      float pkb;
+      auto load_kv = [&](int j) {
+        pk0 = pk1 = pv0 = pv1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        pkb = 0.f;
+        if (j < a.Lk) {
+          const float* r = kvb + (int64_t)j * 2 * E + h * DH;
+          pk0 = *reinterpret_cast<const float4*>(r);
+          pk1 = *reinterpret_cast<const float4*>(r + 4);
+          pv0 = *reinterpret_cast<const float4*>(r + E);
+          pv1 = *reinterpret_cast<const float4*>(r + E + 4);
+          if (kbp) pkb = kbp[j];
+        }
+      };
+      load_kv(jl);
       for (int j0 = 0; j0 < a.Lk; j0 += KTB) {
         const int j = j0 + jl;
         const bool kok = j < a.Lk;
         float k[DH], v[DH], dk[DH], dv[DH];
+        const float kb = pkb;
         {
-          float4 k0 = make_float4(0.f, 0.f, 0.f, 0.f), k1 = k0, v0 = k0, v1 = k0;
-          if (kok) {
-            const float* r = kvb + (int64_t)j * 2 * E + h * DH;
-            k0 = *reinterpret_cast<const float4*>(r);
-            k1 = *reinterpret_cast<const float4*>(r + 4);
-            v0 = *reinterpret_cast<const float4*>(r + E);
-            v1 = *reinterpret_cast<const float4*>(r + E + 4);
-          }
+          const float4 k0 = pk0, k1 = pk1, v0 = pv0, v1 = pv1;
           k[0] = k0.x; k[1] = k0.y; k[2] = k0.z; k[3] = k0.w;
           k[4] = k1.x; k[5] = k1.y; k[6] = k1.z; k[7] = k1.w;
           v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
@@ -631,9 +642,9 @@ __global__ __launch_bounds__(NT) void enc_chain_bwd_kernel(Args args) {
           *reinterpret_cast<float4*>(S.Kt + jl * E + h * DH) = k0;
           *reinterpret_cast<float4*>(S.Kt + jl * E + h * DH + 4) = k1;
         }
+        if (j0 + KTB < a.Lk) load_kv(j + KTB);
 #pragma unroll
         for (int d = 0; d < DH; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
-        const float kb = (kok && kbp) ? kbp[j] : 0.f;
         for (int i = 0; i < T; ++i) {
           const int q = i * 4 + h;
           const float4 qa0 = *reinterpret_cast<const float4*>(S.SV + S_QS + i * E + h * DH);

@@ -143,7 +143,7 @@ __device__ __forceinline__ void store_feat(const LinArgs& p, int64_t row, int nb
 // 32x32 block, output straight in the feature layout (no shuffles).  The
 // weight (zero padded to kbn x nbn blocks of 32) is staged once per workgroup.
 template <bool VIN, bool VOUT>
-__global__ __launch_bounds__(NT) void linear_kernel(LinArgs p, int kbn, int nbn) {
+__device__ __forceinline__ void linear_body(const LinArgs& p, int kbn, int nbn) {
   extern __shared__ float smem[];
   const int LDW = kbn * 32 + 1;             // odd row stride: conflict-free A reads
   float* Ws = smem;                         // [nbn*32][LDW]: Ws[n][k] = W(n, k)
@@ -185,26 +185,57 @@ __global__ __launch_bounds__(NT) void linear_kernel(LinArgs p, int kbn, int nbn)
   }
 }
 
+template <bool VIN, bool VOUT>
+__global__ __launch_bounds__(NT) void linear_kernel(LinArgs p, int kbn, int nbn) {
+  linear_body<VIN, VOUT>(p, kbn, nbn);
+}
+
+// up to LGMAX independent linears with the same (K, N) in one launch: blockIdx.z
+// selects the group (the encoder blocks' context projections, G = 4)
+constexpr int LGMAX = 8;
+struct LinGroup {
+  LinArgs p[LGMAX];
+};
+template <bool VIN, bool VOUT>
+__global__ __launch_bounds__(NT) void linear_group_kernel(LinGroup g, int kbn, int nbn) {
+  linear_body<VIN, VOUT>(g.p[blockIdx.z], kbn, nbn);
+}
+
 bool al16(const void* q, int64_t ld) { return ((uintptr_t)q % 16 == 0) && (ld % 4 == 0); }
 
-int launch_linear(const LinArgs& p, hipStream_t s) {
-  if (p.K < 1 || p.K > MAXK || p.N < 1 || p.N > MAXN) return (int)hipErrorInvalidValue;
-  if (p.M <= 0) return 0;
+// G == 0: one linear (p[0]); G >= 1: a grouped launch over p[0..G) (same K, N)
+int launch_linear_n(const LinArgs* pp, int G, hipStream_t s) {
+  const LinArgs& p = pp[0];
+  if (p.K < 1 || p.K > MAXK || p.N < 1 || p.N > MAXN || G > LGMAX) return (int)hipErrorInvalidValue;
+  int64_t Mmax = p.M;
+  for (int g = 1; g < G; ++g) {
+    if (pp[g].K != p.K || pp[g].N != p.N) return (int)hipErrorInvalidValue;
+    Mmax = pp[g].M > Mmax ? pp[g].M : Mmax;
+  }
+  if (Mmax <= 0) return 0;
   const int kbn = (p.K + 31) / 32, nbn = (p.N + 31) / 32;
-  const int64_t tiles = (p.M + 31) / 32;
+  const int64_t tiles = (Mmax + 31) / 32;
   const int64_t wg = (tiles + NT / 64 - 1) / (NT / 64);
   const int grid = (int)(wg < 2048 ? wg : 2048);
   const size_t shmem = sizeof(float) * ((size_t)nbn * 32 * (kbn * 32 + 1) + nbn * 32);
-  const bool vin = (p.K % 4 == 0) && al16(p.a, p.lda) && (!p.a2 || al16(p.a2, p.lda2)) &&
-                   (!p.act_in_grad || al16(p.zin, p.ldzin));
-  const bool vout = (p.N % 4 == 0) && al16(p.out, p.ldo) && (!p.zout || al16(p.zout, p.ldzo));
+  bool vin = true, vout = true;
+  for (int g = 0; g < (G ? G : 1); ++g) {
+    const LinArgs& q = pp[g];
+    vin = vin && (q.K % 4 == 0) && al16(q.a, q.lda) && (!q.a2 || al16(q.a2, q.lda2)) &&
+          (!q.act_in_grad || al16(q.zin, q.ldzin));
+    vout = vout && (q.N % 4 == 0) && al16(q.out, q.ldo) && (!q.zout || al16(q.zout, q.ldzo));
+  }
   if (shmem > 65536) {   // > 64 KB of LDS (K, N up to 128): opt in once per instantiation
     static bool opted = false;
     if (!opted) {
-      const void* fns[4] = {(const void*)linear_kernel<true, true>,
+      const void* fns[8] = {(const void*)linear_kernel<true, true>,
                             (const void*)linear_kernel<true, false>,
                             (const void*)linear_kernel<false, true>,
-                            (const void*)linear_kernel<false, false>};
+                            (const void*)linear_kernel<false, false>,
+                            (const void*)linear_group_kernel<true, true>,
+                            (const void*)linear_group_kernel<true, false>,
+                            (const void*)linear_group_kernel<false, true>,
+                            (const void*)linear_group_kernel<false, false>};
       for (const void* f : fns) {
         hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return (int)e;
@@ -212,17 +243,33 @@ int launch_linear(const LinArgs& p, hipStream_t s) {
       opted = true;
     }
   }
-  if (vin && vout)
-    hipLaunchKernelGGL((linear_kernel<true, true>), dim3(grid), dim3(NT), shmem, s, p, kbn, nbn);
-  else if (vin)
-    hipLaunchKernelGGL((linear_kernel<true, false>), dim3(grid), dim3(NT), shmem, s, p, kbn, nbn);
-  else if (vout)
-    hipLaunchKernelGGL((linear_kernel<false, true>), dim3(grid), dim3(NT), shmem, s, p, kbn, nbn);
-  else
-    hipLaunchKernelGGL((linear_kernel<false, false>), dim3(grid), dim3(NT), shmem, s, p, kbn, nbn);
+  if (G == 0) {
+    if (vin && vout)
+      hipLaunchKernelGGL((linear_kernel<true, true>), dim3(grid), dim3(NT), shmem, s, p, kbn, nbn);
+    else if (vin)
+      hipLaunchKernelGGL((linear_kernel<true, false>), dim3(grid), dim3(NT), shmem, s, p, kbn, nbn);
+    else if (vout)
+      hipLaunchKernelGGL((linear_kernel<false, true>), dim3(grid), dim3(NT), shmem, s, p, kbn, nbn);
+    else
+      hipLaunchKernelGGL((linear_kernel<false, false>), dim3(grid), dim3(NT), shmem, s, p, kbn, nbn);
+  } else {
+    LinGroup lg{};
+    for (int g = 0; g < G; ++g) lg.p[g] = pp[g];
+    const dim3 gd(grid, 1, G);
+    if (vin && vout)
+      hipLaunchKernelGGL((linear_group_kernel<true, true>), gd, dim3(NT), shmem, s, lg, kbn, nbn);
+    else if (vin)
+      hipLaunchKernelGGL((linear_group_kernel<true, false>), gd, dim3(NT), shmem, s, lg, kbn, nbn);
+    else if (vout)
+      hipLaunchKernelGGL((linear_group_kernel<false, true>), gd, dim3(NT), shmem, s, lg, kbn, nbn);
+    else
+      hipLaunchKernelGGL((linear_group_kernel<false, false>), gd, dim3(NT), shmem, s, lg, kbn, nbn);
+  }
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
+
+int launch_linear(const LinArgs& p, hipStream_t s) { return launch_linear_n(&p, 0, s); }
 
 // ---------------------------------------------------------------------------
 // backward weight
@@ -255,8 +302,8 @@ int64_t wgrad_groups(int64_t M) {
 // in flight at once; out-of-range terms are zeroed afterwards.  With G == 1
 // (gridDim.x) the workgroup writes dW / db directly (no column-sum pass).
 template <int ACT, bool X2>
-__global__ __launch_bounds__(NT) void linear_wgrad_kernel(WgtArgs p, int nib, float* dW, float* db,
-                                                          int accum) {
+__device__ __forceinline__ void wgrad_body(const WgtArgs& p, int nib, float* dW, float* db,
+                                           int accum) {
   __shared__ float red[NT / 64][1024 + 32];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 31, hh = lane >> 5;
@@ -317,6 +364,23 @@ __global__ __launch_bounds__(NT) void linear_wgrad_kernel(WgtArgs p, int nib, fl
       }
     }
   }
+}
+
+template <int ACT, bool X2>
+__global__ __launch_bounds__(NT) void linear_wgrad_kernel(WgtArgs p, int nib, float* dW, float* db,
+                                                          int accum) {
+  wgrad_body<ACT, X2>(p, nib, dW, db, accum);
+}
+
+struct WgtGroup {
+  WgtArgs p[LGMAX];
+  float* dW[LGMAX];
+  float* db[LGMAX];
+};
+template <int ACT, bool X2>
+__global__ __launch_bounds__(NT) void linear_wgrad_group_kernel(WgtGroup g, int nib, int accum) {
+  const int z = blockIdx.z;
+  wgrad_body<ACT, X2>(g.p[z], nib, g.dW[z], g.db[z], accum);
 }
 
 }  // namespace
@@ -386,4 +450,74 @@ VAESNE_API int vaesne_linear_bwd_weight(const float* dy, int64_t lddy, const flo
   if (!defer) return launch_colsum(workspace, G, F, dW, db, O * I, accum, s);
   const int rc = colsum_or_defer(defer, workspace, F, G, O * I, dW, accum, s);
   return rc ? rc : colsum_or_defer(defer, workspace + (int64_t)O * I, F, G, O, db, accum, s);
+}
+
+// ---------------------------------------------------------------------------
+// grouped launches (one kernel for G independent linears of one shape)
+// ---------------------------------------------------------------------------
+VAESNE_API int vaesne_linear_fwd_group(int G, const vaesne_linear_group* g, int K, int N,
+                                       void* stream) {
+  if (G < 1 || G > LGMAX || !g) return (int)hipErrorInvalidValue;
+  LinArgs pp[LGMAX];
+  for (int i = 0; i < G; ++i) {
+    LinArgs& p = pp[i];
+    p = LinArgs{};
+    p.a = g[i].x; p.lda = g[i].ldx; p.W = g[i].W; p.w_trans = 0; p.bias = g[i].b;
+    p.K = K; p.N = N; p.M = g[i].M;
+    p.out = g[i].y; p.ldo = g[i].ldy; p.accum = g[i].accum; p.act_out = ACT_NONE;
+  }
+  return launch_linear_n(pp, G, (hipStream_t)stream);
+}
+
+VAESNE_API int vaesne_linear_bwd_data_group(int G, const vaesne_linear_group* g, int K, int N,
+                                            void* stream) {
+  // per group: y[M, K] (+)= x[M, N] @ W[N, K]   (x = dy, y = dx)
+  if (G < 1 || G > LGMAX || !g) return (int)hipErrorInvalidValue;
+  LinArgs pp[LGMAX];
+  for (int i = 0; i < G; ++i) {
+    LinArgs& p = pp[i];
+    p = LinArgs{};
+    p.a = g[i].x; p.lda = g[i].ldx; p.W = g[i].W; p.w_trans = 1; p.bias = nullptr;
+    p.K = N; p.N = K; p.M = g[i].M;
+    p.out = g[i].y; p.ldo = g[i].ldy; p.accum = g[i].accum; p.act_out = ACT_NONE;
+  }
+  return launch_linear_n(pp, G, (hipStream_t)stream);
+}
+
+VAESNE_API int64_t vaesne_linear_bwd_weight_group_workspace(int G, int64_t M, int O, int I) {
+  return (int64_t)G * vaesne_linear_bwd_weight_workspace(M, O, I);
+}
+
+// per group: dW[O, I] = dy^T x, db[O] = colsum(dy) over M rows (every group the same M)
+VAESNE_API int vaesne_linear_bwd_weight_group(int G, const vaesne_wgrad_group* g, int64_t M, int O,
+                                              int I, float* workspace, vaesne_colsum_list* defer,
+                                              void* stream) {
+  if (G < 1 || G > LGMAX || !g || O < 1 || O > MAXN || I < 1 || I > MAXK || M <= 0)
+    return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const int F = O * I + O;
+  const int Gr = (int)wgrad_groups(M);
+  WgtGroup wg{};
+  for (int i = 0; i < G; ++i) {
+    wg.p[i] = WgtArgs{g[i].dy, g[i].lddy, nullptr, 0, 0, g[i].x, g[i].ldx, nullptr, 0, M, O, I,
+                      workspace + (int64_t)i * Gr * F};
+    wg.dW[i] = g[i].dW;
+    wg.db[i] = g[i].db;
+  }
+  const int nob = (O + 31) / 32, nib = (I + 31) / 32;
+  hipLaunchKernelGGL((linear_wgrad_group_kernel<ACT_NONE, false>), dim3(Gr, nob * nib, G), dim3(NT),
+                     0, s, wg, nib, 0);
+  VAESNE_CHECK_LAUNCH();
+  if (Gr == 1) return 0;   // written directly
+  for (int i = 0; i < G; ++i) {
+    const float* ws = workspace + (int64_t)i * Gr * F;
+    int rc;
+    if (!defer) rc = launch_colsum(ws, Gr, F, g[i].dW, g[i].db, O * I, 0, s);
+    else {
+      rc = colsum_or_defer(defer, ws, F, Gr, O * I, g[i].dW, 0, s);
+      if (!rc) rc = colsum_or_defer(defer, ws + (int64_t)O * I, F, Gr, O, g[i].db, 0, s);
+    }
+    if (rc) return rc;
+  }
+  return 0;
 }
