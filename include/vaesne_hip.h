@@ -172,31 +172,32 @@ int vaesne_attn_force_geometry(int nt, int np);
  * PhotometricLayers.py:66-67): out_proj -> +Drop -> LN1 -> cross-attention over
  * the Lc <= 8 context tokens (unmasked) -> out_proj -> +Drop -> LN2 -> FFN(GELU)
  * -> +Drop -> LN3 [-> the next block's packed in_proj].  E=32, H=4, dh=8, ff=32.
- * x, O, y: [M, 32] with M = Nseq * L; kvc [Nseq, Lc, 64] = context k | v;
+ * x, O, y: [M, 32] with M = Nseq * L; ctx [Nseq, Lc, 32] = the context tokens,
+ * projected to k | v inside the kernels (cross in_proj rows [32, 96));
  * w: HOST array of 18 device pointers {Wo1, bo1, g1, be1, Wq, bq, Wo2, bo2, g2,
- * be2, W1, b1, W2, b2, g3, be3, Wn, bn} (Wq/bq = cross in_proj rows [0, 32);
+ * be2, W1, b1, W2, b2, g3, be3, Wn, bn} (Wq/bq = the cross in_proj weight [96, 32] /
+ * bias [96]: rows [0, 32) project the queries, rows [32, 96) the context;
  * Wn/bn = next self in_proj [96, 32] / [96], null when not fused; qkv [M, 96]).
  * bwd: gflat = ONE device buffer receiving every parameter gradient of the
  * block at the offsets vaesne_dec_tail_grad_layout() reports (same order as w;
  * returns the buffer length, 10752 floats).  The Wq / bq regions span all 3E
- * rows of the cross in_proj (3072 / 96 floats): the kernel fills rows [0, E),
- * the caller's k | v projection gradient goes into rows [E, 3E) in place, so
- * the whole in_proj gradient is one view (the block's column sums never write
- * those rows, deferred or not).  dkvc is complete when the call's work ends.
+ * rows of the cross in_proj (3072 / 96 floats), k | v rows included: the whole
+ * in_proj gradient is one view.  dctx [Nseq, Lc, 32] receives the context tokens'
+ * gradient.
  * y = the forward output; dqkv
  * required iff Wn; workspace sized by vaesne_dec_tail_workspace.
  * drop_masks (nullable, p_drop > 0): uint32 [M][4] keep masks of the block's four
  * dropout sites, written by the forward and read by the backward instead of
  * re-hashing (16 bytes per token). */
 int64_t vaesne_dec_tail_workspace(int M, int L, int Lc);
-int vaesne_dec_tail_fwd(const float* x, const float* O, const float* kvc, int M, int L, int Lc,
+int vaesne_dec_tail_fwd(const float* x, const float* O, const float* ctx, int M, int L, int Lc,
                         const float* const* w, float p_drop, const int64_t* rng_state,
                         uint32_t call_id, float* y, float* qkv, uint32_t* drop_masks,
                         void* stream);
-int vaesne_dec_tail_bwd(const float* x, const float* O, const float* kvc, int M, int L, int Lc,
+int vaesne_dec_tail_bwd(const float* x, const float* O, const float* ctx, int M, int L, int Lc,
                         const float* const* w, float p_drop, const int64_t* rng_state,
                         uint32_t call_id, const float* y, const float* dy, const float* dqkv,
-                        const uint32_t* drop_masks, float* dx, float* dO, float* dkvc,
+                        const uint32_t* drop_masks, float* dx, float* dO, float* dctx,
                         float* gflat, float* workspace, vaesne_colsum_list* defer, void* stream);
 int vaesne_dec_tail_grad_layout(int* offsets);
 /* Test / tuning hook: the decoder-tail backward for sequences of >= 256 tokens runs as

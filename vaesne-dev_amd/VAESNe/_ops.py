@@ -1055,8 +1055,8 @@ STORE_TAIL_MASKS = True
 class DecTailFn(torch.autograd.Function):
     """(x, O, context, cross in_proj Wc [96, 32] / bc [96], 16 more block tensors)
     -> (y [, qkv_next]) for one decoder block.  The context's k|v projection
-    (rows [E, 3E) of Wc) runs inside, and the whole in_proj gradient is returned
-    as one tensor: no slice-gradient zero-fill / copy / add glue per block."""
+    (rows [E, 3E) of Wc) runs inside the tail kernels (forward and backward), and
+    the whole in_proj gradient is returned as one tensor."""
 
     @staticmethod
     def forward(ctx, L, p, x, O, context, Wc, bc, *w16):
@@ -1067,14 +1067,10 @@ class DecTailFn(torch.autograd.Function):
         Wc, bc = Wc.contiguous(), bc.contiguous()
         E = 32
         M = x.numel() // E
-        Nseq, Lc = context.shape[0], context.shape[1]
+        Lc = context.shape[1]
         dev = x.device
-        # kvc = context @ Wc[E:]^T + bc[E:]   ([Nseq, Lc, 64]; the reference's cross k/v proj)
-        kvc = torch.empty((Nseq, Lc, 2 * E), dtype=torch.float32, device=dev)
-        lib.linear_fwd(context.data_ptr(), E, None, 0, Nseq * Lc, E, Wc.data_ptr() + 4 * E * E,
-                       bc.data_ptr() + 4 * E, 2 * E, kvc.data_ptr(), 2 * E, None, 0, 0, 0, stream())
         w16 = [None if t is None else t.contiguous() for t in w16]
-        w = w16[:4] + [Wc, bc] + w16[4:]          # C-ABI order: Wq/bq = rows [0, E) of Wc/bc
+        w = w16[:4] + [Wc, bc] + w16[4:]          # C-ABI order: the whole cross in_proj
         nxt = w[16] is not None
         y = torch.empty((M, E), dtype=torch.float32, device=dev)
         qkv = torch.empty((M, 3 * E), dtype=torch.float32, device=dev) if nxt else None
@@ -1082,10 +1078,11 @@ class DecTailFn(torch.autograd.Function):
         cid = rng.next_call_id() if p > 0 else 0
         masks = torch.empty((M, 4), dtype=torch.int32, device=dev) \
             if p > 0 and STORE_TAIL_MASKS else None
-        lib.dec_tail_fwd(x.data_ptr(), O.data_ptr(), kvc.data_ptr(), M, L, Lc, _lib.ptr_array(w),
-                         float(p), ptr(st), cid, y.data_ptr(), ptr(qkv), ptr(masks), stream())
+        lib.dec_tail_fwd(x.data_ptr(), O.data_ptr(), context.data_ptr(), M, L, Lc,
+                         _lib.ptr_array(w), float(p), ptr(st), cid, y.data_ptr(), ptr(qkv),
+                         ptr(masks), stream())
         ctx.meta = (M, L, Lc, float(p), cid, nxt, x.shape)
-        ctx.save_for_backward(x, O, context, kvc, y, st, masks, *w)
+        ctx.save_for_backward(x, O, context, y, st, masks, *w)
         y = y.view(x.shape)
         if nxt:
             return y, qkv.view(*x.shape[:-1], 3 * E)
@@ -1093,7 +1090,7 @@ class DecTailFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, dqkv):
-        x, O, context, kvc, y, st, masks, *w = ctx.saved_tensors
+        x, O, context, y, st, masks, *w = ctx.saved_tensors
         M, L, Lc, p, cid, nxt, xshape = ctx.meta
         E = 32
         dev = x.device
@@ -1105,35 +1102,23 @@ class DecTailFn(torch.autograd.Function):
             dqkv = None
         dx = torch.empty_like(x)
         dO = torch.empty_like(O)
-        dkvc = torch.empty_like(kvc)
+        dctx = torch.empty_like(context)
         offs, total = _tail_layout()
         gflat = torch.empty(total, dtype=torch.float32, device=dev)
         ws = _ws(lib.dec_tail_workspace(M, L, Lc), dev)
-        Mc = context.shape[0] * Lc
-        wsk = _ws(lib.linear_bwd_weight_workspace(Mc, 2 * E, E), dev)
-        s = stream()
         ng = ctx.needs_input_grad
-        # every parameter gradient is a view of gflat; the full in_proj gradient
-        # too: rows [0, E) from the tail kernel, rows [E, 3E) written in place by
-        # the k|v projection's weight gradient
+        # every parameter gradient is a view of gflat, the whole cross in_proj's too
         gall = [gflat[o:o + t.numel()].view_as(t) if t is not None else None
                 for t, o in zip(w, offs)]
         gall[4] = gflat[offs[4]:offs[4] + 3 * E * E].view_as(w[4])
         gall[5] = gflat[offs[5]:offs[5] + 3 * E]
         need = [ng[7 + j] for j in range(4)] + [ng[5], ng[6]] + [ng[11 + j] for j in range(12)]
         gout = [g if n else None for g, n in zip(gall, need)]
-        dfr = _defer.target(ctx.params, gout, (ws, wsk, gflat))
-        lib.dec_tail_bwd(x.data_ptr(), O.data_ptr(), kvc.data_ptr(), M, L, Lc, _lib.ptr_array(w),
-                         p, ptr(st), cid, y.data_ptr(), dy.data_ptr(), ptr(dqkv), ptr(masks),
-                         dx.data_ptr(), dO.data_ptr(), dkvc.data_ptr(), gflat.data_ptr(),
-                         ws.data_ptr(), dfr, s)
-        Wc, dWc, dbc = w[4], gall[4], gall[5]
-        lib.linear_bwd_weight(dkvc.data_ptr(), 2 * E, None, 0, 0, context.data_ptr(), E, None, 0,
-                              Mc, 2 * E, E, dWc.data_ptr() + 4 * E * E, dbc.data_ptr() + 4 * E, 0,
-                              wsk.data_ptr(), dfr, s)
-        dctx = torch.empty_like(context)
-        lib.linear_bwd_data(dkvc.data_ptr(), 2 * E, None, 0, 0, Mc, 2 * E,
-                            Wc.data_ptr() + 4 * E * E, E, dctx.data_ptr(), E, 0, s)
+        dfr = _defer.target(ctx.params, gout, (ws, gflat))
+        lib.dec_tail_bwd(x.data_ptr(), O.data_ptr(), context.data_ptr(), M, L, Lc,
+                         _lib.ptr_array(w), p, ptr(st), cid, y.data_ptr(), dy.data_ptr(),
+                         ptr(dqkv), ptr(masks), dx.data_ptr(), dO.data_ptr(), dctx.data_ptr(),
+                         gflat.data_ptr(), ws.data_ptr(), dfr, stream())
         gw = gout[:4] + gout[6:]
         return (None, None, dx.view(xshape), dO, dctx, gout[4], gout[5], *gw)
 

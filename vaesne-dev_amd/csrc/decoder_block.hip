@@ -72,7 +72,9 @@ struct Tail {
   float* dx;           // [M, 32]
   float* dO;           // [M, 32]
   float* wpart;        // [G][WPART] per-workgroup partials (gflat itself when G == 1)
-  float* dkvc;         // [Nseq, Lc, 64] context k | v gradients (written per sequence)
+  float* dkvc;         // [Nseq, Lc, 64] context k | v gradients (two-kernel path scratch)
+  const float* ctx;    // [Nseq, Lc, 32] context tokens (k | v projected in the kernels)
+  float* dctx;         // [Nseq, Lc, 32] their gradient (backward)
   int mode;            // MODE_FULL (decoder block tail) / MODE_PRE / MODE_POST (encoder halves)
 };
 
@@ -93,6 +95,7 @@ struct __attribute__((aligned(16))) Smem {
   float bo1[E], bq[E], bo2[E], b1[E], b2[E], bn[3 * E];
   float g1[E], be1[E], g2[E], be2[E], g3[E], be3[E];
   float kv[LCMAX * 2 * E];
+  float ctxs[LCMAX * E];
 };
 
 __device__ void stage_w(float* dst, const float* src, int rows) {
@@ -110,6 +113,23 @@ __device__ void stage_all(Smem& S, const Tail& a, bool next) {
   stage_v(S.b1, a.b1, E); stage_v(S.b2, a.b2, E);
   stage_v(S.g1, a.g1, E); stage_v(S.be1, a.be1, E); stage_v(S.g2, a.g2, E);
   stage_v(S.be2, a.be2, E); stage_v(S.g3, a.g3, E); stage_v(S.be3, a.be3, E);
+}
+
+// The sequence's projected context k | v into S.kv: the cross in_proj rows [E, 3E)
+// (util_layers.py:301; a.Wq / a.bq point at row 0 of the in_proj weight / bias) on
+// its Lc <= 8 context tokens, which also land in S.ctxs.  512 outputs: weights read
+// straight from L2, no launch of their own.
+__device__ void ctx_kv(Smem& S, const Tail& a, int seq) {
+  for (int i = threadIdx.x; i < a.Lc * E; i += NT) S.ctxs[i] = a.ctx[(int64_t)seq * a.Lc * E + i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < a.Lc * 2 * E; i += NT) {
+    const int j = i >> 6, c = i & 63;
+    const float* w = a.Wq + (int64_t)(E + c) * E;
+    float acc = a.bq[E + c];
+#pragma unroll 8
+    for (int k = 0; k < E; ++k) acc = fmaf(S.ctxs[j * E + k], w[k], acc);
+    S.kv[i] = acc;
+  }
 }
 
 // y[r] = b[F(r,h)] + sum_k W[F(r,h)][k] x[k]      (x, y in feature layout)
@@ -276,7 +296,7 @@ __global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
   const int chunks = (a.L + a.chunk - 1) / a.chunk;
   const int seq = blockIdx.x / chunks, ch = blockIdx.x % chunks;
   stage_all(S, a, NEXT);
-  for (int i = threadIdx.x; i < a.Lc * 2 * E; i += NT) S.kv[i] = a.kvc[(int64_t)seq * a.Lc * 2 * E + i];
+  ctx_kv(S, a, seq);
   __syncthreads();
   const uint32_t key = DROP ? key_of(a.rng, a.call_id) : 0u;
   const int t0 = ch * a.chunk, t1 = min(a.L, t0 + a.chunk);
@@ -387,7 +407,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const int chunks = (a.L + a.chunk - 1) / a.chunk;
   const int seq = blockIdx.x / chunks, ch = blockIdx.x % chunks;
   stage_all(S, a, NEXT);
-  for (int i = threadIdx.x; i < a.Lc * 2 * E; i += NT) S.kv[i] = a.kvc[(int64_t)seq * a.Lc * 2 * E + i];
+  ctx_kv(S, a, seq);
   __syncthreads();
   const uint32_t key = DROP ? key_of(a.rng, a.call_id) : 0u;
   const float scale = 0.35355339059327373f;
@@ -1106,7 +1126,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
   const int seq = blockIdx.x;
   stage_all(S, a, NEXT);
-  for (int i = threadIdx.x; i < a.Lc * 2 * E; i += NT) S.kv[i] = a.kvc[(int64_t)seq * a.Lc * 2 * E + i];
+  ctx_kv(S, a, seq);
   __syncthreads();
   float* tX1 = Lt[wave];
   float* tC = tX1 + TILE;
@@ -1404,19 +1424,39 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     __syncthreads();
   }
   // context k | v gradients of this sequence: acc[f = F(r,h)][j' = lane&31] is valid
-  // where (j' & 3) == f >> 3, j = j' >> 2 < Lc
+  // where (j' & 3) == f >> 3, j = j' >> 2 < Lc.  Summed into S.kv (no longer read),
+  // then this sequence's share of the k | v projection backward: d context and the
+  // partials of the in_proj rows [E, 3E) (weights and biases).
   for (int kv = 0; kv < 2; ++kv) {
     const f16v& acc = kv ? aV : aK;
 #pragma unroll
     for (int r = 0; r < 16; ++r) red[wave * RS + F(r, h) * 32 + (lane & 31)] = acc[r];
     __syncthreads();
-    float* dk = a.dkvc + (int64_t)seq * a.Lc * 2 * E + (kv ? E : 0);
     for (int i = threadIdx.x; i < a.Lc * E; i += NT) {
       const int j = i / E, f = i % E;
       const int idx = f * 32 + 4 * j + (f >> 3);
-      dk[j * 2 * E + f] = ((red[idx] + red[RS + idx]) + red[2 * RS + idx]) + red[3 * RS + idx];
+      S.kv[j * 2 * E + (kv ? E : 0) + f] =
+          ((red[idx] + red[RS + idx]) + red[2 * RS + idx]) + red[3 * RS + idx];
     }
     __syncthreads();
+  }
+  for (int i = threadIdx.x; i < a.Lc * E; i += NT) {          // d context
+    const int j = i / E, k = i % E;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int c = 0; c < 2 * E; ++c) acc = fmaf(S.kv[j * 2 * E + c], a.Wq[(int64_t)(E + c) * E + k], acc);
+    a.dctx[((int64_t)seq * a.Lc + j) * E + k] = acc;
+  }
+  for (int i = threadIdx.x; i < 2 * E * E; i += NT) {         // dW rows [E, 3E)
+    const int c = i / E, k = i % E;
+    float acc = 0.f;
+    for (int j = 0; j < a.Lc; ++j) acc = fmaf(S.kv[j * 2 * E + c], S.ctxs[j * E + k], acc);
+    out[OFF_WQ + E * E + i] = acc;
+  }
+  if (threadIdx.x < 2 * E) {                                   // db rows [E, 3E)
+    float acc = 0.f;
+    for (int j = 0; j < a.Lc; ++j) acc += S.kv[j * 2 * E + threadIdx.x];
+    out[OFF_BQ + E + threadIdx.x] = acc;
   }
 }
 
@@ -1519,10 +1559,10 @@ int dispatch(const Tail& a, int grid, float* scr, hipStream_t s) {
 #undef VAESNE_TAIL_CASE
 }
 
-Tail make(const float* x, const float* O, const float* kvc, int M, int L, int Lc,
+Tail make(const float* x, const float* O, const float* ctx, int M, int L, int Lc,
           const float* const* w, float p_drop, const int64_t* rng, uint32_t call_id) {
   Tail a{};
-  a.x = x; a.O = O; a.kvc = kvc; a.M = M; a.L = L; a.Lc = Lc;
+  a.x = x; a.O = O; a.ctx = ctx; a.M = M; a.L = L; a.Lc = Lc;
   a.Wo1 = w[0]; a.bo1 = w[1]; a.g1 = w[2]; a.be1 = w[3]; a.Wq = w[4]; a.bq = w[5];
   a.Wo2 = w[6]; a.bo2 = w[7]; a.g2 = w[8]; a.be2 = w[9]; a.W1 = w[10]; a.b1 = w[11];
   a.W2 = w[12]; a.b2 = w[13]; a.g3 = w[14]; a.be3 = w[15]; a.Wn = w[16]; a.bn = w[17];
@@ -1539,20 +1579,27 @@ bool shapes_ok(int M, int L, int Lc) {
 
 }  // namespace
 
+// two-kernel path: [G][WPART] slabs | scratch vectors | d k|v [Nseq, Lc, 64] | the
+// k | v projection's weight-gradient workspace
+int64_t ctx_grad_floats(int M, int L, int Lc) {
+  const int64_t rows = (int64_t)(M / L) * Lc;
+  return rows * 2 * E + (vaesne_linear_bwd_weight_workspace(rows, 2 * E, E) + 3) / 4;
+}
+
 VAESNE_API int64_t vaesne_dec_tail_workspace(int M, int L, int Lc) {
   if (!shapes_ok(M, L, Lc)) return 0;
   const int chunk = L <= 256 ? ((L + 127) / 128) * 128 : 512;
   const int chunks = (L + chunk - 1) / chunk;
   const int64_t G = (int64_t)(M / L) * chunks;
-  return (G * WPART + (int64_t)NVEC * M * E) * (int64_t)sizeof(float);
+  return (G * WPART + (int64_t)NVEC * M * E + ctx_grad_floats(M, L, Lc)) * (int64_t)sizeof(float);
 }
 
-VAESNE_API int vaesne_dec_tail_fwd(const float* x, const float* O, const float* kvc, int M, int L,
+VAESNE_API int vaesne_dec_tail_fwd(const float* x, const float* O, const float* ctx, int M, int L,
                                    int Lc, const float* const* w, float p_drop,
                                    const int64_t* rng, uint32_t call_id, float* y, float* qkv,
                                    uint32_t* drop_masks, void* stream) {
   if (!shapes_ok(M, L, Lc)) return (int)hipErrorInvalidValue;
-  Tail a = make(x, O, kvc, M, L, Lc, w, p_drop, rng, call_id);
+  Tail a = make(x, O, ctx, M, L, Lc, w, p_drop, rng, call_id);
   a.masks = p_drop > 0.f ? drop_masks : nullptr;
   a.y = y; a.qkv = qkv;
   if (a.Wn && !qkv) return (int)hipErrorInvalidValue;
@@ -1561,21 +1608,22 @@ VAESNE_API int vaesne_dec_tail_fwd(const float* x, const float* O, const float* 
 }
 
 // gflat [WPART]: every parameter gradient of the block in the layout of the
-// per-workgroup slabs (see include/vaesne_hip.h); dkvc [Nseq, Lc, 64].
-VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* kvc, int M, int L,
+// per-workgroup slabs (see include/vaesne_hip.h), the whole cross in_proj included;
+// dctx [Nseq, Lc, 32] the context tokens' gradient.
+VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* ctx, int M, int L,
                                    int Lc, const float* const* w, float p_drop,
                                    const int64_t* rng, uint32_t call_id, const float* y,
                                    const float* dy, const float* dqkv, const uint32_t* drop_masks,
-                                   float* dx, float* dO, float* dkvc, float* gflat,
+                                   float* dx, float* dO, float* dctx, float* gflat,
                                    float* workspace, vaesne_colsum_list* defer, void* stream) {
   if (!shapes_ok(M, L, Lc)) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  Tail a = make(x, O, kvc, M, L, Lc, w, p_drop, rng, call_id);
+  Tail a = make(x, O, ctx, M, L, Lc, w, p_drop, rng, call_id);
   a.masks = p_drop > 0.f ? const_cast<uint32_t*>(drop_masks) : nullptr;
   a.dy = dy; a.dqkv = dqkv; a.dx = dx; a.dO = dO;
   if (a.Wn && !dqkv) return (int)hipErrorInvalidValue;
   a.y = const_cast<float*>(y);
-  a.dkvc = dkvc;
+  a.dctx = dctx;
   if (use_fused(L)) {   // one workgroup per sequence, no scratch
     const int nseq = M / L;
     a.wpart = workspace;
@@ -1592,10 +1640,9 @@ VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* 
                          (const float*)nullptr, (int)J_WN0);
       VAESNE_CHECK_LAUNCH();
     }
-    // fused rows: everything but the in_proj-of-next regions (and the k|v rows)
-    const int fr[5][2] = {{0, OFF_WQ + 1024}, {OFF_WO2, OFF_WN}, {OFF_BO1, OFF_BQ + 32},
-                          {OFF_BO2, OFF_BN}, {OFF_G1, WPART}};
-    for (int k = 0; k < 5; ++k) {
+    // fused rows: everything but the in_proj-of-next regions
+    const int fr[3][2] = {{0, OFF_WN}, {OFF_BO1, OFF_BN}, {OFF_G1, WPART}};
+    for (int k = 0; k < 3; ++k) {
       rc = colsum_or_defer(defer, workspace + fr[k][0], WPART, nseq, fr[k][1] - fr[k][0],
                            gflat + fr[k][0], 0, s);
       if (rc) return rc;
@@ -1610,9 +1657,22 @@ VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* 
   // one workgroup: its slab IS the gradient (no column sum)
   a.wpart = grid == 1 ? gflat : workspace;
   float* scr = workspace + (int64_t)grid * WPART;
-  const int rc = dispatch<false>(a, grid, scr, s);
-  if (rc || grid == 1) return rc;
-  return sum_tail(MODE_FULL, workspace, grid, gflat, defer, s);
+  float* dkv = scr + (int64_t)NVEC * M * E;           // per-sequence d k|v (wgrad J_K / J_V jobs)
+  a.dkvc = dkv;
+  int rc = dispatch<false>(a, grid, scr, s);
+  if (rc) return rc;
+  if (grid > 1) {
+    rc = sum_tail(MODE_FULL, workspace, grid, gflat, defer, s);
+    if (rc) return rc;
+  }
+  // the context k | v projection backward over the Nseq * Lc context tokens
+  const int64_t rows = (int64_t)(M / L) * Lc;
+  float* lws = dkv + rows * 2 * E;
+  rc = vaesne_linear_bwd_weight(dkv, 2 * E, nullptr, 0, 0, ctx, E, nullptr, 0, rows, 2 * E, E,
+                                gflat + OFF_WQ + E * E, gflat + OFF_BQ + E, 0, lws, defer, s);
+  if (rc) return rc;
+  return vaesne_linear_bwd_data(dkv, 2 * E, nullptr, 0, 0, rows, 2 * E, a.Wq + E * E, E, dctx, E,
+                                0, s);
 }
 
 VAESNE_API int64_t vaesne_enc_block_workspace(int M) {
