@@ -286,16 +286,16 @@ def roofline(device, B):
         t = time_kernel(fn, 20, device)
         res[name] = dict(kernel=kern, ms=t * 1e3, tflops=scores * fl / t / 1e12,
                          flops_per_launch=scores * fl)
+        tr, src = _rocprof_avg_ms(kern)   # the committed kernel-trace average inside the step
+        if tr is not None:
+            res[name].update(ms_rocprof=tr, tflops_rocprof=scores * fl / (tr * 1e-3) / 1e12,
+                             rocprof_source=src)
     if pd > 0:
         res["keep_bits_gen"] = dict(kernel="attn_keep_bits_kernel",
                                     ms=time_kernel(gen, 20, device) * 1e3,
                                     note="draws the forward's keep bitmap ahead (off by default)")
         res["fwd_bits_in"] = dict(kernel="attn_fwd_kernel<..., BITSIN> (reads the drawn bitmap)",
                                   ms=time_kernel(fwd_with(1), 20, device) * 1e3)
-        tr, src = _rocprof_avg_ms(kern)
-        if tr is not None:
-            res[name].update(ms_rocprof=tr, tflops_rocprof=scores * fl / (tr * 1e-3) / 1e12,
-                             rocprof_source=src)
     r = res["bwd"]
     a = r["tflops"]
     traffic, tsrc = None, None

@@ -36,6 +36,12 @@ def main(fetch, write, label):
            "kernels": {}}
     for inst in sorted(f):
         base = inst.split("<")[0]
+        # the step's instances: the forward that hashes in-kernel (BITSIN = false), the
+        # fused backward (DQ = true)
+        if inst.startswith("attn_fwd_kernel") and not inst.endswith("false>"):
+            continue
+        if inst.startswith("attn_bwd_kv_kernel") and not inst.endswith("true>"):
+            continue
         if inst in w:
             out["kernels"][base] = {"instance": inst,
                                     "hbm_bytes_per_launch": int(1024 * (2 * f[inst] + w[inst]))}
