@@ -161,6 +161,35 @@ int vaesne_attn_bwd_q(const float* q, int64_t q_bs, int64_t q_ls, const float* k
                       const int64_t* rng_state, uint32_t call_id, const uint32_t* keep_bits,
                       float* workspace, void* stream);
 
+/* ---- the decoders' first block: self-attention over R copies of each sequence ----
+ * The decoders run over N = R*Bd sequences, copy r of distinct sequence b at n = r*Bd + b
+ * (the K samples x both latents: SpectraVAE.py:189-192 / PhotometricVAE.py:196-199
+ * expand z, and the decoder embeds the expanded grid).  Block 1's self-attention input
+ * x = embedding(wavelength | time) (SpectraLayers.py:54-62, PhotometricLayers.py:59-67)
+ * is the same for all R copies, so the scores and softmax statistics are computed once
+ * per distinct sequence; each copy keeps its own dropout masks (util_layers.py:289 ->
+ * torch/nn/functional.py:6594 per sequence).  Results equal vaesne_attn_fwd/bwd on the
+ * expanded input: o [R*Bd, L, E], the keep bitmap bit for bit (same size and layout as
+ * vaesne_attn_fwd's for B = R*Bd), lse [Bd, H, L] (shared), and the backward returns
+ * d(qkv) [Bd, L, 3E] = the sum over the copies.  qkv [Bd, L, 3E] packed (strides
+ * qkv_bs / qkv_ls), kbias [Bd, L] or null, dout dense [R*Bd, L, E], dqkv with qkv's
+ * strides.  dh = 8, L > 16.  workspace: vaesne_attn_rep_workspace bytes. */
+int64_t vaesne_attn_rep_workspace(int Bd, int R, int H, int L, int dh, float p_drop);
+int vaesne_attn_rep_fwd(const float* qkv, int64_t qkv_bs, int64_t qkv_ls, const float* kbias,
+                        int64_t kb_bs, float* o, int64_t o_bs, int64_t o_ls, float* lse, int Bd,
+                        int R, int H, int L, int dh, float p_drop, const int64_t* rng_state,
+                        uint32_t call_id, uint32_t* keep_bits, void* stream);
+int vaesne_attn_rep_bwd(const float* qkv, int64_t qkv_bs, int64_t qkv_ls, const float* kbias,
+                        int64_t kb_bs, const float* o, int64_t o_bs, int64_t o_ls, const float* lse,
+                        const float* dout, float* dqkv, int Bd, int R, int H, int L, int dh,
+                        float p_drop, const int64_t* rng_state, uint32_t call_id,
+                        const uint32_t* keep_bits, float* workspace, void* stream);
+/* Tuning / test hook for the two kernels above: forward fnt threads (0 = auto) x frc
+ * copies per workgroup (2, 4, 8); backward bnt threads (128, 256) x 2*bnp keys per
+ * lane (bnp 1, 2), brc copies per staged tile (8, 16), ~bwgs workgroups.  fnt < 0
+ * restores the defaults.  Process-wide; not while launches are in flight. */
+int vaesne_attn_rep_config(int fnt, int frc, int bnt, int bnp, int brc, int bwgs);
+
 /* Test / tuning hook: force the query-tiled attention kernels' geometry (nt threads
  * per workgroup in {64, 128, 256}, np in {1, 2}: 2*np rows per lane); nt = 0 restores
  * the automatic choice.  Process-wide; not for use while launches are in flight. */

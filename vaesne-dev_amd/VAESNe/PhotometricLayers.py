@@ -8,7 +8,8 @@ from torch import nn
 
 from . import _chain, _ops
 from .util_layers import (MLP, Linear, SinusoidalMLPPositionalEmbedding,
-                          SinusoidalPositionalEmbedding, TransformerBlock, decoder_stack,
+                          SinusoidalPositionalEmbedding, TransformerBlock, decoder_inputs,
+                          decoder_stack,
                           singlelayerMLP, encoder_stack_steps)
 
 
@@ -38,12 +39,10 @@ class photometricTransformerDecoder(nn.Module):
             mask = None
         # x = time_embd + band_embd (PhotometricLayers.py:62-64), the add fused in the gather
         x = _ops.embedding(band, self.bandembd.weight, base=self.sinusoidal_time_embd(time))
-        if repeat > 1:
-            x = _ops.repeat_batch(x, repeat).reshape(repeat * x.shape[0], *x.shape[1:])
-        # x feeds the first block twice and the head: one gradient sum (_ops.fanout)
-        x_res, x_qkv, x_out = _ops.fanout(x, 3)
         bottleneck = self.contextfc(bottleneck)
-        h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, x_qkv=x_qkv)
+        # x feeds the first block twice and the head: one gradient sum (_ops.fanout)
+        x_res, x_qkv, x_out, rep = decoder_inputs(x, repeat, self.transformerblocks, bottleneck)
+        h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, x_qkv=x_qkv, rep=rep)
         return self.get_photo(x_out, h).squeeze(-1)   # get_photo(x + h)
 
 

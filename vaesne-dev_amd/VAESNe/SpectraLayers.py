@@ -10,7 +10,8 @@ from torch import nn
 
 from . import _chain, _ops
 from .util_layers import (MLP, Linear, SinusoidalMLPPositionalEmbedding,
-                          SinusoidalPositionalEmbedding, TransformerBlock, decoder_stack,
+                          SinusoidalPositionalEmbedding, TransformerBlock, decoder_inputs,
+                          decoder_stack,
                           singlelayerMLP, encoder_stack_steps)
 
 
@@ -36,14 +37,13 @@ class spectraTransformerDecoder(nn.Module):
         the embedding MLP runs on the B rows and is broadcast (its gradient is the
         sum over the copies), the rest of the decoder on N."""
         x = self.wavelength_embd_layer(wavelength)
-        if repeat > 1:
-            x = _ops.repeat_batch(x, repeat).reshape(repeat * x.shape[0], *x.shape[1:])
         phase_embd = self.phase_embd_layer(phase[:, None])
-        # x feeds the first block twice and the head: one gradient sum (_ops.fanout)
-        x_res, x_qkv, x_out = _ops.fanout(x, 3)
         bottleneck = torch.cat([self.contextfc(bottleneck), phase_embd], dim=1)
+        # x feeds the first block twice and the head: one gradient sum (_ops.fanout)
+        x_res, x_qkv, x_out, rep = decoder_inputs(x, repeat, self.transformerblocks, bottleneck)
         keep = self.__dict__.pop("_keep_prefetch", None)   # util_layers.prefetch_decoder_dropout
-        h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, keep=keep, x_qkv=x_qkv)
+        h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, keep=keep, x_qkv=x_qkv,
+                          rep=rep)
         return self.get_flux(x_out, h).squeeze(-1)   # get_flux(x + h)
 
 

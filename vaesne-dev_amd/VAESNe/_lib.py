@@ -58,6 +58,12 @@ SIGNATURES = {
     "vaesne_dec_tail_force_path": (I32, [I32]),
     "vaesne_enc_block_workspace": (I64, [I32]),
     "vaesne_attn_force_geometry": (I32, [I32, I32]),
+    "vaesne_attn_rep_workspace": (I64, [I32, I32, I32, I32, I32, F32]),
+    "vaesne_attn_rep_fwd": (I32, [P, I64, I64, P, I64, P, I64, I64, P, I32, I32, I32, I32, I32, F32,
+                                  P, U32, P, P]),
+    "vaesne_attn_rep_bwd": (I32, [P, I64, I64, P, I64, P, I64, I64, P, P, P, I32, I32, I32, I32, I32,
+                                  F32, P, U32, P, P, P]),
+    "vaesne_attn_rep_config": (I32, [I32, I32, I32, I32, I32, I32]),
     "vaesne_enc_block_fwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P]),
     "vaesne_enc_block_bwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P, P, P, P, P, P,
                                    P]),

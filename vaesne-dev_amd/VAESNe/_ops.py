@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 
 import torch
 
@@ -564,6 +565,62 @@ class CrossAttnFn(torch.autograd.Function):
                      Lk * 2 * E, 2 * E, B, H, Lq, Lk, dh, p, ptr(st), cid, ptr(bits),
                      ptr(_attn_ws(B, H, Lq, Lk, dh, 1, q.device)), stream())
         return dq, dkv, None, None, None
+
+
+class SelfAttnRepFn(torch.autograd.Function):
+    """Self-attention of R copies of Bd distinct sequences: packed qkv [Bd, L, 3E]
+    (the in-projection of the distinct rows) -> o [R*Bd, L, E], copy r of sequence
+    b at row r*Bd + b, each copy with its own dropout masks (vaesne_attn_rep_fwd).
+    Equal to self_attention(qkv repeated R times), keep bits included; the
+    backward returns the copies' summed d(qkv)."""
+
+    @staticmethod
+    def forward(ctx, qkv, kbias, H, p, R):
+        _lib.require_device(qkv)
+        qkv = qkv.contiguous()
+        Bd, L, E3 = qkv.shape
+        E = E3 // 3
+        dh = E // H
+        N = R * Bd
+        dev = qkv.device
+        o = torch.empty((N, L, E), dtype=torch.float32, device=dev)
+        lse = torch.empty((Bd, H, L), dtype=torch.float32, device=dev)
+        st = rng.state(dev) if p > 0 else None
+        cid = rng.next_call_id() if p > 0 else 0
+        bits = None
+        if p > 0:
+            n = lib.attn_keep_bits_size(N, H, L, L)
+            bits = torch.empty((n + 3) // 4, dtype=torch.int32, device=dev)
+        lib.attn_rep_fwd(qkv.data_ptr(), L * E3, E3, ptr(kbias), L, o.data_ptr(), L * E, E,
+                         lse.data_ptr(), Bd, R, H, L, dh, float(p), ptr(st), cid, ptr(bits),
+                         stream())
+        ctx.dims = (Bd, R, L, E, H, dh, float(p), cid)
+        ctx.save_for_backward(qkv, kbias, o, lse, bits, st)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, kbias, o, lse, bits, st = ctx.saved_tensors
+        Bd, R, L, E, H, dh, p, cid = ctx.dims
+        do = do.contiguous()
+        E3 = 3 * E
+        dqkv = torch.empty_like(qkv)
+        ws = _ws(lib.attn_rep_workspace(Bd, R, H, L, dh, p), qkv.device)
+        lib.attn_rep_bwd(qkv.data_ptr(), L * E3, E3, ptr(kbias), L, o.data_ptr(), L * E, E,
+                         lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(), Bd, R, H, L, dh, p,
+                         ptr(st), cid, ptr(bits), ptr(ws), stream())
+        return dqkv, None, None, None, None
+
+
+def rep_attention_ok(qkv, num_heads, R):
+    """Shapes vaesne_attn_rep_* take: head_dim 8, L > 16 (query-tiled), R >= 1."""
+    return (qkv.dim() == 3 and qkv.shape[-1] == 3 * 8 * num_heads and qkv.shape[1] > 16
+            and R >= 1 and os.environ.get("VAESNE_REP_ATTN", "1") != "0")
+
+
+def self_attention_rep(qkv, kbias, num_heads, p, R):
+    """kbias: the key bias of the Bd distinct sequences (key_bias of their mask) or None."""
+    return SelfAttnRepFn.apply(qkv, kbias, num_heads, float(p), int(R))
 
 
 def self_attention(qkv, mask, num_heads, p, kbias=None, keep=None):

@@ -237,7 +237,32 @@ def prefetch_decoder_dropout(decoder, N, L, device):
     decoder._keep_prefetch = keep
 
 
-def decoder_stack(blocks, x, context, mask=None, keep=None, x_qkv=None):
+def decoder_fusable(blocks, context):
+    """Whether decoder_stack runs these blocks as fused kernels (else per op)."""
+    blocks = list(blocks)
+    return bool(blocks) and all(_fusable_decoder_block(b) for b in blocks) and \
+        context.dim() == 3 and context.shape[1] <= 8
+
+
+def decoder_inputs(xd, repeat, blocks, context):
+    """The decoders' input embedding xd [Bd, L, E] of the distinct sequences, used by
+    N = repeat * Bd sequences (the K samples x latents expand) -> (x_res, x_qkv, x_out,
+    rep) for decoder_stack(x_res, ..., x_qkv=x_qkv, rep=rep) and the output head.
+    Every use is an alias whose gradients one kernel sums (_ops.fanout); on the fused
+    path the first in-projection reads the distinct rows (rep = repeat)."""
+    if repeat > 1 and decoder_fusable(blocks, context):
+        xd_qkv, xd_rep = _ops.fanout(xd, 2)
+        x = _ops.repeat_batch(xd_rep, repeat).reshape(repeat * xd.shape[0], *xd.shape[1:])
+        x_res, x_out = _ops.fanout(x, 2)
+        return x_res, xd_qkv, x_out, repeat
+    x = xd
+    if repeat > 1:
+        x = _ops.repeat_batch(xd, repeat).reshape(repeat * xd.shape[0], *xd.shape[1:])
+    x_res, x_qkv, x_out = _ops.fanout(x, 3)
+    return x_res, x_qkv, x_out, 1
+
+
+def decoder_stack(blocks, x, context, mask=None, keep=None, x_qkv=None, rep=1):
     """`for blk in blocks: x = blk(x, context, mask=mask)` for the decoders
     (SpectraLayers.py:61-62, PhotometricLayers.py:66-67).  With the reference's
     decoder shape (E 32, 4 heads, ff 32, no context self-attention) each block
@@ -245,30 +270,44 @@ def decoder_stack(blocks, x, context, mask=None, keep=None, x_qkv=None):
     LN1, cross-attention over the context tokens, LN2, FFN, LN3, and the next
     block's in_proj).  Other shapes take the per-op path (TransformerBlock).
     `x_qkv` (optional): an alias of x (_ops.fanout) the first in-projection reads,
-    so the caller's single gradient sum for x covers that use too."""
+    so the caller's single gradient sum for x covers that use too.
+    `rep` > 1: x holds rep copies of Bd = N / rep distinct sequences (row r*Bd + b)
+    and x_qkv is the [Bd, L, E] distinct rows: the first block's in-projection and
+    self-attention scores run once per distinct sequence (_ops.self_attention_rep;
+    each copy keeps its own dropout masks); mask must be repeated the same way."""
     blocks = list(blocks)
-    if not blocks or not all(_fusable_decoder_block(b) for b in blocks) or x.dim() != 3 \
-            or context.shape[1] > 8:
+    if x.dim() != 3 or not decoder_fusable(blocks, context):
+        if rep > 1:
+            raise RuntimeError("decoder_stack(rep > 1) needs the fused decoder blocks")
         for blk in blocks:
             x = blk(x, context, mask=mask)
         return x
     E = 32
     L = x.shape[1]
+    N = x.shape[0]
     b0 = blocks[0].self_attn
     qkv = _ops.linear(x if x_qkv is None else x_qkv, b0.in_proj_weight, b0.in_proj_bias)
     # every block's cross-attention reads the context: one gradient sum for all
     ctxs = _ops.fanout(context, len(blocks))
     kbias = _ops.key_bias(mask)          # one mask conversion for all layers
-    N = x.shape[0]
     if keep is not None and (len(keep) != len(blocks) or any(
             k is not None and k.shape != (N, blk.self_attn.num_heads, L, L)
             for k, blk in zip(keep, blocks))):
         keep = None      # prefetched for another shape: draw in the kernels
+    rep_attn = rep > 1 and (keep is None or keep[0] is None) and \
+        _ops.rep_attention_ok(qkv, b0.num_heads, rep)
+    if rep > 1 and not rep_attn:
+        qkv = _ops.repeat_batch(qkv, rep).reshape(N, L, 3 * E)
     for i, blk in enumerate(blocks):
         p_attn = blk.self_attn.dropout if blk.training else 0.0
         p = blk.dropout.p if blk.training else 0.0
-        O = _ops.self_attention(qkv, None, blk.self_attn.num_heads, p_attn, kbias=kbias,
-                                keep=None if keep is None else keep[i])
+        if i == 0 and rep_attn:
+            Bd = N // rep
+            O = _ops.self_attention_rep(qkv, None if kbias is None else kbias[:Bd],
+                                        blk.self_attn.num_heads, p_attn, rep)
+        else:
+            O = _ops.self_attention(qkv, None, blk.self_attn.num_heads, p_attn, kbias=kbias,
+                                    keep=None if keep is None else keep[i])
         nxt = blocks[i + 1].self_attn if i + 1 < len(blocks) else None
         x, qkv = _ops.DecTailFn.apply(
             L, p, x, O, ctxs[i], blk.cross_attn.in_proj_weight, blk.cross_attn.in_proj_bias,

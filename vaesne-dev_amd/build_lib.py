@@ -87,5 +87,24 @@ def build_profile_lib(out):
     return out
 
 
+def build_variant(out, src_name, defines):
+    """A variant of the library with one source compiled with extra -D flags (A/B
+    studies: profiles/ab_env_list.sh with VAESNE_HIP_LIB=<out>).  Not the product."""
+    os.makedirs(OBJDIR, exist_ok=True)
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    srcs = sources()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(_compile, srcs))
+    tag = "_".join(d.replace("=", "") for d in defines)
+    var = _compile(os.path.join(CSRC, src_name), extra=["-D" + d for d in defines],
+                   obj=os.path.join(OBJDIR, f"{src_name[:-4]}_{tag}.o"))
+    objs = [var if os.path.basename(o) == src_name[:-4] + ".o" else o for o in objs]
+    cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", out, *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    return out
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)

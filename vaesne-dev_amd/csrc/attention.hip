@@ -738,6 +738,402 @@ __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
   }
 }
 
+// ================ repeated sequences: the decoders' first block =================
+// The decoders run over N = R * Bd sequences, copy r of distinct sequence b being
+// sequence n = r * Bd + b (the K samples x both modalities' latents,
+// SpectraVAE.py:189-192, PhotometricVAE.py:196-199).  The first block's
+// self-attention reads x = embedding(wavelength | time), the SAME for all R copies
+// (SpectraLayers.py:54-62, PhotometricLayers.py:59-67): scores, row maxima and
+// softmax denominators are shared, only the dropout masks differ.  These kernels
+// compute the shared part once per distinct sequence and loop over the copies for
+// the rest:
+//   forward : per copy, the keep decisions and P.V (RC copies per workgroup, the
+//             scores and exponentials computed once for them);
+//   backward: per copy, dP = dO.V, the keep mask and the dV terms; the copies' dS
+//             are summed before dK = dS^T Q and dQ = dS K (Q, K, V are shared, so
+//             their gradients are the sums over the copies anyway).
+// Each copy's keep decisions are exactly those attn_fwd_kernel draws for sequence n
+// and the bitmap has its layout ([n*H + h][word][query]), so the plain kernels on
+// the expanded input reproduce these bit for bit (tested).
+// Args: q/k/v/kbias/lse over the Bd distinct sequences (a.B = Bd), o / dout / bits
+// over the N sequences (o_bs, do_bs = per-sequence strides).
+template <int DH, int NTT, int RC, bool DROP>
+__global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R) {
+  __shared__ __attribute__((aligned(16))) float Ks[TK * DH];
+  __shared__ __attribute__((aligned(16))) float Vs[TK * DH];
+  __shared__ float Kb[TK];
+  constexpr int NC = DROP ? RC : 1;       // accumulator sets (no dropout: one for all copies)
+  const int nqb = (a.Lq + 2 * NTT - 1) / (2 * NTT);
+  const int qb = blockIdx.x % nqb;
+  const int bh = blockIdx.x / nqb;        // distinct sequence x head
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int c0 = blockIdx.y * RC;
+  int qi[2], qc[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    qi[u] = qb * 2 * NTT + u * NTT + threadIdx.x;
+    qc[u] = min(qi[u], a.Lq - 1);
+  }
+  f2 q[DH], o[NC][DH], m, l;
+  {
+    const float* qbase = a.q + (int64_t)b * a.q_bs + h * DH;
+    float t0[DH], t1[DH];
+    ldr<DH>(qbase + (int64_t)qc[0] * a.q_ls, t0);
+    ldr<DH>(qbase + (int64_t)qc[1] * a.q_ls, t1);
+#pragma unroll
+    for (int d = 0; d < DH; ++d) q[d] = (f2){t0[d], t1[d]} * a.scale_log2;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int d = 0; d < DH; ++d) o[c][d] = bc(0.f);
+    m = bc(-INFINITY);
+    l = bc(0.f);
+  }
+  // copies past R (R % RC != 0) are computed with copy R - 1's keys and not stored
+  uint32_t rk[NC][2];
+  uint32_t* bitp[NC];
+  uint32_t skey = 0u;
+  if (DROP) {
+    skey = key_of(a.rng_state, a.call_id);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int64_t nh = (int64_t)(min(c0 + c, R - 1) * a.B + b) * a.H + h;
+      bitp[c] = a.bits + nh * a.nw * a.Lq;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) rk[c][u] = attn_row_key(skey, (uint32_t)(nh * a.Lq + qc[u]));
+    }
+  }
+  const float* kg = a.k + (int64_t)b * a.k_bs + h * DH;
+  const float* vg = a.v + (int64_t)b * a.v_bs + h * DH;
+  const float* kbg = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
+  for (int kt = 0; kt < a.Lk; kt += TK) {
+    __syncthreads();
+    stage<DH, NTT>(Ks, kg, a.k_ls, kt, a.Lk, 1.f);
+    stage<DH, NTT>(Vs, vg, a.v_ls, kt, a.Lk, 1.f);
+    for (int i = threadIdx.x; i < TK; i += NTT)
+      Kb[i] = kt + i < a.Lk ? (kbg ? kbg[kt + i] : 0.f) : -INFINITY;
+    __syncthreads();
+    const int kend = min(TK, a.Lk - kt);
+    uint32_t w[NC][2];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) w[c][0] = w[c][1] = 0u;
+    for (int g0 = 0; g0 < kend; g0 += 8) {
+      f2 s[8];
+      f2 x = m;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        f2 kr[DH / 2];
+        lrow2<DH>(Ks + (g0 + u) * DH, kr);
+        f2 acc = bc(Kb[g0 + u]);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) acc = fma2r<DH>(q[d], kr, d, acc);
+        s[u] = acc;
+        x = __builtin_elementwise_max(x, acc);
+      }
+      // lazy rescaling, as attn_fwd_kernel (wave-uniform, first groups only)
+      if (__any((x.x > m.x + 8.f) | (x.y > m.y + 8.f))) {
+        const f2 mo = (f2){m.x == -INFINITY ? 0.f : m.x, m.y == -INFINITY ? 0.f : m.y};
+        const f2 mn = (f2){x.x == -INFINITY ? 0.f : x.x, x.y == -INFINITY ? 0.f : x.y};
+        const f2 cf = ex2(mo - mn);
+        m = x;
+        l *= cf;
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int d = 0; d < DH; ++d) o[c][d] *= cf;
+      }
+      const f2 mu = (f2){m.x == -INFINITY ? 0.f : m.x, m.y == -INFINITY ? 0.f : m.y};
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        const f2 p0 = ex2(s[u] - mu), p1 = ex2(s[u + 1] - mu);
+        l += p0 + p1;
+        f2 v0[DH / 2], v1[DH / 2];
+        lrow2<DH>(Vs + (g0 + u) * DH, v0);
+        lrow2<DH>(Vs + (g0 + u + 1) * DH, v1);
+        if (DROP) {
+          const uint32_t kpm = attn_keypair_mix(skey, (uint32_t)((kt + g0 + u) >> 1));
+          const int sh = (g0 + u) & 31;
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            uint32_t kk[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              const uint32_t bits = attn_pair_bits_mixed(rk[c][t], kpm);
+              kk[t] = ((bits & 0xffffu) >= a.thr ? 1u : 0u) | ((bits >> 16) >= a.thr ? 2u : 0u);
+              w[c][t] |= kk[t] << sh;
+            }
+            const f2 a0 = sel2(kk[0] & 1u, kk[1] & 1u, p0);
+            const f2 a1 = sel2(kk[0] & 2u, kk[1] & 2u, p1);
+#pragma unroll
+            for (int d = 0; d < DH; ++d) {
+              o[c][d] = fma2r<DH>(a0, v0, d, o[c][d]);
+              o[c][d] = fma2r<DH>(a1, v1, d, o[c][d]);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int d = 0; d < DH; ++d) {
+            o[0][d] = fma2r<DH>(p0, v0, d, o[0][d]);
+            o[0][d] = fma2r<DH>(p1, v1, d, o[0][d]);
+          }
+        }
+      }
+      if (DROP && (((g0 + 8) & 31) == 0 || g0 + 8 >= kend)) {
+        const int word = (kt + g0) >> 5;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          if (c0 + c < R) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+              if (qi[t] < a.Lq) bitp[c][(int64_t)word * a.Lq + qi[t]] = w[c][t];
+          }
+          w[c][0] = w[c][1] = 0u;
+        }
+      }
+    }
+  }
+  // l == 0 (every key masked) -> NaN, as the reference
+  const f2 inv = bc(DROP ? a.inv_keep : 1.f) / l;
+  auto put = [&](const f2 (&oc)[DH], int r) {
+    float r0[DH], r1[DH];
+#pragma unroll
+    for (int d = 0; d < DH; ++d) { r0[d] = oc[d].x * inv.x; r1[d] = oc[d].y * inv.y; }
+    float* ob = a.o_out + (int64_t)(r * a.B + b) * a.o_bs + h * DH;
+    if (qi[0] < a.Lq) str<DH>(ob + (int64_t)qi[0] * a.o_ls, r0);
+    if (qi[1] < a.Lq) str<DH>(ob + (int64_t)qi[1] * a.o_ls, r1);
+  };
+  if (DROP) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      if (c0 + c < R) put(o[c], c0 + c);
+  } else {
+    for (int r = 0; r < R; ++r) put(o[0], r);   // every copy the same
+  }
+  if (blockIdx.y == 0) {   // shared over the copies
+    if (qi[0] < a.Lq) a.lse[(int64_t)bh * a.Lq + qi[0]] = m.x + __log2f(l.x);
+    if (qi[1] < a.Lq) a.lse[(int64_t)bh * a.Lq + qi[1]] = m.y + __log2f(l.y);
+  }
+}
+
+// Backward with dropout (head_dim 8, dQ fused as in attn_bwd_kv_kernel).  Lane owns
+// 2*NP adjacent keys of a distinct sequence; query tiles of TQR queries stream
+// through LDS with, per copy, its dO rows (pre-multiplied by 1/(1-p)) and keep
+// words.  grid.x = Bd*H*key blocks, grid.y = query chunks x copy batches (RC
+// copies each); several of either write partial dK / dV (slot y) and dQ (slot
+// kb * copy batches + batch) into the workspace, summed in fixed order afterwards.
+constexpr int TQR = 16;
+#ifndef VAESNE_REP_WPE
+#define VAESNE_REP_WPE 3      // waves per SIMD the register budget is sized for (NP = 1)
+#endif
+template <int NTT, int NP, int RC>
+__global__ __launch_bounds__(NTT) __attribute__((amdgpu_waves_per_eu(NP == 1 ? VAESNE_REP_WPE : 1)))
+void attn_rep_bwd_kernel(AttnArgs a, int R, int QS) {
+  constexpr int DH = 8;
+  constexpr int R2 = 2 * NP;
+  constexpr int KB = R2 * NTT;
+  constexpr int NWB = (KB + 31) / 32;
+  constexpr int NWV = NTT / 64;
+  constexpr int WST = TQR + 1;                       // keep-word row stride (banks)
+  __shared__ __attribute__((aligned(16))) float Qs[TQR * DH];
+  __shared__ __attribute__((aligned(16))) float Dos[RC * TQR * DH];
+  __shared__ float Ls[TQR], Dsum[TQR], Dc[RC * TQR];
+  __shared__ uint32_t Ws[RC * NWB * WST];
+  __shared__ __attribute__((aligned(16))) float Qw[NWV * TQR * DH];
+  const int nkb = (a.Lk + KB - 1) / KB;
+  const int kb = blockIdx.x % nkb;
+  const int bh = blockIdx.x / nkb;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int qs = blockIdx.y % QS, cb = blockIdx.y / QS, ncb = gridDim.y / QS;
+  const int c0 = cb * RC;
+  const int key0 = kb * KB + R2 * threadIdx.x;
+  f2 k[NP][DH], v[NP][DH], dk[NP][DH], dv[NP][DH], kbias[NP];
+  {
+    const float* kbase = a.k + (int64_t)b * a.k_bs + h * DH;
+    const float* vbase = a.v + (int64_t)b * a.v_bs + h * DH;
+    const float* kbp = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int j0 = key0 + 2 * p, j1 = j0 + 1;
+      float t0[DH], t1[DH];
+      ldr<DH>(kbase + (int64_t)min(j0, a.Lk - 1) * a.k_ls, t0);
+      ldr<DH>(kbase + (int64_t)min(j1, a.Lk - 1) * a.k_ls, t1);
+#pragma unroll
+      for (int d = 0; d < DH; ++d) k[p][d] = (f2){t0[d], t1[d]};
+      ldr<DH>(vbase + (int64_t)min(j0, a.Lk - 1) * a.v_ls, t0);
+      ldr<DH>(vbase + (int64_t)min(j1, a.Lk - 1) * a.v_ls, t1);
+#pragma unroll
+      for (int d = 0; d < DH; ++d) {
+        v[p][d] = (f2){t0[d], t1[d]};
+        dk[p][d] = bc(0.f);
+        dv[p][d] = bc(0.f);
+      }
+      kbias[p] = (f2){j0 < a.Lk ? (kbp ? kbp[j0] : 0.f) : -INFINITY,
+                      j1 < a.Lk ? (kbp ? kbp[j1] : 0.f) : -INFINITY};
+    }
+  }
+  const int wl = (R2 * threadIdx.x) >> 5;
+  const int sh = (R2 * threadIdx.x) & 31;
+  const float* qg = a.q + (int64_t)b * a.q_bs + h * DH;
+  const float* lg = a.lse + (int64_t)bh * a.Lq;
+  const int wfirst = (kb * KB) >> 5;
+  const int qbeg = qs * a.qchunk, qlim = min(a.Lq, qbeg + a.qchunk);
+  for (int qt = qbeg; qt < qlim; qt += TQR) {
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < TQR * (DH / 4); idx += NTT) {
+      const int i = idx / (DH / 4), cc = (idx - i * (DH / 4)) * 4;
+      float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (qt + i < qlim) {
+        val = *reinterpret_cast<const float4*>(qg + (int64_t)(qt + i) * a.q_ls + cc);
+        val.x *= a.scale_log2; val.y *= a.scale_log2; val.z *= a.scale_log2; val.w *= a.scale_log2;
+      }
+      *reinterpret_cast<float4*>(Qs + i * DH + cc) = val;
+    }
+    // per copy and query: the dO row (x 1/(1-p)) and D_c = dO_c . O_c (raw dO)
+    for (int idx = threadIdx.x; idx < RC * TQR; idx += NTT) {
+      const int c = idx / TQR, i = idx - c * TQR;
+      const int qi = qt + i;
+      float x[DH], y[DH];
+      float Di = 0.f;
+      if (qi < qlim && c0 + c < R) {
+        const int64_t n = (int64_t)(c0 + c) * a.B + b;
+        ldr<DH>(a.dout + n * a.do_bs + (int64_t)qi * a.do_ls + h * DH, x);
+        ldr<DH>(a.o + n * a.o_bs + (int64_t)qi * a.o_ls + h * DH, y);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) Di = fmaf(x[d], y[d], Di);
+      } else {
+#pragma unroll
+        for (int d = 0; d < DH; ++d) x[d] = 0.f;
+      }
+#pragma unroll
+      for (int d = 0; d < DH; ++d) x[d] *= a.inv_keep;
+      str<DH>(Dos + (c * TQR + i) * DH, x);
+      Dc[c * TQR + i] = Di;
+    }
+    for (int idx = threadIdx.x; idx < RC * NWB * TQR; idx += NTT) {
+      const int c = idx / (NWB * TQR), r = idx - c * (NWB * TQR);
+      const int wv = r / TQR, i = r - wv * TQR;
+      const int qi = qt + i, word = wfirst + wv;
+      uint32_t wd = 0u;
+      if (qi < qlim && word < a.nw && c0 + c < R) {
+        const int64_t nh = (int64_t)((c0 + c) * a.B + b) * a.H + h;
+        wd = a.bits[(nh * a.nw + word) * a.Lq + qi];
+      }
+      Ws[(c * NWB + wv) * WST + i] = wd;
+    }
+    for (int i = threadIdx.x; i < TQR; i += NTT)
+      Ls[i] = qt + i < qlim ? lg[qt + i] : INFINITY;   // +inf for padding rows -> p = 0
+    __syncthreads();
+    for (int i = threadIdx.x; i < TQR; i += NTT) {
+      float sD = 0.f;
+      for (int c = 0; c < RC; ++c) sD += Dc[c * TQR + i];
+      Dsum[i] = sD;
+    }
+    __syncthreads();
+    const int qend = min(TQR, qlim - qt);
+    for (int i0 = 0; i0 < qend; i0 += 2) {
+      f2 dSq[2][NP];
+#pragma unroll
+      for (int i = i0; i < i0 + 2; ++i) {
+        f2 qr[DH / 2];
+        lrow2<DH>(Qs + i * DH, qr);
+        const f2 li = bc(Ls[i]), nD = bc(-Dsum[i]);
+        f2 pr[NP], acc[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          f2 s = kbias[p];
+#pragma unroll
+          for (int d = 0; d < DH; ++d) s = fma2ru<DH>(k[p][d], qr, d, s);
+          pr[p] = ex2(s - li);
+          acc[p] = pr[p] * nD;          // - P sum_c D_c
+        }
+        // every copy's keep word of this query first (one LDS wait, not one per copy)
+        uint32_t wk[RC];
+#pragma unroll
+        for (int c = 0; c < RC; ++c) wk[c] = Ws[(c * NWB + wl) * WST + i];
+        // sum over the copies of keep * P * dP (dS = P (keep dP - D), summed)
+#pragma unroll
+        for (int c = 0; c < RC; ++c) {
+          f2 dr[DH / 2];
+          lrow2<DH>(Dos + (c * TQR + i) * DH, dr);
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            // dP = V . dO as two half chains (even / odd features): no 8-long dependency
+            f2 g0 = mul2_lo(v[p][0], dr[0]), g1 = mul2_hi(v[p][1], dr[0]);
+#pragma unroll
+            for (int d = 2; d < DH; d += 2) {
+              g0 = fma2ru<DH>(v[p][d], dr, d, g0);
+              g1 = fma2ru<DH>(v[p][d + 1], dr, d + 1, g1);
+            }
+            // keep bit -> all-ones / zero mask on P's bits (sign-extending bit extract)
+            const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)wk[c], sh + 2 * p, 1);
+            const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)wk[c], sh + 2 * p + 1, 1);
+            const f2 aP = (f2){__uint_as_float(__float_as_uint(pr[p].x) & m0),
+                               __uint_as_float(__float_as_uint(pr[p].y) & m1)};
+            acc[p] = fma2(aP, g0 + g1, acc[p]);
+#pragma unroll
+            for (int d = 0; d < DH; ++d) dv[p][d] = fma2ru<DH>(aP, dr, d, dv[p][d]);
+          }
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          dSq[i - i0][p] = acc[p];
+#pragma unroll
+          for (int d = 0; d < DH; ++d) dk[p][d] = fma2ru<DH>(acc[p], qr, d, dk[p][d]);
+        }
+      }
+      f2 F[DH];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const f2 sx = {dSq[0][p].x, dSq[1][p].x}, sy = {dSq[0][p].y, dSq[1][p].y};
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+          F[d] = p == 0 ? mul2_lo(sx, k[p][d]) : fma2_lo_u(sx, k[p][d], F[d]);
+          F[d] = fma2_hi_u(sy, k[p][d], F[d]);
+        }
+      }
+      float cr[16];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cr[j] = F[2 * j].x; cr[j + 8] = F[2 * j + 1].x;
+        cr[j + 4] = F[2 * j].y; cr[j + 12] = F[2 * j + 1].y;
+      }
+      const int ln = threadIdx.x & 63;
+      Qw[((threadIdx.x >> 6) * TQR + i0 + ((ln >> 4) & 1)) * DH +
+         (2 * ((ln >> 2) & 1) + 4 * ((ln >> 3) & 1) + ((ln >> 5) & 1))] = wave_sum16_spread(cr);
+    }
+    __syncthreads();
+    // dQ rows of this tile over this key block: slot kb * copy batches + batch
+    float* dqb = a.dq + (int64_t)(kb * ncb + cb) * a.dq_ss + (int64_t)b * a.dq_bs + h * DH;
+    for (int idx = threadIdx.x; idx < qend * (DH / 4); idx += NTT) {
+      const int i = idx / (DH / 4), cc = (idx - i * (DH / 4)) * 4;
+      float4 acc = *reinterpret_cast<const float4*>(Qw + i * DH + cc);
+#pragma unroll
+      for (int wv = 1; wv < NWV; ++wv) {
+        const float4 t = *reinterpret_cast<const float4*>(Qw + (wv * TQR + i) * DH + cc);
+        acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+      }
+      acc.x *= a.scale; acc.y *= a.scale; acc.z *= a.scale; acc.w *= a.scale;
+      *reinterpret_cast<float4*>(dqb + (int64_t)(qt + i) * a.dq_ls + cc) = acc;
+    }
+  }
+  const float kf = a.scale / a.scale_log2;
+  float* dkb = a.dk + blockIdx.y * a.dk_ss + (int64_t)b * a.dk_bs + h * DH;
+  float* dvb = a.dv + blockIdx.y * a.dk_ss + (int64_t)b * a.dv_bs + h * DH;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int j0 = key0 + 2 * p, j1 = j0 + 1;
+    float r0[DH], r1[DH];
+#pragma unroll
+    for (int d = 0; d < DH; ++d) { r0[d] = dk[p][d].x * kf; r1[d] = dk[p][d].y * kf; }
+    if (j0 < a.Lk) str<DH>(dkb + (int64_t)j0 * a.dk_ls, r0);
+    if (j1 < a.Lk) str<DH>(dkb + (int64_t)j1 * a.dk_ls, r1);
+#pragma unroll
+    for (int d = 0; d < DH; ++d) { r0[d] = dv[p][d].x; r1[d] = dv[p][d].y; }
+    if (j0 < a.Lk) str<DH>(dvb + (int64_t)j0 * a.dv_ls, r0);
+    if (j1 < a.Lk) str<DH>(dvb + (int64_t)j1 * a.dv_ls, r1);
+  }
+}
+
 // ======================= few queries (Lq <= 16) ===========================
 // The encoders' latent queries (2*latent_len = 8 rows) attend to the whole
 // light curve / spectrum (60 / 983 keys).  Query-parallel tiling leaves 56 of
@@ -1314,7 +1710,214 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
   return 0;
 }
 
+// ---- repeated sequences (attn_rep_*): configuration and plans ----
+// forward: fnt threads x 2 queries per lane, frc copies per workgroup (frc sets of
+// 8 packed accumulators); backward: bnt threads x 2*bnp keys per lane, brc copies
+// per staged tile, query chunks sized so the grid has ~bwgs workgroups.
+// VAESNE_REP="fnt,frc,bnt,bnp,brc,bwgs" overrides (tuning / tests).
+struct RepCfg { int fnt, frc, bnt, bnp, brc, bwgs; };
+RepCfg g_rep = [] {
+  RepCfg c{0, 2, 256, 1, 16, 1536};
+  if (const char* e = getenv("VAESNE_REP"))
+    sscanf(e, "%d,%d,%d,%d,%d,%d", &c.fnt, &c.frc, &c.bnt, &c.bnp, &c.brc, &c.bwgs);
+  return c;
+}();
+bool rep_cfg_ok(const RepCfg& c) {
+  return (c.fnt == 0 || c.fnt == 64 || c.fnt == 128 || c.fnt == 256) &&
+         (c.frc == 2 || c.frc == 4 || c.frc == 8) && (c.bnt == 128 || c.bnt == 256) &&
+         (c.bnp == 1 || c.bnp == 2) && (c.brc == 8 || c.brc == 16) && c.bwgs > 0;
+}
+int rep_fwd_nt(int64_t bh, int L, int cb) {
+  if (g_rep.fnt > 0) return g_rep.fnt;
+  // fewest wasted query slots among grids of >= 1024 workgroups (else 64 threads)
+  const int nts[3] = {256, 128, 64};
+  int best = 64;
+  double best_eff = -1.0;
+  for (int nt : nts) {
+    const int64_t nb = (L + 2 * nt - 1) / (2 * nt);
+    const double eff = (double)L / (double)(2 * nt * nb);
+    if (bh * nb * cb >= 1024 && eff > best_eff + 1e-9) { best = nt; best_eff = eff; }
+  }
+  return best;
+}
+struct RepPlan { int nkb, QS, chunk, CB; int64_t dkv_floats, dq_floats, dsum_floats, std_floats; };
+RepPlan rep_bwd_plan(int Bd, int R, int H, int L, float p_drop) {
+  RepPlan pl{};
+  const int E = H * 8;
+  if (p_drop <= 0.f) {   // no dropout: copies identical -> one plain backward on sum_r dO_r
+    Split sq, sk;
+    pl.dsum_floats = (int64_t)Bd * L * E;
+    pl.std_floats = bwd_ws_floats(Bd, H, L, L, 8, sq, sk);
+    return pl;
+  }
+  const int KB = 2 * g_rep.bnp * g_rep.bnt;
+  pl.nkb = (L + KB - 1) / KB;
+  pl.CB = (R + g_rep.brc - 1) / g_rep.brc;
+  const int64_t per = (int64_t)Bd * H * pl.nkb * pl.CB;
+  const int tiles = (L + TQR - 1) / TQR;
+  int qs = (int)std::max<int64_t>(1, (g_rep.bwgs + per / 2) / per);
+  qs = std::min(qs, tiles);
+  pl.chunk = (tiles + qs - 1) / qs * TQR;
+  pl.QS = (L + pl.chunk - 1) / pl.chunk;
+  pl.dkv_floats = pl.QS * pl.CB > 1 ? 2 * (int64_t)pl.QS * pl.CB * Bd * L * E : 0;
+  pl.dq_floats = pl.nkb * pl.CB > 1 ? (int64_t)pl.nkb * pl.CB * Bd * L * E : 0;
+  return pl;
+}
+
+int launch_rep_fwd(const AttnArgs& a, int R, float p_drop, hipStream_t s) {
+  const bool drop = p_drop > 0.f;
+  const int rc = drop ? g_rep.frc : 1;
+  const int cb = drop ? (R + rc - 1) / rc : 1;
+  const int nt = rep_fwd_nt((int64_t)a.B * a.H, a.Lq, cb);
+  const int nqb = (a.Lq + 2 * nt - 1) / (2 * nt);
+  const dim3 grid((unsigned)((int64_t)a.B * a.H * nqb), (unsigned)cb);
+#define VAESNE_REP_FWD(NT)                                                                        \
+  if (!drop) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, false>), grid, dim3(NT), 0, s, a, R); \
+  else if (rc == 2) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 2, true>), grid, dim3(NT), 0, s, a, R); \
+  else if (rc == 4) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 4, true>), grid, dim3(NT), 0, s, a, R); \
+  else hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 8, true>), grid, dim3(NT), 0, s, a, R);
+  if (nt == 256) { VAESNE_REP_FWD(256) } else if (nt == 128) { VAESNE_REP_FWD(128) } else { VAESNE_REP_FWD(64) }
+#undef VAESNE_REP_FWD
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+int launch_rep_bwd(const AttnArgs& a, int R, float p_drop, float* ws, hipStream_t s) {
+  const int E = a.H * 8;
+  const RepPlan pl = rep_bwd_plan(a.B, R, a.H, a.Lq, p_drop);
+  if (p_drop <= 0.f) {
+    // every copy's O and P are the same: dS summed over copies = P (V.sum_r dO_r - sum_r D_r),
+    // sum_r D_r = O . sum_r dO_r -- the plain backward of (qkv, O, sum_r dO_r)
+    float* dsum = ws;
+    const int64_t n = (int64_t)a.B * a.Lq * E;
+    hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       a.dout, (int64_t)a.B * a.do_bs, R, a.B, a.Lq, E, dsum, (int64_t)a.Lq * E,
+                       (int64_t)E);
+    VAESNE_CHECK_LAUNCH();
+    AttnArgs c = a;
+    c.dout = dsum; c.do_bs = (int64_t)a.Lq * E; c.do_ls = E;
+    return launch_bwd<8>(c, 0.f, 3, pl.std_floats > 0 ? ws + pl.dsum_floats : nullptr, s);
+  }
+  AttnArgs c = a;
+  c.qchunk = pl.chunk;
+  float* wdkv = ws;
+  float* wdq = ws + pl.dkv_floats;
+  if (pl.dkv_floats > 0) {
+    c.dk = wdkv; c.dk_bs = (int64_t)a.Lk * E; c.dk_ls = E;
+    c.dv = wdkv + (int64_t)pl.QS * pl.CB * a.B * a.Lk * E; c.dv_bs = c.dk_bs; c.dv_ls = E;
+    c.dk_ss = (int64_t)a.B * a.Lk * E;
+  } else {
+    c.dk_ss = 0;
+  }
+  if (pl.dq_floats > 0) {
+    c.dq = wdq; c.dq_bs = (int64_t)a.Lq * E; c.dq_ls = E;
+    c.dq_ss = (int64_t)a.B * a.Lq * E;
+  } else {
+    c.dq_ss = 0;
+  }
+  const dim3 grid((unsigned)((int64_t)a.B * a.H * pl.nkb), (unsigned)(pl.QS * pl.CB));
+#define VAESNE_REP_BWD(NT, NP)                                                                     \
+  if (g_rep.brc == 16) hipLaunchKernelGGL((attn_rep_bwd_kernel<NT, NP, 16>), grid, dim3(NT), 0, s, c, R, pl.QS); \
+  else hipLaunchKernelGGL((attn_rep_bwd_kernel<NT, NP, 8>), grid, dim3(NT), 0, s, c, R, pl.QS);
+  if (g_rep.bnt == 256) {
+    if (g_rep.bnp == 2) { VAESNE_REP_BWD(256, 2) } else { VAESNE_REP_BWD(256, 1) }
+  } else {
+    if (g_rep.bnp == 2) { VAESNE_REP_BWD(128, 2) } else { VAESNE_REP_BWD(128, 1) }
+  }
+#undef VAESNE_REP_BWD
+  VAESNE_CHECK_LAUNCH();
+  if (pl.dkv_floats > 0) {
+    const int64_t n = (int64_t)a.B * a.Lk * E;
+    const unsigned nb = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3(nb), dim3(256), 0, s, c.dk, c.dk_ss,
+                       pl.QS * pl.CB, a.B, a.Lk, E, a.dk, a.dk_bs, a.dk_ls);
+    VAESNE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3(nb), dim3(256), 0, s, c.dv, c.dk_ss,
+                       pl.QS * pl.CB, a.B, a.Lk, E, a.dv, a.dv_bs, a.dv_ls);
+    VAESNE_CHECK_LAUNCH();
+  }
+  if (pl.dq_floats > 0) {
+    const int64_t n = (int64_t)a.B * a.Lq * E;
+    hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       c.dq, c.dq_ss, pl.nkb * pl.CB, a.B, a.Lq, E, a.dq, a.dq_bs, a.dq_ls);
+    VAESNE_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
 }  // namespace
+
+VAESNE_API int vaesne_attn_rep_config(int fnt, int frc, int bnt, int bnp, int brc, int bwgs) {
+  if (fnt < 0) { g_rep = RepCfg{0, 2, 256, 1, 16, 1536}; return 0; }
+  const RepCfg c{fnt, frc, bnt, bnp, brc, bwgs};
+  if (!rep_cfg_ok(c)) return (int)hipErrorInvalidValue;
+  g_rep = c;
+  return 0;
+}
+
+VAESNE_API int64_t vaesne_attn_rep_workspace(int Bd, int R, int H, int L, int dh, float p_drop) {
+  if (Bd <= 0 || R <= 0 || L <= 2 * SQ || dh != 8) return 0;
+  const RepPlan pl = rep_bwd_plan(Bd, R, H, L, p_drop);
+  return (pl.dkv_floats + pl.dq_floats + pl.dsum_floats + pl.std_floats) * (int64_t)sizeof(float);
+}
+
+namespace {
+bool rep_args(AttnArgs& a, const float* qkv, int64_t qkv_bs, int64_t qkv_ls, const float* kbias,
+              int64_t kb_bs, int Bd, int H, int L, int dh, float p_drop, const int64_t* rng_state,
+              uint32_t call_id) {
+  const int E = H * dh;
+  a.q = qkv; a.k = qkv + E; a.v = qkv + 2 * E;
+  a.q_bs = a.k_bs = a.v_bs = qkv_bs;
+  a.q_ls = a.k_ls = a.v_ls = qkv_ls;
+  a.kbias = kbias; a.kb_bs = kb_bs;
+  fill_common(a, Bd, H, L, L, dh, p_drop, rng_state, call_id);
+  return aligned16(a.q, qkv_ls) && aligned16(a.k, qkv_ls) && aligned16(a.v, qkv_ls);
+}
+}  // namespace
+
+VAESNE_API int vaesne_attn_rep_fwd(const float* qkv, int64_t qkv_bs, int64_t qkv_ls,
+                                   const float* kbias, int64_t kb_bs, float* o, int64_t o_bs,
+                                   int64_t o_ls, float* lse, int Bd, int R, int H, int L, int dh,
+                                   float p_drop, const int64_t* rng_state, uint32_t call_id,
+                                   uint32_t* keep_bits, void* stream) {
+  if (Bd <= 0 || R <= 0 || L <= 0) return 0;
+  if (dh != 8 || L <= 2 * SQ || !rep_cfg_ok(g_rep)) return (int)hipErrorInvalidValue;
+  if (p_drop > 0.f && (!keep_bits || !rng_state)) return (int)hipErrorInvalidValue;
+  AttnArgs a{};
+  if (!rep_args(a, qkv, qkv_bs, qkv_ls, kbias, kb_bs, Bd, H, L, dh, p_drop, rng_state, call_id) ||
+      !aligned16(o, o_ls))
+    return (int)hipErrorInvalidValue;
+  a.o = o; a.o_out = o; a.o_bs = o_bs; a.o_ls = o_ls;
+  a.lse = lse;
+  a.bits = keep_bits;
+  return launch_rep_fwd(a, R, p_drop, (hipStream_t)stream);
+}
+
+VAESNE_API int vaesne_attn_rep_bwd(const float* qkv, int64_t qkv_bs, int64_t qkv_ls,
+                                   const float* kbias, int64_t kb_bs, const float* o, int64_t o_bs,
+                                   int64_t o_ls, const float* lse, const float* dout,
+                                   float* dqkv, int Bd, int R, int H, int L, int dh, float p_drop,
+                                   const int64_t* rng_state, uint32_t call_id,
+                                   const uint32_t* keep_bits, float* workspace, void* stream) {
+  if (Bd <= 0 || R <= 0 || L <= 0) return 0;
+  if (dh != 8 || L <= 2 * SQ || !rep_cfg_ok(g_rep)) return (int)hipErrorInvalidValue;
+  if (p_drop > 0.f && !keep_bits) return (int)hipErrorInvalidValue;
+  if (vaesne_attn_rep_workspace(Bd, R, H, L, dh, p_drop) > 0 && !workspace)
+    return (int)hipErrorInvalidValue;
+  const int E = H * dh;
+  AttnArgs a{};
+  if (!rep_args(a, qkv, qkv_bs, qkv_ls, kbias, kb_bs, Bd, H, L, dh, p_drop, rng_state, call_id) ||
+      !aligned16(o, o_ls) || !aligned16(dout, E) || !aligned16(dqkv, qkv_ls))
+    return (int)hipErrorInvalidValue;
+  a.o = o; a.o_bs = o_bs; a.o_ls = o_ls;
+  a.lse = const_cast<float*>(lse);
+  a.dout = dout; a.do_bs = (int64_t)L * E; a.do_ls = E;        // dense [R*Bd, L, E]
+  a.dq = dqkv; a.dk = dqkv + E; a.dv = dqkv + 2 * E;
+  a.dq_bs = a.dk_bs = a.dv_bs = qkv_bs;
+  a.dq_ls = a.dk_ls = a.dv_ls = qkv_ls;
+  a.bits = const_cast<uint32_t*>(keep_bits);
+  return launch_rep_bwd(a, R, p_drop, workspace, (hipStream_t)stream);
+}
 
 VAESNE_API int vaesne_attn_force_geometry(int nt, int np) {
   if (nt == 0) { g_forced = {0, 0}; return 0; }
