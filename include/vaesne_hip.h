@@ -420,7 +420,7 @@ int vaesne_bright_shift_bwd(const float* g, int64_t R, int L, float* dloc, float
  * modalities' latents in ONE decoder call per modality (loc [K, 2B, L_d],
  * cell (r, d) = batch rows [rB, (r+1)B)): kstride 2B*L_d, loc[2r+d] offset r*B*L_d.
  * _bwd takes dL/dlw [2K,B] and writes dloc[4] (same strides), dzs[2], dmu[2],
- * dsc[2] (null entries are skipped). */
+ * dsc[2] (null entries are skipped); K <= 256. */
 int vaesne_iwae_lw_fwd(const float* const* x, const float* llik, const int* L,
                        const float* const* loc, const float* const* scale,
                        const int64_t* kstride, const float* const* zs, const float* const* mu, const float* const* sc,

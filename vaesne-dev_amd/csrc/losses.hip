@@ -151,42 +151,56 @@ __global__ void iwae_dloc_kernel(IwaeArgs a, const float* __restrict__ dlw, floa
 //   dmu_m[b,j]   = sum_{r,k} gw ( -alpha_{rk,m} sgn(z - mu_m) / sc_m )
 //   dsc_m[b,j]   = sum_{r,k} gw ( -alpha_{rk,m} (-1/sc_m + |z - mu_m| / sc_m^2) )
 // alpha_{rk,m} = softmax_m( sum_j log q_m(z_rk) ) (recomputed per thread).
+// One workgroup per b.  Phase 1: thread t < 2K computes the mixture weights
+// alpha_{rk,m} of sample (r, k) once (a thread per (b, j) recomputed them n times:
+// 2K*n^2 serial log-probs per thread, ~55 us at cfg 5); phase 2: thread j < n sums
+// over (r, k) in the same order as before (bitwise-identical results).
+constexpr int DLAT_MAXRK = 512;
 __global__ void iwae_dlat_kernel(IwaeArgs a, const float* __restrict__ dlw, float* dz0, float* dz1,
                                  float* dmu0, float* dsc0, float* dmu1, float* dsc1) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)a.B * a.n) return;
-  const int b = (int)(t / a.n), j = (int)(t - (int64_t)b * a.n);
-  const float mu0 = a.mu[0][t], sc0 = a.sc[0][t], mu1 = a.mu[1][t], sc1 = a.sc[1][t];
-  const float pl = a.pz_loc[j], ps = a.pz_scale[j];
-  float gm0 = 0.f, gs0 = 0.f, gm1 = 0.f, gs1 = 0.f;
-  for (int r = 0; r < 2; ++r) {
-    for (int k = 0; k < a.K; ++k) {
-      const float* zrow = a.zs[r] + ((int64_t)k * a.B + b) * a.n;
-      float lq0 = 0.f, lq1 = 0.f;
-      for (int jj = 0; jj < a.n; ++jj) {
-        float zz = zrow[jj];
-        lq0 += lap_logp(zz, a.mu[0][(int64_t)b * a.n + jj], a.sc[0][(int64_t)b * a.n + jj]);
-        lq1 += lap_logp(zz, a.mu[1][(int64_t)b * a.n + jj], a.sc[1][(int64_t)b * a.n + jj]);
-      }
-      float mx = fmaxf(lq0, lq1);
-      float e0 = expf(lq0 - mx), e1 = expf(lq1 - mx);
-      float al0 = e0 / (e0 + e1), al1 = e1 / (e0 + e1);
-      float gw = dlw[(int64_t)(r * a.K + k) * a.B + b];
-      float z = zrow[j];
-      float d0 = z - mu0, d1 = z - mu1;
-      float dz = gw * (-sgnf(z - pl) / ps + al0 * sgnf(d0) / sc0 + al1 * sgnf(d1) / sc1);
-      float* dzr = r == 0 ? dz0 : dz1;
-      if (dzr) dzr[((int64_t)k * a.B + b) * a.n + j] = dz;
-      gm0 += gw * (-al0 * sgnf(d0) / sc0);
-      gm1 += gw * (-al1 * sgnf(d1) / sc1);
-      gs0 += gw * (-al0 * (-1.f / sc0 + fabsf(d0) / (sc0 * sc0)));
-      gs1 += gw * (-al1 * (-1.f / sc1 + fabsf(d1) / (sc1 * sc1)));
+  __shared__ float al[2][DLAT_MAXRK];
+  const int b = blockIdx.x;
+  const int nrk = 2 * a.K;
+  for (int t = threadIdx.x; t < nrk; t += blockDim.x) {
+    const int r = t / a.K, k = t - r * a.K;
+    const float* zrow = a.zs[r] + ((int64_t)k * a.B + b) * a.n;
+    float lq0 = 0.f, lq1 = 0.f;
+    for (int jj = 0; jj < a.n; ++jj) {
+      float zz = zrow[jj];
+      lq0 += lap_logp(zz, a.mu[0][(int64_t)b * a.n + jj], a.sc[0][(int64_t)b * a.n + jj]);
+      lq1 += lap_logp(zz, a.mu[1][(int64_t)b * a.n + jj], a.sc[1][(int64_t)b * a.n + jj]);
     }
+    float mx = fmaxf(lq0, lq1);
+    float e0 = expf(lq0 - mx), e1 = expf(lq1 - mx);
+    al[0][t] = e0 / (e0 + e1);
+    al[1][t] = e1 / (e0 + e1);
   }
-  if (dmu0) dmu0[t] = gm0;
-  if (dsc0) dsc0[t] = gs0;
-  if (dmu1) dmu1[t] = gm1;
-  if (dsc1) dsc1[t] = gs1;
+  __syncthreads();
+  for (int j = threadIdx.x; j < a.n; j += blockDim.x) {
+    const int64_t t = (int64_t)b * a.n + j;
+    const float mu0 = a.mu[0][t], sc0 = a.sc[0][t], mu1 = a.mu[1][t], sc1 = a.sc[1][t];
+    const float pl = a.pz_loc[j], ps = a.pz_scale[j];
+    float gm0 = 0.f, gs0 = 0.f, gm1 = 0.f, gs1 = 0.f;
+    for (int r = 0; r < 2; ++r) {
+      for (int k = 0; k < a.K; ++k) {
+        const float al0 = al[0][r * a.K + k], al1 = al[1][r * a.K + k];
+        float gw = dlw[(int64_t)(r * a.K + k) * a.B + b];
+        float z = a.zs[r][((int64_t)k * a.B + b) * a.n + j];
+        float d0 = z - mu0, d1 = z - mu1;
+        float dz = gw * (-sgnf(z - pl) / ps + al0 * sgnf(d0) / sc0 + al1 * sgnf(d1) / sc1);
+        float* dzr = r == 0 ? dz0 : dz1;
+        if (dzr) dzr[((int64_t)k * a.B + b) * a.n + j] = dz;
+        gm0 += gw * (-al0 * sgnf(d0) / sc0);
+        gm1 += gw * (-al1 * sgnf(d1) / sc1);
+        gs0 += gw * (-al0 * (-1.f / sc0 + fabsf(d0) / (sc0 * sc0)));
+        gs1 += gw * (-al1 * (-1.f / sc1 + fabsf(d1) / (sc1 * sc1)));
+      }
+    }
+    if (dmu0) dmu0[t] = gm0;
+    if (dsc0) dsc0[t] = gs0;
+    if (dmu1) dmu1[t] = gm1;
+    if (dsc1) dsc1[t] = gs1;
+  }
 }
 
 // ---------------------------------------------------------------- elbo ----
@@ -327,8 +341,9 @@ VAESNE_API int vaesne_iwae_lw_bwd(const float* const* x, const float* llik, cons
   hipLaunchKernelGGL(iwae_dloc_kernel, dim3(nblk(tot)), dim3(NT), 0, s, a, dlw, dloc[0], dloc[1],
                      dloc[2], dloc[3]);
   VAESNE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(iwae_dlat_kernel, dim3(nblk((int64_t)B * n)), dim3(NT), 0, s, a, dlw, dzs[0],
-                     dzs[1], dmu[0], dsc[0], dmu[1], dsc[1]);
+  if (2 * K > DLAT_MAXRK) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(iwae_dlat_kernel, dim3((unsigned)B), dim3(64), 0, s, a, dlw, dzs[0], dzs[1],
+                     dmu[0], dsc[0], dmu[1], dsc[1]);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
