@@ -184,11 +184,12 @@ int vaesne_attn_rep_bwd(const float* qkv, int64_t qkv_bs, int64_t qkv_ls, const 
                         const float* dout, float* dqkv, int Bd, int R, int H, int L, int dh,
                         float p_drop, const int64_t* rng_state, uint32_t call_id,
                         const uint32_t* keep_bits, float* workspace, void* stream);
-/* Tuning / test hook for the two kernels above: forward fnt threads (0 = auto) x frc
- * copies per workgroup (2, 4, 8); backward bnt threads (128, 256) x 2*bnp keys per
- * lane (bnp 1, 2), brc copies per staged tile (8, 16), ~bwgs workgroups.  fnt < 0
- * restores the defaults.  Process-wide; not while launches are in flight. */
-int vaesne_attn_rep_config(int fnt, int frc, int bnt, int bnp, int brc, int bwgs);
+/* Tuning / test hook for the two kernels above: forward fnt threads (0 = auto) x 2*fnp
+ * queries per lane (fnp 1, 2) x frc copies per workgroup (2, 4, 8; 2, 4 with fnp 2);
+ * backward bnt threads (128, 256) x 2*bnp keys per lane (bnp 1, 2), brc copies per
+ * staged tile (8, 16), ~bwgs workgroups.  fnt < 0 restores the defaults.
+ * Process-wide; not while launches are in flight. */
+int vaesne_attn_rep_config(int fnt, int frc, int bnt, int bnp, int brc, int bwgs, int fnp);
 
 /* Test / tuning hook: force the query-tiled attention kernels' geometry (nt threads
  * per workgroup in {64, 128, 256}, np in {1, 2}: 2*np rows per lane); nt = 0 restores

@@ -64,35 +64,35 @@ def _rep_fwd(lib, qkv, kb, Bd, R, L, p, st, cid):
     return o, lse, bits
 
 
-@pytest.mark.parametrize("frc", [2, 4, 8])
+@pytest.mark.parametrize("fnp,frc", [(1, 2), (1, 4), (1, 8), (2, 2), (2, 4)])
 @pytest.mark.parametrize("Bd,R,L,pm,p", [(2, 16, 982, 0.05, 0.1), (3, 6, 60, 0.1, 0.1),
                                          (2, 5, 37, 0.0, 0.1), (1, 16, 300, 0.3, 0.0),
                                          (2, 1, 129, 0.05, 0.1)])
-def test_rep_forward_bitwise_equals_plain_forward(frc, Bd, R, L, pm, p):
-    """Same query-to-wave mapping (plain geometry 256 x 1 = rep forward at 256
-    threads): identical arithmetic per copy, so o, lse and the bitmap are equal."""
+def test_rep_forward_bitwise_equals_plain_forward(fnp, frc, Bd, R, L, pm, p):
+    """Same query-to-wave mapping (plain geometry 256 x fnp = rep forward at 256
+    threads x fnp): identical arithmetic per copy, so o, lse and the bitmap are equal."""
     from VAESNe import _lib, rng
     lib = _lib.lib
     qkv, kb, kb_full, qkv_full = _inputs(Bd, R, L, pm, 11 * L + R)
     st = rng.state(DEV)
     N = R * Bd
-    assert lib.attn_force_geometry(256, 1) == 0
-    assert lib.attn_rep_config(256, frc, 256, 1, 16, 768) == 0
+    assert lib.attn_force_geometry(256, fnp) == 0
+    assert lib.attn_rep_config(256, frc, 256, 1, 16, 768, fnp) == 0
     try:
         o0, l0, b0 = _plain_fwd(lib, qkv_full, kb_full, N, L, p, st, 4242)
         o1, l1, b1 = _rep_fwd(lib, qkv, kb, Bd, R, L, p, st, 4242)
         torch.cuda.synchronize()
     finally:
         lib.attn_force_geometry(0, 0)
-        lib.attn_rep_config(-1, 0, 0, 0, 0, 0)
+        lib.attn_rep_config(-1, 0, 0, 0, 0, 0, 0)
     assert torch.equal(o0, o1)
     assert torch.equal(l0.view(R, Bd, H, L), l1.unsqueeze(0).expand(R, Bd, H, L))
     if p > 0:
         assert torch.equal(b0, b1)
 
 
-@pytest.mark.parametrize("cfg", [(0, 4, 256, 1, 16, 768), (64, 8, 128, 2, 8, 64),
-                                 (128, 2, 256, 2, 16, 4000), (0, 4, 128, 1, 8, 300)])
+@pytest.mark.parametrize("cfg", [(0, 4, 256, 1, 16, 768, 1), (64, 8, 128, 2, 8, 64, 1),
+                                 (128, 2, 256, 2, 16, 4000, 2), (0, 4, 128, 1, 8, 300, 2)])
 @pytest.mark.parametrize("Bd,R,L,pm,p", [(2, 16, 982, 0.05, 0.1), (3, 6, 60, 0.1, 0.1),
                                          (2, 19, 37, 0.0, 0.1), (2, 16, 300, 0.3, 0.0),
                                          (1, 3, 983, 0.05, 0.1)])
@@ -117,7 +117,7 @@ def test_rep_backward_equals_summed_plain_backward(cfg, Bd, R, L, pm, p):
             res.append((o.detach(), dx))
         torch.cuda.synchronize()
     finally:
-        lib.attn_rep_config(-1, 0, 0, 0, 0, 0)
+        lib.attn_rep_config(-1, 0, 0, 0, 0, 0, 0)
     (o0, d0), (o1, d1) = res
     assert _rel(o1, o0) < 1e-5     # plain launch may split the key axis (chunk combine)
     for sl in (slice(0, E), slice(E, 2 * E), slice(2 * E, 3 * E)):     # dQ, dK, dV

@@ -63,7 +63,7 @@ SIGNATURES = {
                                   P, U32, P, P]),
     "vaesne_attn_rep_bwd": (I32, [P, I64, I64, P, I64, P, I64, I64, P, P, P, I32, I32, I32, I32, I32,
                                   F32, P, U32, P, P, P]),
-    "vaesne_attn_rep_config": (I32, [I32, I32, I32, I32, I32, I32]),
+    "vaesne_attn_rep_config": (I32, [I32, I32, I32, I32, I32, I32, I32]),
     "vaesne_enc_block_fwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P]),
     "vaesne_enc_block_bwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P, P, P, P, P, P,
                                    P]),

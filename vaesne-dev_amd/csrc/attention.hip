@@ -757,40 +757,45 @@ __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
 // the expanded input reproduce these bit for bit (tested).
 // Args: q/k/v/kbias/lse over the Bd distinct sequences (a.B = Bd), o / dout / bits
 // over the N sequences (o_bs, do_bs = per-sequence strides).
-template <int DH, int NTT, int RC, bool DROP>
+template <int DH, int NTT, int NP, int RC, bool DROP>
 __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R) {
   __shared__ __attribute__((aligned(16))) float Ks[TK * DH];
   __shared__ __attribute__((aligned(16))) float Vs[TK * DH];
   __shared__ float Kb[TK];
+  constexpr int R2 = 2 * NP;              // queries per lane (pairs p = {2p, 2p + 1})
+  constexpr int QB = R2 * NTT;
   constexpr int NC = DROP ? RC : 1;       // accumulator sets (no dropout: one for all copies)
-  const int nqb = (a.Lq + 2 * NTT - 1) / (2 * NTT);
+  const int nqb = (a.Lq + QB - 1) / QB;
   const int qb = blockIdx.x % nqb;
   const int bh = blockIdx.x / nqb;        // distinct sequence x head
   const int b = bh / a.H, h = bh - b * a.H;
   const int c0 = blockIdx.y * RC;
-  int qi[2], qc[2];
+  int qi[R2], qc[R2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    qi[u] = qb * 2 * NTT + u * NTT + threadIdx.x;
+  for (int u = 0; u < R2; ++u) {
+    qi[u] = qb * QB + u * NTT + threadIdx.x;
     qc[u] = min(qi[u], a.Lq - 1);
   }
-  f2 q[DH], o[NC][DH], m, l;
+  f2 q[NP][DH], o[NC][NP][DH], m[NP], l[NP];
   {
     const float* qbase = a.q + (int64_t)b * a.q_bs + h * DH;
-    float t0[DH], t1[DH];
-    ldr<DH>(qbase + (int64_t)qc[0] * a.q_ls, t0);
-    ldr<DH>(qbase + (int64_t)qc[1] * a.q_ls, t1);
 #pragma unroll
-    for (int d = 0; d < DH; ++d) q[d] = (f2){t0[d], t1[d]} * a.scale_log2;
+    for (int p = 0; p < NP; ++p) {
+      float t0[DH], t1[DH];
+      ldr<DH>(qbase + (int64_t)qc[2 * p] * a.q_ls, t0);
+      ldr<DH>(qbase + (int64_t)qc[2 * p + 1] * a.q_ls, t1);
 #pragma unroll
-    for (int c = 0; c < NC; ++c)
+      for (int d = 0; d < DH; ++d) q[p][d] = (f2){t0[d], t1[d]} * a.scale_log2;
 #pragma unroll
-      for (int d = 0; d < DH; ++d) o[c][d] = bc(0.f);
-    m = bc(-INFINITY);
-    l = bc(0.f);
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int d = 0; d < DH; ++d) o[c][p][d] = bc(0.f);
+      m[p] = bc(-INFINITY);
+      l[p] = bc(0.f);
+    }
   }
   // copies past R (R % RC != 0) are computed with copy R - 1's keys and not stored
-  uint32_t rk[NC][2];
+  uint32_t rk[NC][R2];
   uint32_t* bitp[NC];
   uint32_t skey = 0u;
   if (DROP) {
@@ -800,7 +805,7 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R) {
       const int64_t nh = (int64_t)(min(c0 + c, R - 1) * a.B + b) * a.H + h;
       bitp[c] = a.bits + nh * a.nw * a.Lq;
 #pragma unroll
-      for (int u = 0; u < 2; ++u) rk[c][u] = attn_row_key(skey, (uint32_t)(nh * a.Lq + qc[u]));
+      for (int u = 0; u < R2; ++u) rk[c][u] = attn_row_key(skey, (uint32_t)(nh * a.Lq + qc[u]));
     }
   }
   const float* kg = a.k + (int64_t)b * a.k_bs + h * DH;
@@ -814,39 +819,61 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R) {
       Kb[i] = kt + i < a.Lk ? (kbg ? kbg[kt + i] : 0.f) : -INFINITY;
     __syncthreads();
     const int kend = min(TK, a.Lk - kt);
-    uint32_t w[NC][2];
+    uint32_t w[NC][R2];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) w[c][0] = w[c][1] = 0u;
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int u = 0; u < R2; ++u) w[c][u] = 0u;
     for (int g0 = 0; g0 < kend; g0 += 8) {
-      f2 s[8];
-      f2 x = m;
+      f2 s[NP][8];
+      f2 x[NP];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) x[p] = m[p];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         f2 kr[DH / 2];
         lrow2<DH>(Ks + (g0 + u) * DH, kr);
-        f2 acc = bc(Kb[g0 + u]);
+        const float kb = Kb[g0 + u];
 #pragma unroll
-        for (int d = 0; d < DH; ++d) acc = fma2r<DH>(q[d], kr, d, acc);
-        s[u] = acc;
-        x = __builtin_elementwise_max(x, acc);
+        for (int p = 0; p < NP; ++p) {
+          f2 acc = bc(kb);
+#pragma unroll
+          for (int d = 0; d < DH; ++d) acc = fma2r<DH>(q[p][d], kr, d, acc);
+          s[p][u] = acc;
+          x[p] = __builtin_elementwise_max(x[p], acc);
+        }
       }
       // lazy rescaling, as attn_fwd_kernel (wave-uniform, first groups only)
-      if (__any((x.x > m.x + 8.f) | (x.y > m.y + 8.f))) {
-        const f2 mo = (f2){m.x == -INFINITY ? 0.f : m.x, m.y == -INFINITY ? 0.f : m.y};
-        const f2 mn = (f2){x.x == -INFINITY ? 0.f : x.x, x.y == -INFINITY ? 0.f : x.y};
-        const f2 cf = ex2(mo - mn);
-        m = x;
-        l *= cf;
+      bool move = false;
 #pragma unroll
-        for (int c = 0; c < NC; ++c)
+      for (int p = 0; p < NP; ++p) move |= (x[p].x > m[p].x + 8.f) | (x[p].y > m[p].y + 8.f);
+      if (__any(move)) {
 #pragma unroll
-          for (int d = 0; d < DH; ++d) o[c][d] *= cf;
+        for (int p = 0; p < NP; ++p) {
+          const f2 mo = (f2){m[p].x == -INFINITY ? 0.f : m[p].x, m[p].y == -INFINITY ? 0.f : m[p].y};
+          const f2 mn = (f2){x[p].x == -INFINITY ? 0.f : x[p].x, x[p].y == -INFINITY ? 0.f : x[p].y};
+          const f2 cf = ex2(mo - mn);
+          m[p] = x[p];
+          l[p] *= cf;
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+#pragma unroll
+            for (int d = 0; d < DH; ++d) o[c][p][d] *= cf;
+        }
       }
-      const f2 mu = (f2){m.x == -INFINITY ? 0.f : m.x, m.y == -INFINITY ? 0.f : m.y};
+      f2 mu[NP];
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        mu[p] = (f2){m[p].x == -INFINITY ? 0.f : m[p].x, m[p].y == -INFINITY ? 0.f : m[p].y};
 #pragma unroll
       for (int u = 0; u < 8; u += 2) {
-        const f2 p0 = ex2(s[u] - mu), p1 = ex2(s[u + 1] - mu);
-        l += p0 + p1;
+        f2 p0[NP], p1[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          p0[p] = ex2(s[p][u] - mu[p]);
+          p1[p] = ex2(s[p][u + 1] - mu[p]);
+          l[p] += p0[p] + p1[p];
+        }
         f2 v0[DH / 2], v1[DH / 2];
         lrow2<DH>(Vs + (g0 + u) * DH, v0);
         lrow2<DH>(Vs + (g0 + u + 1) * DH, v1);
@@ -855,27 +882,32 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R) {
           const int sh = (g0 + u) & 31;
 #pragma unroll
           for (int c = 0; c < NC; ++c) {
-            uint32_t kk[2];
+            uint32_t kk[R2];
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
+            for (int t = 0; t < R2; ++t) {
               const uint32_t bits = attn_pair_bits_mixed(rk[c][t], kpm);
               kk[t] = ((bits & 0xffffu) >= a.thr ? 1u : 0u) | ((bits >> 16) >= a.thr ? 2u : 0u);
               w[c][t] |= kk[t] << sh;
             }
-            const f2 a0 = sel2(kk[0] & 1u, kk[1] & 1u, p0);
-            const f2 a1 = sel2(kk[0] & 2u, kk[1] & 2u, p1);
 #pragma unroll
-            for (int d = 0; d < DH; ++d) {
-              o[c][d] = fma2r<DH>(a0, v0, d, o[c][d]);
-              o[c][d] = fma2r<DH>(a1, v1, d, o[c][d]);
+            for (int p = 0; p < NP; ++p) {
+              const f2 a0 = sel2(kk[2 * p] & 1u, kk[2 * p + 1] & 1u, p0[p]);
+              const f2 a1 = sel2(kk[2 * p] & 2u, kk[2 * p + 1] & 2u, p1[p]);
+#pragma unroll
+              for (int d = 0; d < DH; ++d) {
+                o[c][p][d] = fma2r<DH>(a0, v0, d, o[c][p][d]);
+                o[c][p][d] = fma2r<DH>(a1, v1, d, o[c][p][d]);
+              }
             }
           }
         } else {
 #pragma unroll
-          for (int d = 0; d < DH; ++d) {
-            o[0][d] = fma2r<DH>(p0, v0, d, o[0][d]);
-            o[0][d] = fma2r<DH>(p1, v1, d, o[0][d]);
-          }
+          for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int d = 0; d < DH; ++d) {
+              o[0][p][d] = fma2r<DH>(p0[p], v0, d, o[0][p][d]);
+              o[0][p][d] = fma2r<DH>(p1[p], v1, d, o[0][p][d]);
+            }
         }
       }
       if (DROP && (((g0 + 8) & 31) == 0 || g0 + 8 >= kend)) {
@@ -884,23 +916,29 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R) {
         for (int c = 0; c < NC; ++c) {
           if (c0 + c < R) {
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
+            for (int t = 0; t < R2; ++t)
               if (qi[t] < a.Lq) bitp[c][(int64_t)word * a.Lq + qi[t]] = w[c][t];
           }
-          w[c][0] = w[c][1] = 0u;
+#pragma unroll
+          for (int t = 0; t < R2; ++t) w[c][t] = 0u;
         }
       }
     }
   }
   // l == 0 (every key masked) -> NaN, as the reference
-  const f2 inv = bc(DROP ? a.inv_keep : 1.f) / l;
-  auto put = [&](const f2 (&oc)[DH], int r) {
-    float r0[DH], r1[DH];
+  f2 inv[NP];
 #pragma unroll
-    for (int d = 0; d < DH; ++d) { r0[d] = oc[d].x * inv.x; r1[d] = oc[d].y * inv.y; }
-    float* ob = a.o_out + (int64_t)(r * a.B + b) * a.o_bs + h * DH;
-    if (qi[0] < a.Lq) str<DH>(ob + (int64_t)qi[0] * a.o_ls, r0);
-    if (qi[1] < a.Lq) str<DH>(ob + (int64_t)qi[1] * a.o_ls, r1);
+  for (int p = 0; p < NP; ++p) inv[p] = bc(DROP ? a.inv_keep : 1.f) / l[p];
+  auto put = [&](const f2 (&oc)[NP][DH], int r) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      float r0[DH], r1[DH];
+#pragma unroll
+      for (int d = 0; d < DH; ++d) { r0[d] = oc[p][d].x * inv[p].x; r1[d] = oc[p][d].y * inv[p].y; }
+      float* ob = a.o_out + (int64_t)(r * a.B + b) * a.o_bs + h * DH;
+      if (qi[2 * p] < a.Lq) str<DH>(ob + (int64_t)qi[2 * p] * a.o_ls, r0);
+      if (qi[2 * p + 1] < a.Lq) str<DH>(ob + (int64_t)qi[2 * p + 1] * a.o_ls, r1);
+    }
   };
   if (DROP) {
 #pragma unroll
@@ -910,8 +948,11 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R) {
     for (int r = 0; r < R; ++r) put(o[0], r);   // every copy the same
   }
   if (blockIdx.y == 0) {   // shared over the copies
-    if (qi[0] < a.Lq) a.lse[(int64_t)bh * a.Lq + qi[0]] = m.x + __log2f(l.x);
-    if (qi[1] < a.Lq) a.lse[(int64_t)bh * a.Lq + qi[1]] = m.y + __log2f(l.y);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      if (qi[2 * p] < a.Lq) a.lse[(int64_t)bh * a.Lq + qi[2 * p]] = m[p].x + __log2f(l[p].x);
+      if (qi[2 * p + 1] < a.Lq) a.lse[(int64_t)bh * a.Lq + qi[2 * p + 1]] = m[p].y + __log2f(l[p].y);
+    }
   }
 }
 
@@ -1714,28 +1755,32 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
 // forward: fnt threads x 2 queries per lane, frc copies per workgroup (frc sets of
 // 8 packed accumulators); backward: bnt threads x 2*bnp keys per lane, brc copies
 // per staged tile, query chunks sized so the grid has ~bwgs workgroups.
-// VAESNE_REP="fnt,frc,bnt,bnp,brc,bwgs" overrides (tuning / tests).
-struct RepCfg { int fnt, frc, bnt, bnp, brc, bwgs; };
+// forward fnp query pairs per lane.  VAESNE_REP="fnt,frc,bnt,bnp,brc,bwgs,fnp" overrides
+// (tuning / tests).
+struct RepCfg { int fnt, frc, bnt, bnp, brc, bwgs, fnp; };
+const RepCfg kRepDefault{0, 2, 256, 1, 16, 1536, 2};
 RepCfg g_rep = [] {
-  RepCfg c{0, 2, 256, 1, 16, 1536};
+  RepCfg c = kRepDefault;
   if (const char* e = getenv("VAESNE_REP"))
-    sscanf(e, "%d,%d,%d,%d,%d,%d", &c.fnt, &c.frc, &c.bnt, &c.bnp, &c.brc, &c.bwgs);
+    sscanf(e, "%d,%d,%d,%d,%d,%d,%d", &c.fnt, &c.frc, &c.bnt, &c.bnp, &c.brc, &c.bwgs, &c.fnp);
   return c;
 }();
 bool rep_cfg_ok(const RepCfg& c) {
   return (c.fnt == 0 || c.fnt == 64 || c.fnt == 128 || c.fnt == 256) &&
          (c.frc == 2 || c.frc == 4 || c.frc == 8) && (c.bnt == 128 || c.bnt == 256) &&
-         (c.bnp == 1 || c.bnp == 2) && (c.brc == 8 || c.brc == 16) && c.bwgs > 0;
+         (c.bnp == 1 || c.bnp == 2) && (c.brc == 8 || c.brc == 16) && c.bwgs > 0 &&
+         (c.fnp == 1 || (c.fnp == 2 && c.frc <= 4));
 }
-int rep_fwd_nt(int64_t bh, int L, int cb) {
+int rep_fwd_nt(int64_t bh, int L, int cb, int np) {
   if (g_rep.fnt > 0) return g_rep.fnt;
   // fewest wasted query slots among grids of >= 1024 workgroups (else 64 threads)
   const int nts[3] = {256, 128, 64};
   int best = 64;
   double best_eff = -1.0;
   for (int nt : nts) {
-    const int64_t nb = (L + 2 * nt - 1) / (2 * nt);
-    const double eff = (double)L / (double)(2 * nt * nb);
+    const int rows = 2 * np * nt;
+    const int64_t nb = (L + rows - 1) / rows;
+    const double eff = (double)L / (double)(rows * nb);
     if (bh * nb * cb >= 1024 && eff > best_eff + 1e-9) { best = nt; best_eff = eff; }
   }
   return best;
@@ -1768,14 +1813,17 @@ int launch_rep_fwd(const AttnArgs& a, int R, float p_drop, hipStream_t s) {
   const bool drop = p_drop > 0.f;
   const int rc = drop ? g_rep.frc : 1;
   const int cb = drop ? (R + rc - 1) / rc : 1;
-  const int nt = rep_fwd_nt((int64_t)a.B * a.H, a.Lq, cb);
-  const int nqb = (a.Lq + 2 * nt - 1) / (2 * nt);
+  const int np = drop ? g_rep.fnp : 1;
+  const int nt = rep_fwd_nt((int64_t)a.B * a.H, a.Lq, cb, np);
+  const int nqb = (a.Lq + 2 * np * nt - 1) / (2 * np * nt);
   const dim3 grid((unsigned)((int64_t)a.B * a.H * nqb), (unsigned)cb);
 #define VAESNE_REP_FWD(NT)                                                                        \
-  if (!drop) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, false>), grid, dim3(NT), 0, s, a, R); \
-  else if (rc == 2) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 2, true>), grid, dim3(NT), 0, s, a, R); \
-  else if (rc == 4) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 4, true>), grid, dim3(NT), 0, s, a, R); \
-  else hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 8, true>), grid, dim3(NT), 0, s, a, R);
+  if (!drop) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, 1, false>), grid, dim3(NT), 0, s, a, R); \
+  else if (np == 2 && rc == 2) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 2, 2, true>), grid, dim3(NT), 0, s, a, R); \
+  else if (np == 2) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 2, 4, true>), grid, dim3(NT), 0, s, a, R); \
+  else if (rc == 2) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, 2, true>), grid, dim3(NT), 0, s, a, R); \
+  else if (rc == 4) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, 4, true>), grid, dim3(NT), 0, s, a, R); \
+  else hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, 8, true>), grid, dim3(NT), 0, s, a, R);
   if (nt == 256) { VAESNE_REP_FWD(256) } else if (nt == 128) { VAESNE_REP_FWD(128) } else { VAESNE_REP_FWD(64) }
 #undef VAESNE_REP_FWD
   VAESNE_CHECK_LAUNCH();
@@ -1847,9 +1895,10 @@ int launch_rep_bwd(const AttnArgs& a, int R, float p_drop, float* ws, hipStream_
 
 }  // namespace
 
-VAESNE_API int vaesne_attn_rep_config(int fnt, int frc, int bnt, int bnp, int brc, int bwgs) {
-  if (fnt < 0) { g_rep = RepCfg{0, 2, 256, 1, 16, 1536}; return 0; }
-  const RepCfg c{fnt, frc, bnt, bnp, brc, bwgs};
+VAESNE_API int vaesne_attn_rep_config(int fnt, int frc, int bnt, int bnp, int brc, int bwgs,
+                                      int fnp) {
+  if (fnt < 0) { g_rep = kRepDefault; return 0; }
+  const RepCfg c{fnt, frc, bnt, bnp, brc, bwgs, fnp};
   if (!rep_cfg_ok(c)) return (int)hipErrorInvalidValue;
   g_rep = c;
   return 0;
