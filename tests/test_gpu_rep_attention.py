@@ -127,8 +127,11 @@ def test_rep_backward_equals_summed_plain_backward(cfg, Bd, R, L, pm, p):
 def test_rep_decoder_stack_and_model_step_equal_expanded_path(monkeypatch):
     """A cfg-5-shaped MMVAE training step (dropout on) with the repeated first-block
     attention against VAESNE_REP_ATTN=0 (expanded input, plain kernels): the same
-    dropout call ids, so loss and every parameter gradient agree to fp32 summation
-    order."""
+    dropout call ids, so the loss agrees to fp32 summation order (1e-5) and so do
+    the gradients, up to the importance weights: lw sums ~10^3 log-probabilities, so
+    a 1e-7 relative change in a decoder location moves lw by ~1e-4 and the softmax
+    weights over the K samples by as much (gradients max-abs-relative 2e-3).  The
+    repeated path itself is bitwise reproducible (a stream race would not be)."""
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -140,7 +143,7 @@ def test_rep_decoder_stack_and_model_step_equal_expanded_path(monkeypatch):
     model.train()
     x = bench.synthetic_batch(2, 5, DEV)
     outs = []
-    for flag in ("0", "1"):
+    for flag in ("0", "1", "1"):
         monkeypatch.setenv("VAESNE_REP_ATTN", flag)
         model.zero_grad(set_to_none=True)
         rng.manual_seed(77)
@@ -148,8 +151,10 @@ def test_rep_decoder_stack_and_model_step_equal_expanded_path(monkeypatch):
         loss.backward()
         outs.append((loss.item(), {n: p.grad.detach().clone() for n, p in model.named_parameters()
                                    if p.grad is not None}))
-    (l0, g0), (l1, g1) = outs
+    (l0, g0), (l1, g1), (l2, g2) = outs
     assert abs(l1 - l0) <= 1e-5 * abs(l0)
-    assert g0.keys() == g1.keys()
+    assert g0.keys() == g1.keys() == g2.keys()
+    assert l1 == l2
     for n in g0:
-        assert _rel(g1[n], g0[n]) < 1e-4, (n, _rel(g1[n], g0[n]))
+        assert torch.equal(g1[n], g2[n]), n
+        assert _rel(g1[n], g0[n]) < 2e-3, (n, _rel(g1[n], g0[n]))

@@ -8,8 +8,8 @@ from torch import nn
 
 from . import _chain, _ops
 from .util_layers import (MLP, Linear, SinusoidalMLPPositionalEmbedding,
-                          SinusoidalPositionalEmbedding, TransformerBlock, decoder_inputs,
-                          decoder_stack,
+                          SinusoidalPositionalEmbedding, TransformerBlock, decoder_fusable,
+                          decoder_inputs, decoder_stack, decoder_stack_first,
                           singlelayerMLP, encoder_stack_steps)
 
 
@@ -31,19 +31,35 @@ class photometricTransformerDecoder(nn.Module):
         self.get_photo = singlelayerMLP(model_dim, 1)
         self.donotmask = donotmask
 
-    def forward(self, time, band, bottleneck, mask=None, repeat=1):
+    def forward(self, time, band, bottleneck, mask=None, repeat=1, prepared=None):
         """`repeat` > 1: time / band hold the B distinct rows of the N = repeat * B
         sequences (PhotometricVAE.py:190-193 expand): the embedding runs on the B rows
-        and is broadcast (its gradient summed over the copies)."""
+        and is broadcast (its gradient summed over the copies).  `prepared`: this
+        call's prepare() result, computed ahead."""
+        if self.donotmask:
+            mask = None
+        if prepared is None:
+            prepared = self.prepare(time, band, mask, repeat, bottleneck.shape[1])
+        x_res, x_qkv, x_out, rep, first = prepared
+        bottleneck = self.contextfc(bottleneck)
+        h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, x_qkv=x_qkv, rep=rep,
+                          first=first)
+        return self.get_photo(x_out, h).squeeze(-1)   # get_photo(x + h)
+
+    def prepare(self, time, band, mask=None, repeat=1, lc=1, attend=True):
+        """The part of forward() that does not read the latents: the time / band
+        embedding and, on the fused path, block 1's in-projection and (attend)
+        its masked self-attention.  lc: context tokens (latent_len)."""
         if self.donotmask:
             mask = None
         # x = time_embd + band_embd (PhotometricLayers.py:62-64), the add fused in the gather
         x = _ops.embedding(band, self.bandembd.weight, base=self.sinusoidal_time_embd(time))
-        bottleneck = self.contextfc(bottleneck)
         # x feeds the first block twice and the head: one gradient sum (_ops.fanout)
-        x_res, x_qkv, x_out, rep = decoder_inputs(x, repeat, self.transformerblocks, bottleneck)
-        h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, x_qkv=x_qkv, rep=rep)
-        return self.get_photo(x_out, h).squeeze(-1)   # get_photo(x + h)
+        x_res, x_qkv, x_out, rep = decoder_inputs(x, repeat, self.transformerblocks, lc)
+        first = None
+        if x_res.dim() == 3 and decoder_fusable(self.transformerblocks, lc):
+            first = decoder_stack_first(self.transformerblocks, x_res, mask, None, x_qkv, rep, attend)
+        return x_res, x_qkv, x_out, rep, first
 
 
 class photometricTransformerEncoder(nn.Module):

@@ -44,11 +44,11 @@ class PhotometricDec(nn.Module):
         self.generativetransformer = photometricTransformerDecoder(
             latent_dim, num_bands, model_dim, num_heads, ff_dim, num_layers, dropout, selfattn)
 
-    def pxz(self, time, band, z, mask=None, repeat=1):
-        return self.generativetransformer(time, band, z, mask, repeat=repeat)
+    def pxz(self, time, band, z, mask=None, repeat=1, prepared=None):
+        return self.generativetransformer(time, band, z, mask, repeat=repeat, prepared=prepared)
 
-    def forward(self, time, band, z, mask=None, repeat=1):
-        x_rec = self.pxz(time, band, z, mask, repeat=repeat)
+    def forward(self, time, band, z, mask=None, repeat=1, prepared=None):
+        x_rec = self.pxz(time, band, z, mask, repeat=repeat, prepared=prepared)
         if mask is None:
             var = torch.ones_like(x_rec)
         else:
@@ -112,16 +112,35 @@ class PhotometricVAE(VAE):
         wrap in the likelihood distribution [K, B, L]."""
         return self._dist(self.px_z, *self.decode_params(zs, x))
 
-    def decode_params(self, zs, x, groups=1):
+    def _dec_mask(self, x, K, groups):
+        mask = x[3]
+        B, L = x[1].shape
+        return None if mask is None else \
+            mask.unsqueeze(0).unsqueeze(0).expand(K, groups, B, L).reshape(-1, L)
+
+    def decode_prepare(self, x, K, groups=1, attend=True):
+        """The latent-independent part of decode_params(zs, x, groups) for K samples
+        (embedding, block 1's in-projection and, with attend, its self-attention):
+        -> `prepared` for decode_params."""
+        _, time, band, _ = x
+        mask = self._dec_mask(x, K, groups)
+        return (K, groups, mask, self.dec.generativetransformer.prepare(
+            time, band, mask, repeat=K * groups, lc=self.latent_len, attend=attend))
+
+    def decode_params(self, zs, x, groups=1, prepared=None):
         """(loc, scale) [K, groups*B, L] for latents zs [K, groups*B, Lz, Dz]
-        decoded at x's grid, x's batch repeated `groups` times (group-major)."""
-        _, time, band, mask = x
+        decoded at x's grid, x's batch repeated `groups` times (group-major).
+        `prepared`: decode_prepare(x, K, groups) computed ahead."""
+        _, time, band, _ = x
         K = zs.shape[0]
         B, L = time.shape
-        rep = lambda t: t.unsqueeze(0).unsqueeze(0).expand(K, groups, B, L).reshape(-1, L)
+        if prepared is not None and prepared[:2] == (K, groups):
+            mask, pre = prepared[2], prepared[3]
+        else:
+            mask, pre = self._dec_mask(x, K, groups), None
         # the time / band embedding runs once per distinct light curve (repeat = K * groups)
-        loc, scale = self.dec(time, band, zs.reshape(-1, zs.shape[-2], zs.shape[-1]),
-                              None if mask is None else rep(mask), repeat=K * groups)
+        loc, scale = self.dec(time, band, zs.reshape(-1, zs.shape[-2], zs.shape[-1]), mask,
+                              repeat=K * groups, prepared=pre)
         return loc.reshape(K, groups * B, L), scale.reshape(K, groups * B, L)
 
     def reconstruct(self, x, K=1):
@@ -165,7 +184,7 @@ class BrightPhotometricVAE(PhotometricVAE):
                          beta=beta, prior=prior, likelihood=likelihood, posterior=posterior)
         self.brightnessfc = MLP(latent_dim, 1, [model_dim])
 
-    def decode_params(self, zs, x, groups=1):
-        loc, scale = super().decode_params(zs, x, groups)
+    def decode_params(self, zs, x, groups=1, prepared=None):
+        loc, scale = super().decode_params(zs, x, groups, prepared)
         brightness = self.brightnessfc(_ops.bright_input(zs))     # [K, groups*B, 1]
         return _ops.bright_shift(loc, brightness), scale

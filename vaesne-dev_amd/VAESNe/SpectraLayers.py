@@ -10,8 +10,8 @@ from torch import nn
 
 from . import _chain, _ops
 from .util_layers import (MLP, Linear, SinusoidalMLPPositionalEmbedding,
-                          SinusoidalPositionalEmbedding, TransformerBlock, decoder_inputs,
-                          decoder_stack,
+                          SinusoidalPositionalEmbedding, TransformerBlock, decoder_fusable,
+                          decoder_inputs, decoder_stack, decoder_stack_first,
                           singlelayerMLP, encoder_stack_steps)
 
 
@@ -31,20 +31,34 @@ class spectraTransformerDecoder(nn.Module):
         self.contextfc = MLP(bottleneck_dim, model_dim, [model_dim])
         self.get_flux = singlelayerMLP(model_dim, 1)
 
-    def forward(self, wavelength, phase, bottleneck, mask=None, repeat=1):
+    def forward(self, wavelength, phase, bottleneck, mask=None, repeat=1, prepared=None):
         """`repeat` > 1: wavelength holds the B distinct rows of the N = repeat * B
         sequences (the decoders' K-sample / two-latent expand, SpectraVAE.py:189-192):
         the embedding MLP runs on the B rows and is broadcast (its gradient is the
-        sum over the copies), the rest of the decoder on N."""
+        sum over the copies), the rest of the decoder on N.  `prepared`: this call's
+        prepare() result, computed ahead (photospecMMVAE.forward: beside the encoders)."""
+        keep = self.__dict__.pop("_keep_prefetch", None)   # util_layers.prefetch_decoder_dropout
+        if prepared is None:
+            prepared = self.prepare(wavelength, phase, mask, repeat, bottleneck.shape[1] + 1, keep)
+        x_res, x_qkv, x_out, rep, phase_embd, first = prepared
+        bottleneck = torch.cat([self.contextfc(bottleneck), phase_embd], dim=1)
+        h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, keep=keep, x_qkv=x_qkv,
+                          rep=rep, first=first)
+        return self.get_flux(x_out, h).squeeze(-1)   # get_flux(x + h)
+
+    def prepare(self, wavelength, phase, mask=None, repeat=1, lc=1, keep=None, attend=True):
+        """The part of forward() that does not read the latents: the wavelength and
+        phase embeddings and, on the fused path, block 1's in-projection and (attend)
+        its masked self-attention (util_layers.decoder_stack_first).  lc: context tokens
+        (latent_len + 1)."""
         x = self.wavelength_embd_layer(wavelength)
         phase_embd = self.phase_embd_layer(phase[:, None])
-        bottleneck = torch.cat([self.contextfc(bottleneck), phase_embd], dim=1)
         # x feeds the first block twice and the head: one gradient sum (_ops.fanout)
-        x_res, x_qkv, x_out, rep = decoder_inputs(x, repeat, self.transformerblocks, bottleneck)
-        keep = self.__dict__.pop("_keep_prefetch", None)   # util_layers.prefetch_decoder_dropout
-        h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, keep=keep, x_qkv=x_qkv,
-                          rep=rep)
-        return self.get_flux(x_out, h).squeeze(-1)   # get_flux(x + h)
+        x_res, x_qkv, x_out, rep = decoder_inputs(x, repeat, self.transformerblocks, lc)
+        first = None
+        if x_res.dim() == 3 and decoder_fusable(self.transformerblocks, lc):
+            first = decoder_stack_first(self.transformerblocks, x_res, mask, keep, x_qkv, rep, attend)
+        return x_res, x_qkv, x_out, rep, phase_embd, first
 
 
 class spectraTransformerEncoder(nn.Module):

@@ -43,11 +43,11 @@ class SpectraDec(nn.Module):
         self.generativetransformer = spectraTransformerDecoder(
             latent_dim, model_dim, num_heads, ff_dim, num_layers, dropout, selfattn)
 
-    def pxz(self, wavelength, phase, z, mask=None, repeat=1):
-        return self.generativetransformer(wavelength, phase, z, mask, repeat=repeat)
+    def pxz(self, wavelength, phase, z, mask=None, repeat=1, prepared=None):
+        return self.generativetransformer(wavelength, phase, z, mask, repeat=repeat, prepared=prepared)
 
-    def forward(self, wavelength, phase, z, mask=None, repeat=1):
-        x_rec = self.pxz(wavelength, phase, z, mask, repeat=repeat)
+    def forward(self, wavelength, phase, z, mask=None, repeat=1, prepared=None):
+        x_rec = self.pxz(wavelength, phase, z, mask, repeat=repeat, prepared=prepared)
         if mask is None:
             var = torch.ones_like(x_rec)
         else:
@@ -118,18 +118,35 @@ class SpectraVAE(VAE):
         """SpectraVAE.py:186-196."""
         return self._dist(self.px_z, *self.decode_params(zs, x))
 
-    def decode_params(self, zs, x, groups=1):
-        """(loc, scale) [K, groups*B, L] for latents zs [K, groups*B, Lz, Dz]
-        decoded at x's grid, x's batch repeated `groups` times (group-major)."""
+    def _dec_inputs(self, x, K, groups):
         _, wavelength, phase, mask = x
-        K = zs.shape[0]
         B, L = wavelength.shape
         rep = lambda t: t.unsqueeze(0).unsqueeze(0).expand(K, groups, B, L).reshape(-1, L)
+        return (wavelength, phase.unsqueeze(0).unsqueeze(0).expand(K, groups, B).reshape(-1),
+                None if mask is None else rep(mask))
+
+    def decode_prepare(self, x, K, groups=1, attend=True):
+        """The latent-independent part of decode_params(zs, x, groups) for K samples
+        (embeddings, block 1's in-projection and, with attend, its self-attention):
+        -> `prepared` for decode_params."""
+        wavelength, phase, mask = self._dec_inputs(x, K, groups)
+        return (K, groups, mask, self.dec.generativetransformer.prepare(
+            wavelength, phase, mask, repeat=K * groups, lc=self.latent_len + 1, attend=attend))
+
+    def decode_params(self, zs, x, groups=1, prepared=None):
+        """(loc, scale) [K, groups*B, L] for latents zs [K, groups*B, Lz, Dz]
+        decoded at x's grid, x's batch repeated `groups` times (group-major).
+        `prepared`: decode_prepare(x, K, groups) computed ahead."""
+        K = zs.shape[0]
+        B, L = x[1].shape
+        if prepared is not None and prepared[:2] == (K, groups):
+            wavelength, phase = x[1], None
+            mask, pre = prepared[2], prepared[3]
+        else:
+            (wavelength, phase, mask), pre = self._dec_inputs(x, K, groups), None
         # the wavelength embedding runs once per distinct spectrum (repeat = K * groups)
-        loc, scale = self.dec(wavelength,
-                              phase.unsqueeze(0).unsqueeze(0).expand(K, groups, B).reshape(-1),
-                              zs.reshape(-1, zs.shape[-2], zs.shape[-1]),
-                              None if mask is None else rep(mask), repeat=K * groups)
+        loc, scale = self.dec(wavelength, phase, zs.reshape(-1, zs.shape[-2], zs.shape[-1]), mask,
+                              repeat=K * groups, prepared=pre)
         return loc.reshape(K, groups * B, L), scale.reshape(K, groups * B, L)
 
     def generate(self, N, x):
@@ -160,8 +177,8 @@ class BrightSpectraVAE(SpectraVAE):
                          likelihood=likelihood, posterior=posterior)
         self.brightnessfc = MLP(latent_dim + 1, 1, [model_dim])
 
-    def decode_params(self, zs, x, groups=1):
-        loc, scale = super().decode_params(zs, x, groups)
+    def decode_params(self, zs, x, groups=1, prepared=None):
+        loc, scale = super().decode_params(zs, x, groups, prepared)
         phase = x[2]
         brightness = self.brightnessfc(_ops.bright_input(zs, phase))   # [K, groups*B, 1]
         return _ops.bright_shift(loc, brightness), scale

@@ -25,6 +25,31 @@ def _side_stream(t):
     return st
 
 
+_PREP = {}
+
+
+def _prep_stream(t):
+    """The stream the decoders' latent-independent first parts run on, beside the
+    encoders (VAESNE_STREAMS=0: none, they run first on the current stream)."""
+    if not t.is_cuda or os.environ.get("VAESNE_STREAMS", "1") == "0":
+        return None
+    dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
+    st = _PREP.get(dev)
+    if st is None:
+        st = _PREP[dev] = torch.cuda.Stream(device=dev)
+    return st
+
+
+def _tensors(obj):
+    if isinstance(obj, torch.Tensor):
+        return [obj]
+    if isinstance(obj, (tuple, list)):
+        return [t for o in obj for t in _tensors(o)]
+    if hasattr(obj, "tensors"):
+        return obj.tensors()
+    return []
+
+
 class _Branches:
     """Run branch 0 (photometry) on a side stream and branch 1 (spectra) on the
     current stream, then join.  The photometry encoder / decoder are chains of
@@ -112,6 +137,39 @@ class photospecMMVAE(nn.Module):
             for d, vae in enumerate(self.vaes):
                 prefetch_decoder_dropout(vae.dec.generativetransformer, K * n * B,
                                          x[d][1].shape[-1], x[d][1].device)
+        # The decoders' input embeddings and first in-projections read only the decoder
+        # input grids (util_layers.decoder_stack_first), not the latents: they run on
+        # their own stream beside the latency-bound encoders
+        # The decoders' input embeddings and first in-projections (and, mode 2 / 4,
+        # block 1's self-attention) read only the decoder input grids
+        # (util_layers.decoder_stack_first), not the latents.  VAESNE_DEC_PREPARE
+        # (A/B, ms per step at cfg 5): 0 = in the decoders (10.15); 1 / 2 = on a
+        # stream of their own beside the encoders (10.60 / 10.49: one more graph
+        # branch costs more than the overlap gains); 3 / 4 (default) = on the
+        # photometry stream after its (shorter) encoder, beside the spectra encoder
+        # (10.05 / 9.79); 5 = 4 with the spectra decoder's part issued first.
+        mode = os.environ.get("VAESNE_DEC_PREPARE", "4")
+        preps, prep_ev = [None] * n, None
+        prep_ok = merged and mode != "0" and \
+            all(hasattr(v, "decode_prepare") for v in self.vaes) and \
+            not any("_keep_prefetch" in v.dec.generativetransformer.__dict__ for v in self.vaes)
+        attend = mode in ("2", "4", "5")
+
+        def prepare_all():
+            order = range(n - 1, -1, -1) if mode == "5" else range(n)
+            for d in order:
+                preps[d] = self.vaes[d].decode_prepare(x[d], K, groups=n, attend=attend)
+
+        if prep_ok and mode in ("1", "2"):
+            ps = _prep_stream(x[0][0])
+            if ps is not None:
+                ps.wait_stream(torch.cuda.current_stream())
+                _ops.used_on(ps, *[t for xd in x for t in xd if isinstance(t, torch.Tensor)])
+            with torch.cuda.stream(ps) if ps is not None else contextlib.nullcontext():
+                prepare_all()
+                if ps is not None:
+                    prep_ev = torch.cuda.Event()
+                    prep_ev.record(ps)
         qz_xs, zss = [None] * n, [None] * n
         if os.environ.get("VAESNE_ENC_GROUP", "0") == "1" and \
                 all(hasattr(v, "posterior_steps") for v in self.vaes):
@@ -126,7 +184,10 @@ class photospecMMVAE(nn.Module):
                 for m, vae in enumerate(self.vaes):
                     with br.on(m):
                         qz_xs[m], zss[m] = vae.posterior(x[m], K=K)
-                br.to_main(qz_xs[0].loc, qz_xs[0].scale, zss[0])
+                        if m == 0 and prep_ok and mode in ("3", "4", "5"):
+                            br.to_side(*x[1])
+                            prepare_all()
+                br.to_main(qz_xs[0].loc, qz_xs[0].scale, zss[0], *_tensors(preps))
         px_zs = _CellMatrix([[None for _ in range(n)] for _ in range(n)])
         if all(z.shape == zss[0].shape for z in zss):
             B = zss[0].shape[1]
@@ -135,12 +196,17 @@ class photospecMMVAE(nn.Module):
             order = list(range(n))
             if os.environ.get("VAESNE_DEC_ORDER", "") == "rev":
                 order.reverse()       # the long spectra decoder issued first
+            if prep_ev is not None:
+                main = torch.cuda.current_stream()
+                main.wait_event(prep_ev)
+                _ops.used_on(main, *_tensors(preps))
             with _Branches(side) as br:
-                br.to_side(zcat)
+                br.to_side(zcat, *_tensors(preps))
                 for d in order:
                     vae = self.vaes[d]
                     with br.on(d):
-                        px_zs.merged[d] = vae.decode_params(zcat, x[d], groups=n)
+                        px_zs.merged[d] = vae.decode_params(zcat, x[d], groups=n,
+                                                            prepared=preps[d])
                 br.to_main(*px_zs.merged[0])
             for d, vae in enumerate(self.vaes):
                 loc, scale = px_zs.merged[d]

@@ -238,10 +238,14 @@ def prefetch_decoder_dropout(decoder, N, L, device):
 
 
 def decoder_fusable(blocks, context):
-    """Whether decoder_stack runs these blocks as fused kernels (else per op)."""
+    """Whether decoder_stack runs these blocks as fused kernels (else per op).
+    `context`: the context tensor [N, Lc, E], or its token count Lc."""
     blocks = list(blocks)
-    return bool(blocks) and all(_fusable_decoder_block(b) for b in blocks) and \
-        context.dim() == 3 and context.shape[1] <= 8
+    if isinstance(context, torch.Tensor):
+        if context.dim() != 3:
+            return False
+        context = context.shape[1]
+    return bool(blocks) and all(_fusable_decoder_block(b) for b in blocks) and context <= 8
 
 
 def decoder_inputs(xd, repeat, blocks, context):
@@ -249,7 +253,8 @@ def decoder_inputs(xd, repeat, blocks, context):
     N = repeat * Bd sequences (the K samples x latents expand) -> (x_res, x_qkv, x_out,
     rep) for decoder_stack(x_res, ..., x_qkv=x_qkv, rep=rep) and the output head.
     Every use is an alias whose gradients one kernel sums (_ops.fanout); on the fused
-    path the first in-projection reads the distinct rows (rep = repeat)."""
+    path the first in-projection reads the distinct rows (rep = repeat).
+    `context`: the decoder's context tensor or its token count."""
     if repeat > 1 and decoder_fusable(blocks, context):
         xd_qkv, xd_rep = _ops.fanout(xd, 2)
         x = _ops.repeat_batch(xd_rep, repeat).reshape(repeat * xd.shape[0], *xd.shape[1:])
@@ -262,7 +267,65 @@ def decoder_inputs(xd, repeat, blocks, context):
     return x_res, x_qkv, x_out, 1
 
 
-def decoder_stack(blocks, x, context, mask=None, keep=None, x_qkv=None, rep=1):
+class DecoderFirst:
+    """What a fused decoder stack computes before it needs the context: block 1's
+    in-projection (and, with attend, its masked self-attention) read only the
+    decoder input (the embedding of the wavelength / time grid,
+    SpectraLayers.py:54-62, PhotometricLayers.py:59-67), not the latents, so they
+    can run while the encoders still work (photospecMMVAE.forward issues them on
+    their own stream)."""
+    __slots__ = ("N", "L", "kbias", "qkv", "rep", "O1", "keep")
+
+    def __init__(self, N, L, kbias, qkv, rep, O1, keep):
+        self.N, self.L, self.kbias, self.qkv, self.rep = N, L, kbias, qkv, rep
+        self.O1, self.keep = O1, keep
+
+    def tensors(self):
+        return [t for t in (self.kbias, self.qkv, self.O1) if t is not None]
+
+    def attend(self, blocks):
+        """Block 1's masked self-attention (once)."""
+        if self.O1 is None:
+            b0 = blocks[0].self_attn
+            p_attn = b0.dropout if blocks[0].training else 0.0
+            if self.rep > 1:
+                Bd = self.N // self.rep
+                self.O1 = _ops.self_attention_rep(self.qkv, None if self.kbias is None
+                                                  else self.kbias[:Bd], b0.num_heads, p_attn,
+                                                  self.rep)
+            else:
+                self.O1 = _ops.self_attention(self.qkv, None, b0.num_heads, p_attn,
+                                              kbias=self.kbias,
+                                              keep=None if self.keep is None else self.keep[0])
+            self.qkv = None
+        return self.O1
+
+
+def decoder_stack_first(blocks, x, mask=None, keep=None, x_qkv=None, rep=1, attend=True):
+    """Block 1's in-projection and (attend) self-attention of a fused decoder stack
+    (see decoder_stack): -> DecoderFirst."""
+    blocks = list(blocks)
+    E = 32
+    L = x.shape[1]
+    N = x.shape[0]
+    b0 = blocks[0].self_attn
+    qkv = _ops.linear(x if x_qkv is None else x_qkv, b0.in_proj_weight, b0.in_proj_bias)
+    kbias = _ops.key_bias(mask)          # one mask conversion for all layers
+    if keep is not None and (len(keep) != len(blocks) or any(
+            k is not None and k.shape != (N, blk.self_attn.num_heads, L, L)
+            for k, blk in zip(keep, blocks))):
+        keep = None      # prefetched for another shape: draw in the kernels
+    rep_attn = rep > 1 and (keep is None or keep[0] is None) and \
+        _ops.rep_attention_ok(qkv, b0.num_heads, rep)
+    if rep > 1 and not rep_attn:
+        qkv = _ops.repeat_batch(qkv, rep).reshape(N, L, 3 * E)
+    first = DecoderFirst(N, L, kbias, qkv, rep if rep_attn else 1, None, keep)
+    if attend:
+        first.attend(blocks)
+    return first
+
+
+def decoder_stack(blocks, x, context, mask=None, keep=None, x_qkv=None, rep=1, first=None):
     """`for blk in blocks: x = blk(x, context, mask=mask)` for the decoders
     (SpectraLayers.py:61-62, PhotometricLayers.py:66-67).  With the reference's
     decoder shape (E 32, 4 heads, ff 32, no context self-attention) each block
@@ -274,37 +337,29 @@ def decoder_stack(blocks, x, context, mask=None, keep=None, x_qkv=None, rep=1):
     `rep` > 1: x holds rep copies of Bd = N / rep distinct sequences (row r*Bd + b)
     and x_qkv is the [Bd, L, E] distinct rows: the first block's in-projection and
     self-attention scores run once per distinct sequence (_ops.self_attention_rep;
-    each copy keeps its own dropout masks); mask must be repeated the same way."""
+    each copy keeps its own dropout masks); mask must be repeated the same way.
+    `first`: block 1's in-projection and self-attention already computed
+    (decoder_stack_first on the same x / mask / rep)."""
     blocks = list(blocks)
     if x.dim() != 3 or not decoder_fusable(blocks, context):
-        if rep > 1:
-            raise RuntimeError("decoder_stack(rep > 1) needs the fused decoder blocks")
+        if rep > 1 or first is not None:
+            raise RuntimeError("decoder_stack(rep > 1 / first) needs the fused decoder blocks")
         for blk in blocks:
             x = blk(x, context, mask=mask)
         return x
-    E = 32
-    L = x.shape[1]
-    N = x.shape[0]
-    b0 = blocks[0].self_attn
-    qkv = _ops.linear(x if x_qkv is None else x_qkv, b0.in_proj_weight, b0.in_proj_bias)
+    if first is None:
+        first = decoder_stack_first(blocks, x, mask, keep, x_qkv, rep)
+    elif first.N != x.shape[0] or first.L != x.shape[1]:
+        raise RuntimeError("decoder_stack: `first` was computed for another input")
+    L, kbias, keep = first.L, first.kbias, first.keep
     # every block's cross-attention reads the context: one gradient sum for all
     ctxs = _ops.fanout(context, len(blocks))
-    kbias = _ops.key_bias(mask)          # one mask conversion for all layers
-    if keep is not None and (len(keep) != len(blocks) or any(
-            k is not None and k.shape != (N, blk.self_attn.num_heads, L, L)
-            for k, blk in zip(keep, blocks))):
-        keep = None      # prefetched for another shape: draw in the kernels
-    rep_attn = rep > 1 and (keep is None or keep[0] is None) and \
-        _ops.rep_attention_ok(qkv, b0.num_heads, rep)
-    if rep > 1 and not rep_attn:
-        qkv = _ops.repeat_batch(qkv, rep).reshape(N, L, 3 * E)
+    qkv = None
     for i, blk in enumerate(blocks):
         p_attn = blk.self_attn.dropout if blk.training else 0.0
         p = blk.dropout.p if blk.training else 0.0
-        if i == 0 and rep_attn:
-            Bd = N // rep
-            O = _ops.self_attention_rep(qkv, None if kbias is None else kbias[:Bd],
-                                        blk.self_attn.num_heads, p_attn, rep)
+        if i == 0:
+            O = first.attend(blocks)
         else:
             O = _ops.self_attention(qkv, None, blk.self_attn.num_heads, p_attn, kbias=kbias,
                                     keep=None if keep is None else keep[i])

@@ -1758,7 +1758,7 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
 // forward fnp query pairs per lane.  VAESNE_REP="fnt,frc,bnt,bnp,brc,bwgs,fnp" overrides
 // (tuning / tests).
 struct RepCfg { int fnt, frc, bnt, bnp, brc, bwgs, fnp; };
-const RepCfg kRepDefault{0, 2, 256, 1, 16, 1536, 2};
+const RepCfg kRepDefault{0, 2, 256, 1, 16, 1536, 1};
 RepCfg g_rep = [] {
   RepCfg c = kRepDefault;
   if (const char* e = getenv("VAESNE_REP"))
