@@ -80,6 +80,23 @@ int vaesne_linear_bwd_weight(const float* dy, int64_t lddy, const float* z, int6
                              int64_t M, int O, int I, float* dW, float* db, int accum,
                              float* workspace, vaesne_colsum_list* defer, void* stream);
 
+/* ---- decoder output head ----------------------------------------------------
+ * singlelayerMLP(E -> 1) on the decoder's residual sum (util_layers.py:9-18 as
+ * SpectraLayers.py:63 get_flux(x + h) and PhotometricLayers.py:69 get_photo(x + h)
+ * call it):  y[t] = W2 . relu(W1 (x[t] + h[t]) + b1) + b2, one pass, E = 32, h may be
+ * null.  Backward: ds = d(x + h) [M, E] and g = d(W1 s + b1) [M, E] (dense), the fc2
+ * weight / bias gradients dW2 [E], db2 [1] as fixed-order sums of per-workgroup
+ * partials (workspace: vaesne_mlp_head_bwd_workspace bytes; now, or deferred); the
+ * fc1 weight gradient is vaesne_linear_bwd_weight(dy = g, x, x2 = h). */
+int vaesne_mlp_head_fwd(const float* x, int64_t ldx, const float* h, int64_t ldh, int64_t M,
+                        int E, const float* W1, const float* b1, const float* W2, const float* b2,
+                        float* y, void* stream);
+int64_t vaesne_mlp_head_bwd_workspace(int64_t M, int E);
+int vaesne_mlp_head_bwd(const float* x, int64_t ldx, const float* h, int64_t ldh, const float* dy,
+                        int64_t M, int E, const float* W1, const float* b1, const float* W2,
+                        float* ds, float* g, float* dW2, float* db2, float* workspace,
+                        vaesne_colsum_list* defer, void* stream);
+
 /* ---- post-LN residual join ------------------------------------------------
  * TransformerBlock: x = LayerNorm(x + Dropout(res))  util_layers.py:291,298,303,307
  * (nn.LayerNorm eps 1e-5; nn.Dropout p).  mean/rstd [M] saved for backward. */

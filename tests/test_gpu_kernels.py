@@ -673,3 +673,45 @@ def test_prefetched_decoder_bitmaps_give_the_hashing_result():
     assert torch.equal(dx0, dx1) and torch.equal(dc0, dc1)
     for a, b in zip(g0, g1):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,with_h,defer", [(982 * 3, True, False), (251392, True, True),
+                                            (77, False, False), (1, True, False)])
+def test_fused_mlp_head_matches_two_linears(M, with_h, defer, monkeypatch):
+    """singlelayerMLP(32 -> 1) on x (+ h) (util_layers.py:9-18, the decoders'
+    get_flux / get_photo heads): the fused kernel pair (vaesne_mlp_head_fwd/bwd)
+    against the two-linear path (fc1 + ReLU, fc2), forward and every gradient.
+    Tokens with a pre-activation within 1e-3 of the ReLU kink get dy = 0: the two
+    paths sum in different orders, so there a ReLU decision may legitimately flip."""
+    from VAESNe import _defer
+    from VAESNe.util_layers import singlelayerMLP
+    g = torch.Generator().manual_seed(M)
+    head = singlelayerMLP(32, 1)
+    x0 = torch.randn(M, 32, generator=g)
+    h0 = torch.randn(M, 32, generator=g) if with_h else None
+    dy = torch.randn(M, 1, generator=g)
+    s64 = (x0 if h0 is None else x0 + h0).double()
+    z64 = s64 @ head.fc1.weight.detach().double().T + head.fc1.bias.detach().double()
+    dy[(z64.abs() < 1e-3).any(dim=1)] = 0.0
+    head = head.to(DEV)
+    x0, dy = x0.to(DEV), dy.to(DEV)
+    h0 = None if h0 is None else h0.to(DEV)
+    res = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("VAESNE_FUSED_HEAD", fused)
+        head.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        h = None if h0 is None else h0.clone().requires_grad_(True)
+        with _defer.deferred(defer):
+            y = head(x, h)
+            y.backward(dy)
+        res.append((y.detach(), x.grad, None if h is None else h.grad,
+                    [p.grad.clone() for p in head.parameters()]))
+    (y0, dx0, dh0, g0), (y1, dx1, dh1, g1) = res
+    assert y1.shape == y0.shape
+    assert _rel(y1, y0) < 1e-5
+    assert _rel(dx1, dx0) < 1e-5
+    if with_h:
+        assert torch.equal(dh1, dx1) and _rel(dh1, dh0) < 1e-5
+    for a, b in zip(g1, g0):
+        assert _rel(a, b) < 1e-5

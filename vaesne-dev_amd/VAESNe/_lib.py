@@ -36,6 +36,9 @@ SIGNATURES = {
     "vaesne_linear_bwd_weight": (I32, [P, I64, P, I64, I32, P, I64, P, I64, I64, I32, I32, P, P,
                                        I32, P, P, P]),
     "vaesne_colsum_flush": (I32, [P, P]),
+    "vaesne_mlp_head_fwd": (I32, [P, I64, P, I64, I64, I32, P, P, P, P, P, P]),
+    "vaesne_mlp_head_bwd_workspace": (I64, [I64, I32]),
+    "vaesne_mlp_head_bwd": (I32, [P, I64, P, I64, P, I64, I32, P, P, P, P, P, P, P, P, P, P]),
     "vaesne_add_ln_fwd": (I32, [P, I64, P, I64, I64, I32, P, P, F32, P, U32, P, I64, P, P, P]),
     "vaesne_add_ln_bwd_workspace": (I64, [I64, I32]),
     "vaesne_add_ln_bwd": (I32, [P, I64, P, I64, P, I64, I64, I32, P, P, P, F32, P, U32, P, I64,

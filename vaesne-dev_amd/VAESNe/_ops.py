@@ -113,6 +113,71 @@ def linear(x, weight, bias=None, act=None, x2=None, base=None):
     return LinearFn.apply(x, weight, bias, ACT[act], x2, base)
 
 
+class MlpHeadFn(torch.autograd.Function):
+    """singlelayerMLP(E -> 1) on x (+ x2): fc2(relu(fc1(x + x2))) in one kernel
+    (vaesne_mlp_head_fwd); backward: d(x + x2) and the fc1 pre-activation gradient in
+    one pass (vaesne_mlp_head_bwd, fc2 gradients as partials), then the fc1 weight
+    gradient (vaesne_linear_bwd_weight)."""
+
+    @staticmethod
+    def forward(ctx, x, x2, W1, b1, W2, b2):
+        _lib.require_device(x, x2, W1, b1, W2, b2)
+        _f32(x)
+        _defer.count_uses(W1, b1, W2, b2)
+        ctx.params = (W1, b1, W2, b2)
+        lead = x.shape[:-1]
+        E = x.shape[-1]
+        xr, M, ldx = _rows(x)
+        x2r, ldx2 = None, 0
+        if x2 is not None:
+            if x2.shape != x.shape:
+                raise RuntimeError("MlpHeadFn: x2 must match x")
+            x2r, _, ldx2 = _rows(x2)
+        W1, b1, W2, b2 = (t.contiguous() for t in (W1, b1, W2, b2))
+        y = torch.empty(M, dtype=torch.float32, device=x.device)
+        lib.mlp_head_fwd(xr.data_ptr(), ldx, ptr(x2r), ldx2, M, E, W1.data_ptr(), b1.data_ptr(),
+                         W2.data_ptr(), b2.data_ptr(), y.data_ptr(), stream())
+        ctx.M, ctx.E, ctx.ldx, ctx.ldx2, ctx.xshape = M, E, ldx, ldx2, x.shape
+        ctx.save_for_backward(xr, x2r, W1, b1, W2)
+        return y.view(*lead, 1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xr, x2r, W1, b1, W2 = ctx.saved_tensors
+        M, E = ctx.M, ctx.E
+        dev = dy.device
+        dy = dy.contiguous()
+        ds = torch.empty((M, E), dtype=torch.float32, device=dev)
+        g = torch.empty((M, E), dtype=torch.float32, device=dev)
+        dW1 = torch.empty((E, E), dtype=torch.float32, device=dev)
+        db1 = torch.empty((E,), dtype=torch.float32, device=dev)
+        dW2 = torch.empty((1, E), dtype=torch.float32, device=dev)
+        db2 = torch.empty((1,), dtype=torch.float32, device=dev)
+        ws = _ws(lib.mlp_head_bwd_workspace(M, E), dev)
+        ws1 = _ws(lib.linear_bwd_weight_workspace(M, E, E), dev)
+        dfr = _defer.target(ctx.params, (dW1, db1, dW2, db2), (ws, ws1))
+        s = stream()
+        lib.mlp_head_bwd(xr.data_ptr(), ctx.ldx, ptr(x2r), ctx.ldx2, dy.data_ptr(), M, E,
+                         W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), ds.data_ptr(), g.data_ptr(),
+                         dW2.data_ptr(), db2.data_ptr(), ws.data_ptr(), dfr, s)
+        lib.linear_bwd_weight(g.data_ptr(), E, None, E, 0, xr.data_ptr(), ctx.ldx, ptr(x2r),
+                              ctx.ldx2, M, E, E, dW1.data_ptr(), db1.data_ptr(), 0, ws1.data_ptr(),
+                              dfr, s)
+        ds = ds.view(ctx.xshape)
+        return (ds if ctx.needs_input_grad[0] else None,
+                ds if ctx.needs_input_grad[1] else None, dW1, db1, dW2, db2)
+
+
+def mlp_head_ok(x, fc1, fc2):
+    return (x.shape[-1] == 32 and fc1.weight.shape == (32, 32) and fc2.weight.shape == (1, 32)
+            and fc1.bias is not None and fc2.bias is not None and x.is_cuda
+            and os.environ.get("VAESNE_FUSED_HEAD", "1") != "0")
+
+
+def mlp_head(x, x2, fc1, fc2):
+    return MlpHeadFn.apply(x, x2, fc1.weight, fc1.bias, fc2.weight, fc2.bias)
+
+
 class InProjPairFn(torch.autograd.Function):
     """Cross-attention in-projection: q = query W[:E]^T + b[:E] and
     kv = key W[E:]^T + b[E:] (functional.py's in_proj split, as

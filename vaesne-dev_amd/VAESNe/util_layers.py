@@ -43,6 +43,8 @@ class singlelayerMLP(nn.Module):
         self.fc2 = Linear(in_dim, out_dim)
 
     def forward(self, x, x2=None):
+        if _ops.mlp_head_ok(x, self.fc1, self.fc2):     # E -> 1 heads: one fused kernel
+            return _ops.mlp_head(x, x2, self.fc1, self.fc2)
         return self.fc2(self.fc1(x, act="relu", x2=x2))
 
 
