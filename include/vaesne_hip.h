@@ -196,6 +196,14 @@ int vaesne_attn_rep_fwd(const float* qkv, int64_t qkv_bs, int64_t qkv_ls, const 
                         int64_t kb_bs, float* o, int64_t o_bs, int64_t o_ls, float* lse, int Bd,
                         int R, int H, int L, int dh, float p_drop, const int64_t* rng_state,
                         uint32_t call_id, uint32_t* keep_bits, void* stream);
+/* The forward's query rows in parts: query blocks [p0, p1) of nparts (each part writes
+ * its rows of o and lse and their keep bits; parts 0..nparts-1 together = the whole
+ * forward), so a caller can run a part early beside other work and the rest later. */
+int vaesne_attn_rep_fwd_part(const float* qkv, int64_t qkv_bs, int64_t qkv_ls, const float* kbias,
+                             int64_t kb_bs, float* o, int64_t o_bs, int64_t o_ls, float* lse,
+                             int Bd, int R, int H, int L, int dh, float p_drop,
+                             const int64_t* rng_state, uint32_t call_id, uint32_t* keep_bits,
+                             int p0, int p1, int nparts, void* stream);
 int vaesne_attn_rep_bwd(const float* qkv, int64_t qkv_bs, int64_t qkv_ls, const float* kbias,
                         int64_t kb_bs, const float* o, int64_t o_bs, int64_t o_ls, const float* lse,
                         const float* dout, float* dqkv, int Bd, int R, int H, int L, int dh,

@@ -158,3 +158,29 @@ def test_rep_decoder_stack_and_model_step_equal_expanded_path(monkeypatch):
     for n in g0:
         assert torch.equal(g1[n], g2[n]), n
         assert _rel(g1[n], g0[n]) < 2e-3, (n, _rel(g1[n], g0[n]))
+
+
+@pytest.mark.parametrize("parts", [(1, 2), (2, 3), (1, 3), (3, 4)])
+@pytest.mark.parametrize("Bd,R,L,p", [(2, 16, 982, 0.1), (3, 6, 60, 0.1), (2, 4, 300, 0.0)])
+def test_rep_forward_in_parts_equals_one_launch(parts, Bd, R, L, p):
+    """vaesne_attn_rep_fwd_part: query parts [0, k) and [k, n) launched separately (the
+    first beside the encoders, the rest later) give the one-launch o, lse and bitmap."""
+    from VAESNe import _lib, rng
+    lib = _lib.lib
+    k, n = parts
+    qkv, kb, _, _ = _inputs(Bd, R, L, 0.05, 3 * L + R)
+    st = rng.state(DEV)
+    o0, l0, b0 = _rep_fwd(lib, qkv, kb, Bd, R, L, p, st, 77)
+    N = R * Bd
+    o1 = torch.full((N, L, E), float("nan"), device=DEV)
+    l1 = torch.empty(Bd, H, L, device=DEV)
+    b1 = torch.full((lib.attn_keep_bits_size(N, H, L, L) // 4,), -1, dtype=torch.int32, device=DEV)
+    for p0, p1 in ((0, k), (k, n)):
+        assert lib.attn_rep_fwd_part(qkv.data_ptr(), L * 3 * E, 3 * E, kb.data_ptr(), L,
+                                     o1.data_ptr(), L * E, E, l1.data_ptr(), Bd, R, H, L, 8, p,
+                                     st.data_ptr(), 77, b1.data_ptr(), p0, p1, n,
+                                     _lib.stream()) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(o0, o1) and torch.equal(l0, l1)
+    if p > 0:
+        assert torch.equal(b0, b1)

@@ -64,6 +64,8 @@ SIGNATURES = {
     "vaesne_attn_rep_workspace": (I64, [I32, I32, I32, I32, I32, F32]),
     "vaesne_attn_rep_fwd": (I32, [P, I64, I64, P, I64, P, I64, I64, P, I32, I32, I32, I32, I32, F32,
                                   P, U32, P, P]),
+    "vaesne_attn_rep_fwd_part": (I32, [P, I64, I64, P, I64, P, I64, I64, P, I32, I32, I32, I32, I32,
+                                       F32, P, U32, P, I32, I32, I32, P]),
     "vaesne_attn_rep_bwd": (I32, [P, I64, I64, P, I64, P, I64, I64, P, P, P, I32, I32, I32, I32, I32,
                                   F32, P, U32, P, P, P]),
     "vaesne_attn_rep_config": (I32, [I32, I32, I32, I32, I32, I32, I32]),

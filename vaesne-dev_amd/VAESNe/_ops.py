@@ -640,25 +640,18 @@ class SelfAttnRepFn(torch.autograd.Function):
     backward returns the copies' summed d(qkv)."""
 
     @staticmethod
-    def forward(ctx, qkv, kbias, H, p, R):
+    def forward(ctx, qkv, kbias, H, p, R, early=None):
         _lib.require_device(qkv)
         qkv = qkv.contiguous()
         Bd, L, E3 = qkv.shape
         E = E3 // 3
         dh = E // H
-        N = R * Bd
-        dev = qkv.device
-        o = torch.empty((N, L, E), dtype=torch.float32, device=dev)
-        lse = torch.empty((Bd, H, L), dtype=torch.float32, device=dev)
-        st = rng.state(dev) if p > 0 else None
-        cid = rng.next_call_id() if p > 0 else 0
-        bits = None
-        if p > 0:
-            n = lib.attn_keep_bits_size(N, H, L, L)
-            bits = torch.empty((n + 3) // 4, dtype=torch.int32, device=dev)
-        lib.attn_rep_fwd(qkv.data_ptr(), L * E3, E3, ptr(kbias), L, o.data_ptr(), L * E, E,
-                         lse.data_ptr(), Bd, R, H, L, dh, float(p), ptr(st), cid, ptr(bits),
-                         stream())
+        if early is None:
+            early = RepAttnStart(qkv, kbias, H, p, R)
+        elif early.qkv is not qkv:
+            raise RuntimeError("SelfAttnRepFn: `early` was started for another input")
+        early.launch(early.done, early.nparts)      # the rows not yet computed
+        o, lse, bits, st, cid = early.o, early.lse, early.bits, early.st, early.cid
         ctx.dims = (Bd, R, L, E, H, dh, float(p), cid)
         ctx.save_for_backward(qkv, kbias, o, lse, bits, st)
         return o
@@ -674,7 +667,46 @@ class SelfAttnRepFn(torch.autograd.Function):
         lib.attn_rep_bwd(qkv.data_ptr(), L * E3, E3, ptr(kbias), L, o.data_ptr(), L * E, E,
                          lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(), Bd, R, H, L, dh, p,
                          ptr(st), cid, ptr(bits), ptr(ws), stream())
-        return dqkv, None, None, None, None
+        return dqkv, None, None, None, None, None
+
+
+class RepAttnStart:
+    """The outputs of one SelfAttnRepFn forward, with query-row parts launched ahead
+    (vaesne_attn_rep_fwd_part): launch(0, k) beside other work, the rest when
+    SelfAttnRepFn runs (it draws no second call id: one call id for all parts)."""
+
+    def __init__(self, qkv, kbias, H, p, R, nparts=1):
+        qkv = qkv.contiguous()
+        self.qkv, self.kbias, self.H, self.p, self.R = qkv, kbias, H, float(p), int(R)
+        Bd, L, E3 = qkv.shape
+        E = E3 // 3
+        N = R * Bd
+        dev = qkv.device
+        self.o = torch.empty((N, L, E), dtype=torch.float32, device=dev)
+        self.lse = torch.empty((Bd, H, L), dtype=torch.float32, device=dev)
+        self.st = rng.state(dev) if p > 0 else None
+        self.cid = rng.next_call_id() if p > 0 else 0
+        self.bits = None
+        if p > 0:
+            n = lib.attn_keep_bits_size(N, H, L, L)
+            self.bits = torch.empty((n + 3) // 4, dtype=torch.int32, device=dev)
+        self.nparts, self.done = int(nparts), 0
+
+    def launch(self, p0, p1):
+        if p1 <= p0:
+            return
+        qkv = self.qkv
+        Bd, L, E3 = qkv.shape
+        E = E3 // 3
+        lib.attn_rep_fwd_part(qkv.data_ptr(), L * E3, E3, ptr(self.kbias), L, self.o.data_ptr(),
+                              L * E, E, self.lse.data_ptr(), Bd, self.R, self.H, L, E // self.H,
+                              self.p, ptr(self.st), self.cid, ptr(self.bits), p0, p1,
+                              self.nparts, stream())
+        self.done = max(self.done, p1)
+
+    def tensors(self):
+        return [t for t in (self.qkv, self.kbias, self.o, self.lse, self.bits, self.st)
+                if t is not None]
 
 
 def rep_attention_ok(qkv, num_heads, R):
@@ -683,9 +715,10 @@ def rep_attention_ok(qkv, num_heads, R):
             and R >= 1 and os.environ.get("VAESNE_REP_ATTN", "1") != "0")
 
 
-def self_attention_rep(qkv, kbias, num_heads, p, R):
-    """kbias: the key bias of the Bd distinct sequences (key_bias of their mask) or None."""
-    return SelfAttnRepFn.apply(qkv, kbias, num_heads, float(p), int(R))
+def self_attention_rep(qkv, kbias, num_heads, p, R, early=None):
+    """kbias: the key bias of the Bd distinct sequences (key_bias of their mask) or None;
+    early: a RepAttnStart for these arguments with some rows already launched."""
+    return SelfAttnRepFn.apply(qkv, kbias, num_heads, float(p), int(R), early)
 
 
 def self_attention(qkv, mask, num_heads, p, kbias=None, keep=None):

@@ -276,14 +276,27 @@ class DecoderFirst:
     SpectraLayers.py:54-62, PhotometricLayers.py:59-67), not the latents, so they
     can run while the encoders still work (photospecMMVAE.forward issues them on
     their own stream)."""
-    __slots__ = ("N", "L", "kbias", "qkv", "rep", "O1", "keep")
+    __slots__ = ("N", "L", "kbias", "qkv", "rep", "O1", "keep", "early")
 
     def __init__(self, N, L, kbias, qkv, rep, O1, keep):
         self.N, self.L, self.kbias, self.qkv, self.rep = N, L, kbias, qkv, rep
-        self.O1, self.keep = O1, keep
+        self.O1, self.keep, self.early = O1, keep, None
 
     def tensors(self):
-        return [t for t in (self.kbias, self.qkv, self.O1) if t is not None]
+        ts = [t for t in (self.kbias, self.qkv, self.O1) if t is not None]
+        return ts + (self.early.tensors() if self.early is not None else [])
+
+    def start(self, blocks, k, n):
+        """Launch query parts [0, k) of n of block 1's repeated-sequence self-attention
+        now; attend() launches the rest (one call id for all parts)."""
+        if self.O1 is not None or self.rep <= 1 or self.early is not None:
+            return
+        b0 = blocks[0].self_attn
+        p_attn = b0.dropout if blocks[0].training else 0.0
+        Bd = self.N // self.rep
+        self.early = _ops.RepAttnStart(self.qkv, None if self.kbias is None else self.kbias[:Bd],
+                                       b0.num_heads, p_attn, self.rep, nparts=n)
+        self.early.launch(0, k)
 
     def attend(self, blocks):
         """Block 1's masked self-attention (once)."""
@@ -294,7 +307,8 @@ class DecoderFirst:
                 Bd = self.N // self.rep
                 self.O1 = _ops.self_attention_rep(self.qkv, None if self.kbias is None
                                                   else self.kbias[:Bd], b0.num_heads, p_attn,
-                                                  self.rep)
+                                                  self.rep, self.early)
+                self.early = None
             else:
                 self.O1 = _ops.self_attention(self.qkv, None, b0.num_heads, p_attn,
                                               kbias=self.kbias,
@@ -323,7 +337,13 @@ def decoder_stack_first(blocks, x, mask=None, keep=None, x_qkv=None, rep=1, atte
         qkv = _ops.repeat_batch(qkv, rep).reshape(N, L, 3 * E)
     first = DecoderFirst(N, L, kbias, qkv, rep if rep_attn else 1, None, keep)
     if attend:
-        first.attend(blocks)
+        # VAESNE_REP_EARLY="k/n": only query parts [0, k) of n now, the rest in
+        # decoder_stack (A/B tuning of how much of it overlaps the encoders)
+        k, n = (int(v) for v in os.environ.get("VAESNE_REP_EARLY", "1/1").split("/"))
+        if rep_attn and 0 < k < n:
+            first.start(blocks, k, n)
+        else:
+            first.attend(blocks)
     return first
 
 

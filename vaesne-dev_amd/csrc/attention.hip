@@ -757,17 +757,18 @@ __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
 // the expanded input reproduce these bit for bit (tested).
 // Args: q/k/v/kbias/lse over the Bd distinct sequences (a.B = Bd), o / dout / bits
 // over the N sequences (o_bs, do_bs = per-sequence strides).
+// grid.x covers query blocks [qb0, qb0 + nqbs) of every (sequence, head): a launch may do
+// a part of the rows (vaesne_attn_rep_fwd_part)
 template <int DH, int NTT, int NP, int RC, bool DROP>
-__global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R) {
+__global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R, int qb0, int nqbs) {
   __shared__ __attribute__((aligned(16))) float Ks[TK * DH];
   __shared__ __attribute__((aligned(16))) float Vs[TK * DH];
   __shared__ float Kb[TK];
   constexpr int R2 = 2 * NP;              // queries per lane (pairs p = {2p, 2p + 1})
   constexpr int QB = R2 * NTT;
   constexpr int NC = DROP ? RC : 1;       // accumulator sets (no dropout: one for all copies)
-  const int nqb = (a.Lq + QB - 1) / QB;
-  const int qb = blockIdx.x % nqb;
-  const int bh = blockIdx.x / nqb;        // distinct sequence x head
+  const int qb = qb0 + blockIdx.x % nqbs;
+  const int bh = blockIdx.x / nqbs;       // distinct sequence x head
   const int b = bh / a.H, h = bh - b * a.H;
   const int c0 = blockIdx.y * RC;
   int qi[R2], qc[R2];
@@ -1809,21 +1810,25 @@ RepPlan rep_bwd_plan(int Bd, int R, int H, int L, float p_drop) {
   return pl;
 }
 
-int launch_rep_fwd(const AttnArgs& a, int R, float p_drop, hipStream_t s) {
+// query blocks [p0 * nqb / np_, p1 * nqb / np_) of the launch geometry
+int launch_rep_fwd(const AttnArgs& a, int R, float p_drop, int p0, int p1, int np_, hipStream_t s) {
   const bool drop = p_drop > 0.f;
   const int rc = drop ? g_rep.frc : 1;
   const int cb = drop ? (R + rc - 1) / rc : 1;
   const int np = drop ? g_rep.fnp : 1;
   const int nt = rep_fwd_nt((int64_t)a.B * a.H, a.Lq, cb, np);
   const int nqb = (a.Lq + 2 * np * nt - 1) / (2 * np * nt);
-  const dim3 grid((unsigned)((int64_t)a.B * a.H * nqb), (unsigned)cb);
+  const int qb0 = (int)((int64_t)p0 * nqb / np_), qb1 = (int)((int64_t)p1 * nqb / np_);
+  const int nqbs = qb1 - qb0;
+  if (nqbs <= 0) return 0;
+  const dim3 grid((unsigned)((int64_t)a.B * a.H * nqbs), (unsigned)cb);
 #define VAESNE_REP_FWD(NT)                                                                        \
-  if (!drop) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, 1, false>), grid, dim3(NT), 0, s, a, R); \
-  else if (np == 2 && rc == 2) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 2, 2, true>), grid, dim3(NT), 0, s, a, R); \
-  else if (np == 2) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 2, 4, true>), grid, dim3(NT), 0, s, a, R); \
-  else if (rc == 2) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, 2, true>), grid, dim3(NT), 0, s, a, R); \
-  else if (rc == 4) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, 4, true>), grid, dim3(NT), 0, s, a, R); \
-  else hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, 8, true>), grid, dim3(NT), 0, s, a, R);
+  if (!drop) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, 1, false>), grid, dim3(NT), 0, s, a, R, qb0, nqbs); \
+  else if (np == 2 && rc == 2) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 2, 2, true>), grid, dim3(NT), 0, s, a, R, qb0, nqbs); \
+  else if (np == 2) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 2, 4, true>), grid, dim3(NT), 0, s, a, R, qb0, nqbs); \
+  else if (rc == 2) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, 2, true>), grid, dim3(NT), 0, s, a, R, qb0, nqbs); \
+  else if (rc == 4) hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, 4, true>), grid, dim3(NT), 0, s, a, R, qb0, nqbs); \
+  else hipLaunchKernelGGL((attn_rep_fwd_kernel<8, NT, 1, 8, true>), grid, dim3(NT), 0, s, a, R, qb0, nqbs);
   if (nt == 256) { VAESNE_REP_FWD(256) } else if (nt == 128) { VAESNE_REP_FWD(128) } else { VAESNE_REP_FWD(64) }
 #undef VAESNE_REP_FWD
   VAESNE_CHECK_LAUNCH();
@@ -1924,12 +1929,14 @@ bool rep_args(AttnArgs& a, const float* qkv, int64_t qkv_bs, int64_t qkv_ls, con
 }
 }  // namespace
 
-VAESNE_API int vaesne_attn_rep_fwd(const float* qkv, int64_t qkv_bs, int64_t qkv_ls,
-                                   const float* kbias, int64_t kb_bs, float* o, int64_t o_bs,
-                                   int64_t o_ls, float* lse, int Bd, int R, int H, int L, int dh,
-                                   float p_drop, const int64_t* rng_state, uint32_t call_id,
-                                   uint32_t* keep_bits, void* stream) {
+VAESNE_API int vaesne_attn_rep_fwd_part(const float* qkv, int64_t qkv_bs, int64_t qkv_ls,
+                                        const float* kbias, int64_t kb_bs, float* o, int64_t o_bs,
+                                        int64_t o_ls, float* lse, int Bd, int R, int H, int L,
+                                        int dh, float p_drop, const int64_t* rng_state,
+                                        uint32_t call_id, uint32_t* keep_bits, int p0, int p1,
+                                        int nparts, void* stream) {
   if (Bd <= 0 || R <= 0 || L <= 0) return 0;
+  if (nparts < 1 || p0 < 0 || p1 > nparts || p0 > p1) return (int)hipErrorInvalidValue;
   if (dh != 8 || L <= 2 * SQ || !rep_cfg_ok(g_rep)) return (int)hipErrorInvalidValue;
   if (p_drop > 0.f && (!keep_bits || !rng_state)) return (int)hipErrorInvalidValue;
   AttnArgs a{};
@@ -1939,7 +1946,16 @@ VAESNE_API int vaesne_attn_rep_fwd(const float* qkv, int64_t qkv_bs, int64_t qkv
   a.o = o; a.o_out = o; a.o_bs = o_bs; a.o_ls = o_ls;
   a.lse = lse;
   a.bits = keep_bits;
-  return launch_rep_fwd(a, R, p_drop, (hipStream_t)stream);
+  return launch_rep_fwd(a, R, p_drop, p0, p1, nparts, (hipStream_t)stream);
+}
+
+VAESNE_API int vaesne_attn_rep_fwd(const float* qkv, int64_t qkv_bs, int64_t qkv_ls,
+                                   const float* kbias, int64_t kb_bs, float* o, int64_t o_bs,
+                                   int64_t o_ls, float* lse, int Bd, int R, int H, int L, int dh,
+                                   float p_drop, const int64_t* rng_state, uint32_t call_id,
+                                   uint32_t* keep_bits, void* stream) {
+  return vaesne_attn_rep_fwd_part(qkv, qkv_bs, qkv_ls, kbias, kb_bs, o, o_bs, o_ls, lse, Bd, R, H,
+                                  L, dh, p_drop, rng_state, call_id, keep_bits, 0, 1, 1, stream);
 }
 
 VAESNE_API int vaesne_attn_rep_bwd(const float* qkv, int64_t qkv_bs, int64_t qkv_ls,
