@@ -296,6 +296,34 @@ def roofline(device, B):
                                     note="draws the forward's keep bitmap ahead (off by default)")
         res["fwd_bits_in"] = dict(kernel="attn_fwd_kernel<..., BITSIN> (reads the drawn bitmap)",
                                   ms=time_kernel(fwd_with(1), 20, device) * 1e3)
+    # the decoders' first block: the same step shape as R = 2K copies of Bd = B distinct
+    # sequences (attn_rep_*; scores, exponentials and dK/dQ products shared by the copies).
+    # "equiv_tflops" counts the FLOPs of the R*Bd expanded sequences (the reference's work)
+    R, Bd = 2 * CFG["K"], B
+    qd = torch.randn(Bd, L, 3 * E, device=device)
+    kbd = kbias[:Bd].contiguous()
+    ord_ = torch.empty(N, L, E, device=device)
+    lsed = torch.empty(Bd, H, L, device=device)
+    dqd = torch.empty_like(qd)
+    wsr = torch.empty(max(1, lib.attn_rep_workspace(Bd, R, H, L, dh, pd) // 4), device=device)
+    qp, sp = qd.data_ptr(), L * 3 * E
+
+    def rep_fwd():
+        lib.attn_rep_fwd(qp, sp, 3 * E, kbd.data_ptr(), L, ord_.data_ptr(), L * E, E,
+                         lsed.data_ptr(), Bd, R, H, L, dh, pd, st.data_ptr(), 9, bits.data_ptr(),
+                         _lib.stream())
+
+    def rep_bwd():
+        lib.attn_rep_bwd(qp, sp, 3 * E, kbd.data_ptr(), L, ord_.data_ptr(), L * E, E,
+                         lsed.data_ptr(), do.data_ptr(), dqd.data_ptr(), Bd, R, H, L, dh, pd,
+                         st.data_ptr(), 9, bits.data_ptr(), wsr.data_ptr(), _lib.stream())
+
+    rep_fwd()
+    for name, kern, fn, fl in [("rep_fwd", "attn_rep_fwd_kernel", rep_fwd, 4 * dh),
+                               ("rep_bwd", "attn_rep_bwd_kernel", rep_bwd, 8 * dh)]:
+        t = time_kernel(fn, 20, device)
+        res[name] = dict(kernel=kern, ms=t * 1e3, equiv_tflops=scores * fl / t / 1e12,
+                         note=f"{R} copies x {Bd} sequences (decoder block 1)")
     r = res["bwd"]
     a = r["tflops"]
     traffic, tsrc = None, None
