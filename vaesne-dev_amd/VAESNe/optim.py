@@ -64,7 +64,7 @@ class FusedAdamW(torch.optim.Optimizer):
         return self._flat[group]["grad"]
 
     def pack_grads(self):
-        """Gather every p.grad into the flat gradient buffer (one launch per 48 tensors)."""
+        """Gather every p.grad into the flat gradient buffer (one launch per 144 tensors)."""
         for fl in self._flat:
             if fl is None:
                 continue

@@ -304,7 +304,7 @@ __global__ void sum_n_kernel(SumArgs a, int64_t numel, float* __restrict__ out) 
   }
 }
 
-constexpr int PACK_MAX = 48;
+constexpr int PACK_MAX = 144;     // 144 x 24 B of kernel arguments (< 4 KB): one launch per 144 tensors
 struct PackArgs {
   const float* src[PACK_MAX];
   int64_t off[PACK_MAX];
