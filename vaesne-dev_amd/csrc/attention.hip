@@ -1465,6 +1465,14 @@ Geo g_forced = [] {
   if (const char* e = getenv("VAESNE_ATTN_GEO")) sscanf(e, "%d,%d", &f.nt, &f.np);
   return f;
 }();
+// geometry of the split launches (grids that leave a split in place: the encoder's
+// context self-attention): 256 x 2 (staging shared by 4 waves; A/B 9.52 -> 9.49 ms per
+// step); VAESNE_ATTN_SPLIT_GEO="nt,np" at load, "0,0" = the row-slot rule
+Geo g_split = [] {
+  Geo f{256, 2};
+  if (const char* e = getenv("VAESNE_ATTN_SPLIT_GEO")) sscanf(e, "%d,%d", &f.nt, &f.np);
+  return f;
+}();
 Geo pick_geo(int64_t bh, int L) {
   if (g_forced.nt > 0) return g_forced;
   // among geometries with >= 1024 workgroups, the one wasting the fewest row
@@ -1480,6 +1488,11 @@ Geo pick_geo(int64_t bh, int L) {
       const double eff = (double)L / (double)(rows * nb);
       if (bh * nb >= 1024 && eff > best_eff + 1e-9) { best = {nt, np}; best_eff = eff; }
     }
+  if (g_split.nt > 0 && L >= 256) {   // this pick would be split (< 2048 waves): g_split
+    const int64_t waves = bh * ((L + 2 * best.np * best.nt - 1) / (2 * best.np * best.nt)) *
+                          (best.nt / 64);
+    if (waves < 2048) return g_split;
+  }
   return best;
 }
 
@@ -1499,10 +1512,15 @@ bool fused_dq_enabled() {
 // grid row; partial results go to the workspace and a fixed-order combine
 // kernel finishes them (bitwise reproducible).
 struct Split { int n, chunk; };
+// target waves of a split launch: VAESNE_ATTN_SPLIT_WAVES at load (tuning)
+const int64_t g_split_waves = [] {
+  const char* e = getenv("VAESNE_ATTN_SPLIT_WAVES");
+  return e ? std::max<int64_t>(1024, atoll(e)) : (int64_t)4096;
+}();
 Split pick_split(int64_t waves, int L) {
   Split sp{1, L};
   if (waves >= 2048 || L < 256) return sp;
-  int n = (int)std::min<int64_t>(16, (4096 + waves - 1) / waves);
+  int n = (int)std::min<int64_t>(16, (g_split_waves + waves - 1) / waves);
   n = std::min(n, L / 128);
   if (n <= 1) return sp;
   sp.chunk = ((L + n - 1) / n + 63) / 64 * 64;
