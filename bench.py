@@ -219,6 +219,14 @@ def _rocprof_avg_ms(kernel_prefix):
     import re
     try:
         d = open(os.path.join(ROOT, "profiles", "LATEST")).read().strip()
+        # the decoder-shape launches picked from the trace by grid (roofline_launches.py):
+        # the stats average also holds the encoder's context launches of the same
+        # instantiation
+        lj = os.path.join(ROOT, "profiles", d, "roofline_launches.json")
+        if os.path.exists(lj):
+            k = json.load(open(lj))["kernels"].get(kernel_prefix)
+            if k:
+                return k["avg_ms"], f"profiles/{d}/roofline_launches.json"
         path = os.path.join(ROOT, "profiles", d, "kernel_stats.csv")
         pat = re.compile(r"(^|::|\s)" + re.escape(kernel_prefix) + r"<")
         rows = [r for r in csv.DictReader(open(path)) if pat.search(r["Name"])]

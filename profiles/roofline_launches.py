@@ -1,0 +1,33 @@
+"""Per-launch averages of the roofline kernels at the spectra decoder's launch shape,
+from a rocprofv3 kernel trace of bench.py.  The --stats summary averages every launch
+of an instantiation, and the spectra encoder's context self-attention (a split launch,
+grid y > 1) uses the decoder's instantiation too, so the decoder launches are picked
+by grid: N*H query/key blocks of 256 threads in x, one chunk in y.
+    python profiles/roofline_launches.py <run_kernel_trace.csv> <out.json>"""
+import csv
+import json
+import sys
+
+N, H = 256, 4          # 2*K*B sequences x heads at cfg 5
+KERNELS = {
+    "attn_bwd_kv_kernel": "attn_bwd_kv_kernel<8, 256, 2, true, true>",
+    "attn_fwd_kernel": "attn_fwd_kernel<8, 256, 2, true, false>",
+}
+
+
+def main(path, out):
+    res = {}
+    rows = list(csv.DictReader(open(path)))
+    for key, inst in KERNELS.items():
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in rows
+                if inst in r["Kernel_Name"] and int(r["Grid_Size_X"]) == N * H * 256
+                and int(r.get("Grid_Size_Y", 1) or 1) == 1]
+        if durs:
+            res[key] = {"instance": inst, "grid": f"{N * H * 256}x1", "launches": len(durs),
+                        "avg_ms": round(sum(durs) / len(durs), 4)}
+    json.dump({"source": path, "kernels": res}, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
