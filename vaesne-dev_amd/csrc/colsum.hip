@@ -1,6 +1,8 @@
 // Deterministic partial-sum reduction shared by every weight / LayerNorm /
 // embedding gradient (see common.h), immediate or deferred to one batched
 // launch per backward pass (vaesne_colsum_flush).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace vaesne {
@@ -68,18 +70,59 @@ struct ColsumBatch {
   int G[CS_MAX];
   int F[CS_MAX];
   int accum[CS_MAX];
+  int vec[CS_MAX];          // 4 columns per thread (16-byte aligned rows)
   int start[CS_MAX + 1];
   int count;
 };
 
 __global__ void __launch_bounds__(1024) colsum_batch_kernel(ColsumBatch b) {
-  __shared__ float red[16][65];
+  __shared__ float4 red4[16][64];
   int i = 0;
   while (i + 1 < b.count && (int)blockIdx.x >= b.start[i + 1]) ++i;
   const float* P = b.P[i];
   const int64_t ld = b.ld[i];
   const int G = b.G[i], F = b.F[i];
   const int fl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  if (b.vec[i]) {
+    // 4 adjacent columns per thread (one 16-byte load per row: a wave reads 1 KB of a
+    // row per request); every column keeps colsum_kernel's summation order
+    const int f = ((int)blockIdx.x - b.start[i]) * 256 + fl * 4;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (f < F) {
+      int64_t g = sl;
+      for (; g + 48 < G; g += 64) {
+        const float4 a = *reinterpret_cast<const float4*>(P + g * ld + f);
+        const float4 c = *reinterpret_cast<const float4*>(P + (g + 16) * ld + f);
+        const float4 d = *reinterpret_cast<const float4*>(P + (g + 32) * ld + f);
+        const float4 e = *reinterpret_cast<const float4*>(P + (g + 48) * ld + f);
+        s.x += a.x; s.x += c.x; s.x += d.x; s.x += e.x;
+        s.y += a.y; s.y += c.y; s.y += d.y; s.y += e.y;
+        s.z += a.z; s.z += c.z; s.z += d.z; s.z += e.z;
+        s.w += a.w; s.w += c.w; s.w += d.w; s.w += e.w;
+      }
+      for (; g < G; g += 16) {
+        const float4 a = *reinterpret_cast<const float4*>(P + g * ld + f);
+        s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+      }
+    }
+    red4[sl][fl] = s;
+    __syncthreads();
+    if (sl == 0 && f < F) {
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float4 r = red4[k][fl];
+        t.x += r.x; t.y += r.y; t.z += r.z; t.w += r.w;
+      }
+      float* o = b.out[i] + f;
+      const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (f + c < F) o[c] = b.accum[i] ? o[c] + tv[c] : tv[c];
+    }
+    return;
+  }
+  float (*red)[65] = reinterpret_cast<float (*)[65]>(&red4[0][0]);
   const int f = ((int)blockIdx.x - b.start[i]) * 64 + fl;
   float s = 0.f;
   if (f < F) {
@@ -141,8 +184,17 @@ VAESNE_API int vaesne_colsum_flush(vaesne_colsum_list* list, void* stream) {
       if (e.cols > 0 && e.out) {
         b.P[b.count] = e.partial; b.out[b.count] = e.out; b.ld[b.count] = e.ld;
         b.G[b.count] = e.groups; b.F[b.count] = e.cols; b.accum[b.count] = e.accum;
+        // a padded last row read is never past the partials: cols % 4 == 0 (the float4
+        // at f < cols stays inside the row)
+        static const bool vec_on = [] {   // VAESNE_COLSUM_VEC=0: 1 column per thread (A/B)
+          const char* v = getenv("VAESNE_COLSUM_VEC");
+          return !(v && v[0] == '0');
+        }();
+        const int vec = vec_on && e.ld % 4 == 0 && e.cols % 4 == 0 &&
+                        (uintptr_t)e.partial % 16 == 0;
+        b.vec[b.count] = vec;
         b.start[b.count] = blocks;
-        blocks += (e.cols + 63) / 64;
+        blocks += vec ? (e.cols + 255) / 256 : (e.cols + 63) / 64;
         ++b.count;
       }
       ++i;
