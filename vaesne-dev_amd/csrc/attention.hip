@@ -1579,6 +1579,36 @@ __global__ void attn_sum_chunks_kernel(const float* __restrict__ ws, int64_t ss,
   out[(int64_t)b * bs + (int64_t)l * ls + e] = v;
 }
 
+// attn_sum_chunks_kernel with 4 adjacent features per thread (16-byte loads / stores)
+__global__ void attn_sum_chunks4_kernel(const float* __restrict__ ws, int64_t ss, int n, int B,
+                                        int L, int E, float* __restrict__ out, int64_t bs,
+                                        int64_t ls) {
+  const int64_t t = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (t >= (int64_t)B * L * E) return;
+  const int e = (int)(t % E);
+  const int64_t bl = t / E;
+  const int l = (int)(bl % L), b = (int)(bl / L);
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int c = 0; c < n; ++c) {
+    const float4 w = *reinterpret_cast<const float4*>(ws + c * ss + t);
+    v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+  }
+  *reinterpret_cast<float4*>(out + (int64_t)b * bs + (int64_t)l * ls + e) = v;
+}
+
+// out = sum of n dense [B, L, E] chunks (stride ss) -- same per-element order either way
+void launch_sum_chunks(const float* ws, int64_t ss, int n, int B, int L, int E, float* out,
+                       int64_t bs, int64_t ls, hipStream_t s) {
+  const int64_t total = (int64_t)B * L * E;
+  if (E % 4 == 0 && ss % 4 == 0 && bs % 4 == 0 && ls % 4 == 0 && (uintptr_t)ws % 16 == 0 &&
+      (uintptr_t)out % 16 == 0)
+    hipLaunchKernelGGL(attn_sum_chunks4_kernel, dim3((unsigned)((total / 4 + 255) / 256)),
+                       dim3(256), 0, s, ws, ss, n, B, L, E, out, bs, ls);
+  else
+    hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256),
+                       0, s, ws, ss, n, B, L, E, out, bs, ls);
+}
+
 // workspace of a split launch (bytes; 0 = no split for this shape)
 int64_t fwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sp) {
   sp = {1, Lk};
@@ -1727,19 +1757,13 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
     })
     VAESNE_CHECK_LAUNCH();
     if (sk.n > 1) {
-      const int64_t n = (int64_t)a.B * a.Lk * E;
-      const unsigned nb = (unsigned)((n + 255) / 256);
-      hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3(nb), dim3(256), 0, s, c.dk, c.dk_ss, sk.n,
-                         a.B, a.Lk, E, a.dk, a.dk_bs, a.dk_ls);
+      launch_sum_chunks(c.dk, c.dk_ss, sk.n, a.B, a.Lk, E, a.dk, a.dk_bs, a.dk_ls, s);
       VAESNE_CHECK_LAUNCH();
-      hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3(nb), dim3(256), 0, s, c.dv, c.dk_ss, sk.n,
-                         a.B, a.Lk, E, a.dv, a.dv_bs, a.dv_ls);
+      launch_sum_chunks(c.dv, c.dk_ss, sk.n, a.B, a.Lk, E, a.dv, a.dv_bs, a.dv_ls, s);
       VAESNE_CHECK_LAUNCH();
     }
     if (fuse && nkb > 1) {
-      const int64_t n = (int64_t)a.B * a.Lq * E;
-      hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                         c.dq, c.dq_ss, nkb, a.B, a.Lq, E, a.dq, a.dq_bs, a.dq_ls);
+      launch_sum_chunks(c.dq, c.dq_ss, nkb, a.B, a.Lq, E, a.dq, a.dq_bs, a.dq_ls, s);
       VAESNE_CHECK_LAUNCH();
     }
   }
@@ -1761,9 +1785,7 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
     })
     VAESNE_CHECK_LAUNCH();
     if (sq.n > 1) {
-      const int64_t n = (int64_t)a.B * a.Lq * E;
-      hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                         c.dq, c.dq_ss, sq.n, a.B, a.Lq, E, a.dq, a.dq_bs, a.dq_ls);
+      launch_sum_chunks(c.dq, c.dq_ss, sq.n, a.B, a.Lq, E, a.dq, a.dq_bs, a.dq_ls, s);
       VAESNE_CHECK_LAUNCH();
     }
   }
@@ -1860,10 +1882,7 @@ int launch_rep_bwd(const AttnArgs& a, int R, float p_drop, float* ws, hipStream_
     // every copy's O and P are the same: dS summed over copies = P (V.sum_r dO_r - sum_r D_r),
     // sum_r D_r = O . sum_r dO_r -- the plain backward of (qkv, O, sum_r dO_r)
     float* dsum = ws;
-    const int64_t n = (int64_t)a.B * a.Lq * E;
-    hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                       a.dout, (int64_t)a.B * a.do_bs, R, a.B, a.Lq, E, dsum, (int64_t)a.Lq * E,
-                       (int64_t)E);
+    launch_sum_chunks(a.dout, (int64_t)a.B * a.do_bs, R, a.B, a.Lq, E, dsum, (int64_t)a.Lq * E, (int64_t)E, s);
     VAESNE_CHECK_LAUNCH();
     AttnArgs c = a;
     c.dout = dsum; c.do_bs = (int64_t)a.Lq * E; c.do_ls = E;
@@ -1898,19 +1917,13 @@ int launch_rep_bwd(const AttnArgs& a, int R, float p_drop, float* ws, hipStream_
 #undef VAESNE_REP_BWD
   VAESNE_CHECK_LAUNCH();
   if (pl.dkv_floats > 0) {
-    const int64_t n = (int64_t)a.B * a.Lk * E;
-    const unsigned nb = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3(nb), dim3(256), 0, s, c.dk, c.dk_ss,
-                       pl.QS * pl.CB, a.B, a.Lk, E, a.dk, a.dk_bs, a.dk_ls);
+    launch_sum_chunks(c.dk, c.dk_ss, pl.QS * pl.CB, a.B, a.Lk, E, a.dk, a.dk_bs, a.dk_ls, s);
     VAESNE_CHECK_LAUNCH();
-    hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3(nb), dim3(256), 0, s, c.dv, c.dk_ss,
-                       pl.QS * pl.CB, a.B, a.Lk, E, a.dv, a.dv_bs, a.dv_ls);
+    launch_sum_chunks(c.dv, c.dk_ss, pl.QS * pl.CB, a.B, a.Lk, E, a.dv, a.dv_bs, a.dv_ls, s);
     VAESNE_CHECK_LAUNCH();
   }
   if (pl.dq_floats > 0) {
-    const int64_t n = (int64_t)a.B * a.Lq * E;
-    hipLaunchKernelGGL(attn_sum_chunks_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                       c.dq, c.dq_ss, pl.nkb * pl.CB, a.B, a.Lq, E, a.dq, a.dq_bs, a.dq_ls);
+    launch_sum_chunks(c.dq, c.dq_ss, pl.nkb * pl.CB, a.B, a.Lq, E, a.dq, a.dq_bs, a.dq_ls, s);
     VAESNE_CHECK_LAUNCH();
   }
   return 0;
