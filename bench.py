@@ -10,10 +10,22 @@ in HBM (weak scaling).  The step is captured once as a hipGraph and replayed.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-graph]
                     [--no-cpu-baseline]
 
+Multi-GPU: one process per GPU.  Under a launcher (torchrun sets WORLD_SIZE /
+RANK / LOCAL_RANK) each process is one rank; with `--gpus N > 1` and no launcher
+environment, this script starts the N rank processes itself (fresh children,
+before anything touches the GPU) and exits with their status.  Backend "nccl"
+(RCCL over xGMI); VAESNE_DP_BACKEND=gloo lets ranks share a GPU (rehearsing
+`--gpus 2` on a 1-GPU box).  The headline is weak scaling (B pairs per GPU);
+`strong_scaling` times the unchanged script's split of ONE global batch of 16
+(cannon/ZTF_photospect.py:76 DataLoader(batch_size=16), sliced per rank as
+training_util.training_step does).
+
 Rank 0 prints ONE JSON line (value = whole-job SN pairs/s).  Beside it:
   roofline     : the dominant kernel (spectra-decoder masked self-attention
-                 backward, dK/dV) timed with HIP events on its own stream,
-                 its algorithmic FLOPs / average launch time vs the FP32 peak;
+                 fused backward) timed with HIP events around its launches
+                 INSIDE the training step (eager replay of the same step, on
+                 the launch's own stream), its algorithmic FLOPs / average
+                 launch time vs the FP32 peak; isolated launches beside it;
   cpu_baseline : the CPU oracle (pure-PyTorch restatement of the reference,
                  oracle/vaesne_oracle.py) timed on the host cores on a bounded
                  sample (rank 0, N=1 only);
@@ -27,6 +39,8 @@ import contextlib
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -68,14 +82,14 @@ def make_model(device, dropout):
     return photospecMMVAE(vaes=[photo, spec], beta=c["beta"]).to(device)
 
 
-def synthetic_batch(B, seed, device):
+def synthetic_batch(B, seed, device, num_bands=None):
     """SURVEY.md §8(d) synthetic inputs (tests/golden/fill_rule.py recipe)."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("fill_rule", os.path.join(ROOT, "tests", "golden", "fill_rule.py"))
     fr = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(fr)
     rng = np.random.default_rng(seed)
-    pf, pt, pb, pm = fr.photo_inputs(rng, B, CFG["Lp"], CFG["num_bands"])
+    pf, pt, pb, pm = fr.photo_inputs(rng, B, CFG["Lp"], num_bands or CFG["num_bands"])
     sf, sw, sp, sm = fr.spec_inputs(rng, B, CFG["Ls"])
     T = lambda a: torch.from_numpy(a).to(device)
     return [(T(pf), T(pt), T(pb), T(pm)), (T(sf), T(sw), T(sp), T(sm))]
@@ -238,7 +252,7 @@ def _rocprof_avg_ms(kernel_prefix):
     return None, None
 
 
-def roofline(device, B):
+def roofline(device, B, in_step=None):
     """Spectra-decoder masked self-attention at its step shape (N = 2*K*B
     sequences x 982 tokens: the decoder runs once over both modalities'
     latents; 4 heads x dh 8, dropout 0.1, 5 % key padding),
@@ -249,7 +263,10 @@ def roofline(device, B):
     FlopCounterMode basis: fwd 4*dh (QK^T, PV), bwd 8*dh (= 2x forward: dP, dV,
     dK, dQ).  The flash backward also recomputes S (2*dh more per score):
     reported separately as flops_incl_recompute, never in `achieved`.  The kernel
-    is packed-VALU fp32 (v_pk_fma_f32), so the peak is the FP32 vector rate."""
+    is packed-VALU fp32 (v_pk_fma_f32), so the peak is the FP32 vector rate.
+    `in_step`: {"attn_fwd" / "attn_bwd": (avg ms, launches)} timed with HIP events
+    around the decoder-shape launches inside the training step (in_step_kernel_times);
+    the headline `achieved` uses it, the isolated launches are reported beside it."""
     from VAESNe import _lib, rng
     N, L, E, H, dh = 2 * CFG["K"] * B, CFG["Ls"], CFG["model_dim"], CFG["num_heads"], 8
     pd = float(os.environ.get("VAESNE_ROOFLINE_PDROP", CFG["dropout"]))   # A/B studies only
@@ -266,18 +283,11 @@ def roofline(device, B):
     bits = torch.empty(lib.attn_keep_bits_size(N, H, L, L), dtype=torch.uint8, device=device)
     b, d, s3 = qkv.data_ptr(), dqkv.data_ptr(), L * 3 * E
 
-    def fwd_with(bits_in):
-        return lambda: lib.attn_fwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E,
-                                    kbias.data_ptr(), L, o.data_ptr(), L * E, E, lse.data_ptr(),
-                                    N, H, L, L, dh, pd, st.data_ptr(), 7, bits.data_ptr(), bits_in,
-                                    None, _lib.stream())
-
-    def gen():
-        lib.attn_keep_bits(N, H, L, L, pd, st.data_ptr(), 7, bits.data_ptr(), _lib.stream())
-
-    # the step's forward hashes its dropout decisions in-kernel (the pre-drawn bitmap
-    # variant, VAESNE_PREFETCH_DROPOUT=1, is timed beside it with its generator)
-    fwd = fwd_with(0)
+    def fwd():
+        lib.attn_fwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E,
+                     kbias.data_ptr(), L, o.data_ptr(), L * E, E, lse.data_ptr(),
+                     N, H, L, L, dh, pd, st.data_ptr(), 7, bits.data_ptr(), 0,
+                     None, _lib.stream())
 
     def bwd(fn):
         return lambda: fn(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E,
@@ -298,12 +308,6 @@ def roofline(device, B):
         if tr is not None:
             res[name].update(ms_rocprof=tr, tflops_rocprof=scores * fl / (tr * 1e-3) / 1e12,
                              rocprof_source=src)
-    if pd > 0:
-        res["keep_bits_gen"] = dict(kernel="attn_keep_bits_kernel",
-                                    ms=time_kernel(gen, 20, device) * 1e3,
-                                    note="draws the forward's keep bitmap ahead (off by default)")
-        res["fwd_bits_in"] = dict(kernel="attn_fwd_kernel<..., BITSIN> (reads the drawn bitmap)",
-                                  ms=time_kernel(fwd_with(1), 20, device) * 1e3)
     # the decoders' first block: the same step shape as R = 2K copies of Bd = B distinct
     # sequences (attn_rep_*; scores, exponentials and dK/dQ products shared by the copies).
     # "equiv_tflops" counts the FLOPs of the R*Bd expanded sequences (the reference's work)
@@ -332,8 +336,13 @@ def roofline(device, B):
         t = time_kernel(fn, 20, device)
         res[name] = dict(kernel=kern, ms=t * 1e3, equiv_tflops=scores * fl / t / 1e12,
                          note=f"{R} copies x {Bd} sequences (decoder block 1)")
+    for name, key, fl in (("fwd", "attn_fwd", 4 * dh), ("bwd", "attn_bwd", 8 * dh)):
+        if in_step and key in in_step:
+            ms, n = in_step[key]
+            res[name].update(ms_in_step=ms, launches_in_step=n,
+                             tflops_in_step=scores * fl / (ms * 1e-3) / 1e12)
     r = res["bwd"]
-    a = r["tflops"]
+    a = r.get("tflops_in_step", r["tflops"])
     traffic, tsrc = None, None
     try:   # HBM bytes per launch from the committed rocprofv3 --pmc passes (gpu_run.sh pmc)
         t = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
@@ -344,19 +353,80 @@ def roofline(device, B):
     out = dict(bound="valu_fp32", kernel=r["kernel"], achieved=round(a, 3), peak=FP32_PEAK_TFLOPS,
                unit="TFLOP/s", frac=round(a / FP32_PEAK_TFLOPS, 4), traffic=traffic,
                traffic_source=tsrc,
-               launch_ms=round(r["ms"], 4), flops_per_launch=r["flops_per_launch"],
+               launch_ms=round(r.get("ms_in_step", r["ms"]), 4),
+               launch_ms_source=("HIP events around the step's own decoder-shape launches "
+                                 "(eager replay of the training step, on the launch stream)"
+                                 if "ms_in_step" in r else "HIP events, isolated launches"),
+               launch_ms_isolated=round(r["ms"], 4),
+               frac_isolated=round(r["tflops"] / FP32_PEAK_TFLOPS, 4),
+               flops_per_launch=r["flops_per_launch"],
                flops_incl_recompute=scores * 10 * dh,
+               algorithmic_bytes_per_launch=attn_bwd_algorithmic_bytes(N, H, L, dh, pd),
                detail={k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                            for kk, vv in v.items()} for k, v in res.items()},
                note="fp32 packed-VALU kernel (v_pk_fma_f32); peak = FP32 157.3 TF (vector = "
                     "f32-MFMA rate on gfx950); FLOPs per score 8*dh (FlopCounterMode: backward = "
                     "2x forward, S recompute excluded); scores per launch = 2*K*B*H*982^2 = %d; "
-                    "launch_ms = HIP events on the kernel's stream (isolated launches), "
-                    "ms_rocprof = the committed kernel-trace average inside the step" % scores)
+                    "launch_ms = in-step HIP events (headline), launch_ms_isolated = the same "
+                    "launch alone on a stream, ms_rocprof = the committed kernel-trace "
+                    "average inside the captured step" % scores)
     if "ms_rocprof" in r:
         out["launch_ms_rocprof"] = round(r["ms_rocprof"], 4)
         out["frac_rocprof"] = round(r["tflops_rocprof"] / FP32_PEAK_TFLOPS, 4)
     return out
+
+
+def attn_bwd_algorithmic_bytes(N, H, L, dh, p):
+    """HBM bytes the fused attention backward must move at least once: q|k|v read and
+    dq|dk|dv written (fp32, 3*E each per token), o and dO read (E each), lse read
+    (H per token), the key bias (1 per token) and, with dropout, the keep bitmap
+    (1 bit per score)."""
+    E = H * dh
+    per_tok = 4 * (3 * E + 3 * E + 2 * E + H + 1)
+    bits = N * H * L * L / 8 if p > 0 else 0
+    return int(N * L * per_tok + bits)
+
+
+class LaunchTimer:
+    """_ops.launch_timer: HIP events around each launch of one attention shape
+    (`work` = B*H*Lq*Lk scores) on the stream it is launched on."""
+
+    def __init__(self, work):
+        self.work = work
+        self.ev = {}
+
+    def run(self, name, work, fn):
+        if work != self.work:
+            return fn()
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        r = fn()
+        e1.record(s)
+        self.ev.setdefault(name, []).append((e0, e1))
+        return r
+
+    def averages(self):
+        torch.cuda.synchronize()
+        return {k: (sum(a.elapsed_time(b) for a, b in v) / len(v), len(v))
+                for k, v in self.ev.items()}
+
+
+def in_step_kernel_times(step, B, reps=3):
+    """Average duration of the spectra decoder's self-attention launches (blocks 2-4:
+    N = 2*K*B sequences x 982 tokens) inside `reps` eager training steps, with the
+    step's other streams running beside them.  Every rank runs it (the step's
+    all-reduce is a collective)."""
+    from VAESNe import _ops
+    t = LaunchTimer(2 * CFG["K"] * B * CFG["num_heads"] * CFG["Ls"] * CFG["Ls"])
+    step.eager()                       # settle allocations outside the timed launches
+    _ops.launch_timer = t
+    try:
+        for _ in range(reps):
+            step.eager()
+    finally:
+        _ops.launch_timer = None
+    return t.averages()
 
 
 def cpu_baseline(sample_B=4, steps=1):
@@ -504,6 +574,205 @@ def extras(device, use_graph, reps=10):
     return out
 
 
+def time_steps(step, steps, warmup, device, world):
+    """W untimed steps, then K timed steps bracketed by a barrier + device sync on both
+    sides; the max over ranks (seconds)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64,
+                         device=device if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    return dt
+
+
+def make_step(device, world, B, seed, use_graph, rank=0):
+    """The cfg-5 training step on this rank's B pairs (captured when use_graph)."""
+    from VAESNe.distributed import broadcast_parameters
+    torch.manual_seed(0)
+    model = make_model(device, CFG["dropout"])
+    broadcast_parameters(model)
+    x = synthetic_batch(B, seed + rank, device)
+    step = Step(model, x, device, world, use_graph=use_graph)
+    graph = False
+    if use_graph:
+        try:
+            step.capture()
+            graph = True
+        except Exception as e:  # reported in the JSON line, never silent
+            log(f"[bench] hipGraph capture failed ({e!r}); timing eager steps")
+            step.graphs = None
+            torch.cuda.synchronize(device)
+    return step, graph
+
+
+def strong_point(device, world, rank, args, global_batch=16):
+    """The unchanged script's data parallelism: ONE DataLoader batch of 16 pairs
+    (cannon/ZTF_photospect.py:76) split over the ranks as training_step does
+    (training_util.py: torch.tensor_split's rule), so each rank runs global/N pairs."""
+    from VAESNe.distributed import split_bounds
+    lo, hi = split_bounds(global_batch, rank, world)
+    step, graph = make_step(device, world, hi - lo, 4321, not args.no_graph, rank)
+    dt = time_steps(step, args.steps, args.warmup, device, world)
+    loss = step.loss.item()
+    del step
+    torch.cuda.empty_cache()
+    return dict(global_batch=global_batch,
+                per_gpu_batch=[b - a for a, b in (split_bounds(global_batch, r, world)
+                                                  for r in range(world))],
+                value=round(global_batch * args.steps / dt, 2), unit="SN pairs/s",
+                ms_per_step=round(dt / args.steps * 1e3, 4), hipgraph=graph,
+                finite_loss=math.isfinite(loss),
+                note="total work fixed (one global batch of 16 per step, as the script's "
+                     "DataLoader gives it) -- strong scaling; `value` above is weak scaling")
+
+
+def config_lines(device, use_graph, steps=10, warmup=3):
+    """BASELINE configs[1..3] (the other GPU configurations), each a captured training
+    step (forward, backward, FusedAdamW) on synthetic inputs of its script's shape,
+    with its matmul-FLOP basis from SURVEY.md §6 (FlopCounterMode, fwd + bwd):
+      cfg 2  cannon/test_spectra.py:59-75      SpectraVAE 4x4, beta 1, B 32, elbo K=1
+      cfg 3  cannon/test_photometry.py:52-66   PhotometricVAE 4x2, beta 0.5, B 32, elbo K=1
+                                               (ZTF light curves: 2 bands, 60 epochs)
+      cfg 4  cannon/test_photospectra.py:90-133 MMVAE 6 bands, beta 1, B 16, m_iwae K=2"""
+    from VAESNe.PhotometricVAE import PhotometricVAE
+    from VAESNe.SpectraVAE import SpectraVAE
+    from VAESNe.losses import elbo, m_iwae
+    from VAESNe.mmVAE import photospecMMVAE
+    common = dict(model_dim=32, num_heads=4, ff_dim=32, num_layers=4, dropout=0.1, selfattn=False)
+    cases = {
+        "cfg2_spectra_elbo": dict(
+            gf=1.783, B=32, lr=2.5e-4, loss=lambda m, x: elbo(m, x[1], K=1),
+            make=lambda: SpectraVAE(latent_len=4, latent_dim=4, beta=1.0, **common),
+            src="cannon/test_spectra.py:59-75"),
+        "cfg3_photometry_elbo": dict(
+            gf=0.027, B=32, lr=2.5e-4, loss=lambda m, x: elbo(m, x[0], K=1),
+            make=lambda: PhotometricVAE(num_bands=2, latent_len=4, latent_dim=2, beta=0.5, **common),
+            src="cannon/test_photometry.py:52-66 (2 ZTF bands)"),
+        "cfg4_mmvae_K2": dict(
+            gf=6.974, B=16, lr=1e-4, loss=lambda m, x: m_iwae(m, x, K=2),
+            make=lambda: photospecMMVAE(vaes=[PhotometricVAE(num_bands=6, latent_len=4, latent_dim=4,
+                                                             **common),
+                                              SpectraVAE(latent_len=4, latent_dim=4, **common)],
+                                        beta=1.0),
+            src="cannon/test_photospectra.py:90-133"),
+    }
+    out = {}
+    for name, c in cases.items():
+        torch.manual_seed(0)
+        model = c["make"]().to(device)
+        nb = 6 if name == "cfg4_mmvae_K2" else 2
+        x = synthetic_batch(c["B"], 77, device, num_bands=nb)
+        step = Step(model, x, device, 1, use_graph, loss_fn=c["loss"], lr=c["lr"])
+        graph = False
+        if use_graph:
+            try:
+                step.capture()
+                graph = True
+            except Exception as e:
+                log(f"[bench] {name}: capture failed ({e!r}); eager")
+                step.graphs = None
+        dt = time_steps(step, steps, warmup, device, 1)
+        v = c["B"] * steps / dt
+        out[name] = dict(value=round(v, 2), unit="samples/s", batch=c["B"],
+                         ms_per_step=round(dt / steps * 1e3, 4), hipgraph=graph,
+                         finite_loss=math.isfinite(step.loss.item()), script=c["src"],
+                         gflop_per_sample=c["gf"],
+                         matmul_tflops=round(v * c["gf"] / 1e3, 3),
+                         frac_fp32_peak=round(v * c["gf"] / 1e3 / FP32_PEAK_TFLOPS, 4))
+        del step, model, x
+        torch.cuda.empty_cache()
+    return out
+
+
+def training_step_eager(device, batches=4):
+    """What the script runs, literally (cannon/ZTF_photospect.py:76,119-128):
+    training_step(model, torch.optim.AdamW, DataLoader(multimodalDataset(...), 16),
+    m_iwae K=8, multimodal=True) with HOST-resident batches (H2D copies, eager launches,
+    the per-batch loss sync), one epoch of `batches` batches after a warm-up epoch."""
+    from torch.utils.data import DataLoader, TensorDataset
+    from VAESNe.data_util import multimodalDataset
+    from VAESNe.losses import m_iwae
+    from VAESNe.training_util import training_step
+    torch.manual_seed(0)
+    model = make_model(device, CFG["dropout"])
+    opt = torch.optim.AdamW(model.parameters(), lr=CFG["lr"])
+    x = synthetic_batch(16 * batches, 2024, "cpu")
+    loader = DataLoader(multimodalDataset(TensorDataset(*x[0]), TensorDataset(*x[1])),
+                        batch_size=16, shuffle=False)
+    fn = lambda m, xx: m_iwae(m, xx, K=CFG["K"])
+    training_step(model, opt, loader, loss_fn=fn, multimodal=True)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    loss = training_step(model, opt, loader, loss_fn=fn, multimodal=True)
+    torch.cuda.synchronize(device)
+    dt = (time.perf_counter() - t0) / batches
+    del model, opt
+    torch.cuda.empty_cache()
+    return dict(value=round(16 / dt, 2), unit="SN pairs/s", ms_per_step=round(dt * 1e3, 3),
+                batch=16, batches=batches, optimizer="torch.optim.AdamW", finite_loss=math.isfinite(loss),
+                note="eager, host-resident DataLoader batches, per-batch loss sync; "
+                     "the headline times the captured step with FusedAdamW on HBM-resident inputs")
+
+
+def launch_ranks(n, argv):
+    """Start ranks 0..n-1 of this script as fresh child processes (nothing in this
+    process touches the GPU), wait for them, and return the worst exit status.  A
+    failing rank ends the others (their exact PIDs)."""
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for pr in list(live):
+            code = pr.poll()
+            if code is None:
+                continue
+            live.remove(pr)
+            if code != 0:
+                rc = rc or code
+                for other in live:
+                    other.terminate()
+        time.sleep(0.2)
+    return rc if rc >= 0 else 128 - rc
+
+
+def rank_check(world):
+    """Each rank (as launch_ranks or torchrun started it) joins a gloo group on the CPU
+    and all-gathers (RANK, LOCAL_RANK, WORLD_SIZE); rank 0 prints them as JSON."""
+    rank = int(os.environ.get("RANK", "0"))
+    if os.environ.get("VAESNE_RANK_CHECK_FAIL") == str(rank):
+        sys.exit(3)        # the launcher test: one rank dies before the rendezvous
+    me = [rank, int(os.environ.get("LOCAL_RANK", "0")), world]
+    seen = [me]
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        seen = [None] * world
+        dist.all_gather_object(seen, me)
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"world": world, "ranks": seen}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -513,12 +782,17 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling point (N>1)")
     ap.add_argument("--throughput-batch", type=int, default=64,
                     help="also time the same step at this per-GPU batch (N=1 only; 0 = skip)")
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip the §8(f) side measurements (reconstruct K=100, contrastive step)")
+                    help="skip the side measurements (reconstruct K=100, contrastive step, "
+                         "eager training_step, BASELINE cfgs 2-4)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the roofline kernel launches (for rocprofv3 --pmc passes)")
+    ap.add_argument("--rank-check", action="store_true",
+                    help="launcher check without a GPU: every rank joins a gloo group and rank 0 "
+                         "prints the world it sees (tests/test_bench_launcher.py)")
     args = ap.parse_args()
     if args.roofline_only:
         device = torch.device("cuda", 0)
@@ -529,50 +803,41 @@ def main():
         print(json.dumps(roofline(device, args.batch)), flush=True)
         return
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_ws = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if env_ws == 0 and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = max(1, env_ws)
+    if args.rank_check:
+        rank_check(world)
+        return
+    if world != args.gpus:
+        log(f"[bench] --gpus {args.gpus} but the launcher describes {world} ranks: using {world}")
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = torch.device("cuda", local)
+    from VAESNe.distributed import dp_backend, local_device_index
+    device = torch.device("cuda", local_device_index())
     torch.cuda.set_device(device)
+    backend = dp_backend() if world > 1 else None
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     from VAESNe import _lib, rng
-    from VAESNe.distributed import broadcast_parameters
     _lib.load()
-    torch.manual_seed(0)
     rng.manual_seed(1234)        # each rank folds its rank in (rng.rank_seed): own noise / dropout
-    model = make_model(device, CFG["dropout"])
-    broadcast_parameters(model)
-    x = synthetic_batch(args.batch, 1234 + rank, device)
-    step = Step(model, x, device, world, use_graph=not args.no_graph)
-    graph = False
-    if not args.no_graph:
-        try:
-            step.capture()
-            graph = True
-        except Exception as e:  # reported in the JSON line, never silent
-            log(f"[bench] hipGraph capture failed ({e!r}); timing eager steps")
-            step.graphs = None
-            torch.cuda.synchronize(device)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(device)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
+    step, graph = make_step(device, world, args.batch, 1234, not args.no_graph, rank)
+    dt = time_steps(step, args.steps, args.warmup, device, world)
     loss = step.loss.item()
     if not math.isfinite(loss):
         raise RuntimeError(f"non-finite training loss {loss}")
+    in_step = None
+    if not args.no_roofline:
+        in_step = in_step_kernel_times(step, args.batch)
+    del step
+    torch.cuda.empty_cache()
+    strong = None
+    if world > 1 and not args.no_strong:
+        strong = strong_point(device, world, rank, args)
     ms = dt / args.steps * 1e3
     value = world * args.batch * args.steps / dt
     out = {
@@ -584,18 +849,24 @@ def main():
                    "global_batch": args.batch * world, "K": CFG["K"], "seq_len": CFG["Ls"],
                    "photometry_len": CFG["Lp"], "num_bands": CFG["num_bands"], "beta": CFG["beta"],
                    "dropout": CFG["dropout"], "spectra_selfattn": True, "parallelism": f"dp{world}",
-                   "hipgraph": graph},
+                   "dp_backend": backend, "hipgraph": graph},
         "value_per_gpu": round(value / world, 2),
         # whole-step rates from SURVEY.md §8(d)'s per-pair work at cfg 5 (FlopCounterMode on
         # the reference: 29.214 GFLOP of matmul fwd+bwd per pair; 262.4 M softmax scores per
         # pair in the forward), against the fp32 peak the step computes at
         "step_utilization": {
             "matmul_tflops": round(value * STEP_GFLOP_PER_PAIR / 1e3, 2),
-            "frac_fp32_peak": round(value * STEP_GFLOP_PER_PAIR / 1e3 / FP32_PEAK_TFLOPS, 4),
+            "frac_fp32_peak": round(value * STEP_GFLOP_PER_PAIR / 1e3 / FP32_PEAK_TFLOPS / world, 4),
             "softmax_gscores_per_s": round(value * STEP_MSCORES_PER_PAIR / 1e3, 1),
             "gflop_per_pair": STEP_GFLOP_PER_PAIR, "mscores_per_pair_fwd": STEP_MSCORES_PER_PAIR},
         "final_loss": loss,
     }
+    if world == 1:
+        out["strong_scaling"] = dict(global_batch=args.batch, per_gpu_batch=[args.batch],
+                                     value=out["value"], unit="SN pairs/s", ms_per_step=out["ms_per_step"],
+                                     note="one GPU: the headline step itself")
+    elif strong is not None:
+        out["strong_scaling"] = strong
     if rank == 0:
         try:
             out.update(parity(device))
@@ -603,19 +874,26 @@ def main():
             out["elbo_rel_err"] = None
             log(f"[bench] parity failed: {e!r}")
         if not args.no_roofline:
-            out["roofline"] = roofline(device, args.batch)
+            out["roofline"] = roofline(device, args.batch, in_step)
         if world == 1 and args.throughput_batch > 0:
             out["throughput_batch"] = throughput_point(device, args.throughput_batch, not args.no_graph)
         if world == 1 and not args.no_extras:
-            try:
-                out["extras"] = extras(device, not args.no_graph)
-            except Exception as e:   # a side measurement never hides the headline line
-                out["extras"] = None
-                log(f"[bench] extras failed: {e!r}")
+            ex = {}
+            for name, fn in (("f", lambda: extras(device, not args.no_graph)),
+                             ("configs", lambda: config_lines(device, not args.no_graph)),
+                             ("training_step_eager", lambda: training_step_eager(device))):
+                try:   # a side measurement never hides the headline line
+                    r = fn()
+                    ex.update(r) if name == "f" else ex.__setitem__(name, r)
+                except Exception as e:
+                    ex[name] = None
+                    log(f"[bench] extras {name} failed: {e!r}")
+            out["extras"] = ex
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

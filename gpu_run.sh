@@ -12,6 +12,7 @@ for s in $STAGES; do
     tests) timeout -k 10 900 python -m pytest tests -m gpu -q -rf --timeout 300 ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1; rc=$?;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?;;
     bench) timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?;;
+    bench2) VAESNE_DP_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 10 --warmup 3 > gpurun_out/bench2.json 2> gpurun_out/bench2.err; rc=$?;;
     prof)  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --throughput-batch 0 --no-extras > gpurun_out/prof.log 2>&1; rc=$?;;
     pmc)   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --roofline-only > gpurun_out/pmc_fetch.log 2>&1; rc=$?
            [ $rc -eq 0 ] && { timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --roofline-only > gpurun_out/pmc_write.log 2>&1; rc=$?; };;
@@ -19,7 +20,7 @@ for s in $STAGES; do
   echo "$s rc=$rc"
   ok $rc || exit $rc
   # a GPU fault inside pytest still exits 1: stop the session there
-  if grep -qsE "illegal memory access|Memory access fault|hipErrorIllegalAddress|HSA_STATUS_ERROR" gpurun_out/pytest_gpu.log gpurun_out/smoke.log gpurun_out/bench.err; then
+  if grep -qsE "illegal memory access|Memory access fault|hipErrorIllegalAddress|HSA_STATUS_ERROR" gpurun_out/pytest_gpu.log gpurun_out/smoke.log gpurun_out/bench.err gpurun_out/bench2.err; then
     echo "GPU fault reported in $s; stopping"; exit 3
   fi
 done

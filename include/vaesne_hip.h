@@ -497,12 +497,17 @@ int vaesne_infonce_bwd(const float* nz, const float* nrm, const float* lse, int 
  * be captured in a hipGraph. */
 int vaesne_adamw(float* p, const float* g, float* m, float* v, int64_t n, const float* step,
                  const int32_t* pidx, float lr, float b1, float b2, float eps, float wd,
-                 void* stream);
+                 const int32_t* skip, void* stream);
 /* per-parameter step counts (torch.optim.AdamW's state['step']): pidx [n] maps each
  * element to its parameter and step[pidx[t]] is that parameter's count (pidx null: one
  * count step[0] for all).  steps[i] += 1 for the parameters that have a gradient this
- * step (active[i] != 0; active null: all). */
-int vaesne_adamw_steps_advance(float* steps, const uint8_t* active, int P, void* stream);
+ * step (active[i] != 0; active null: all).  skip (both calls, nullable): the non-finite
+ * guard flag int32[2] the latent-head and loss kernels set (VAESNe/guard.py); when
+ * either word is non-zero neither kernel changes anything, so a flagged step never
+ * reaches the parameters or the step counts (the reference stops before its update on a
+ * NaN posterior, PhotometricVAE.py:160-161). */
+int vaesne_adamw_steps_advance(float* steps, const uint8_t* active, int P, const int32_t* skip,
+                               void* stream);
 int vaesne_step_advance(float* step, int64_t* rng_state, void* stream);
 /* gather (unpack=0) / scatter (unpack=1) `count` tensors to/from a flat buffer */
 int vaesne_pack(const float* const* srcs, const int64_t* offs, const int64_t* ns, int count,

@@ -350,6 +350,24 @@ def mmvae_forward(p, cfg: MMVAECfg, x, K, us, p_drop=0.0, training=False):
     return qz, px, zss
 
 
+def mmvae_generate(p, cfg: MMVAECfg, x, N, u):
+    """photospecMMVAE.generate -- mmVAE.py:108-118: latents = Laplace(_pz_params)
+    .rsample([N, B]) (u [N, B, Lz, Dz]), decoded by every modality at its x grid; the
+    decoders' means (= loc).  Eval mode: no dropout."""
+    z = laplace_rsample(p["_pz_params.0"], p["_pz_params.1"], u)
+    cfgs = [cfg.photo, cfg.spec]
+    return [decode(p, f"vaes.{d}.", cfgs[d], z, x[d]).loc for d in range(2)]
+
+
+def spectra_generate(p, pre: str, c: VaeCfg, x, N, u):
+    """SpectraVAE.generate -- SpectraVAE.py:198-206: zs = Laplace(pz_params).rsample(
+    [N, 1]) (u [N, 1, Lz, Dz]) decoded at x's grid (one conditioning spectrum: the
+    reference's decode expands x K = N times against N latent rows), returned as
+    mean.unsqueeze(0) [1, N, 1, L]."""
+    z = laplace_rsample(p[pre + "_pz_params.0"], p[pre + "_pz_params.1"], u)
+    return decode(p, pre, c, z, x).loc.unsqueeze(0)
+
+
 # ----------------------------------------------------------------------------
 # L5 objectives (losses.py)
 # ----------------------------------------------------------------------------

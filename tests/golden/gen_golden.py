@@ -262,6 +262,36 @@ def run_case(name, c, outdir):
     print(f"{name}: loss={out['loss']:.6f} traj={losses} -> {path}")
 
 
+# §8(f) 1: generation from the prior (mmVAE.py:108-118, SpectraVAE.py:198-206); each
+# consumes ONE uniform draw (Laplace.rsample of the prior), recorded by replay.
+GEN_CASES = ["mmvae_tiny", "mmvae_cfg5"]
+
+
+def run_generate(name, c, outdir, N=3):
+    """gen_<name>.npz: photospecMMVAE.generate(N, x) (prior draws [N, B, Lz, Dz] decoded
+    by both modalities) and SpectraVAE.generate(N, x1[:1]) (draws [N, 1, Lz, Dz]; the
+    reference's decode needs a single conditioning spectrum there) of the filled model."""
+    model = build(c)
+    x = to_x(c, inputs(c))
+    eps = torch.finfo(torch.float32).eps
+    out = {"config": np.array(json.dumps(c)), "N": np.array(N)}
+    B = x[0][0].shape[0]
+    torch.manual_seed(21)
+    out["u_gen"] = torch.empty(N, B, c["Lz"], c["Dz"]).uniform_(eps - 1, 1).numpy()
+    torch.manual_seed(21)
+    gen = model.generate(N, x)
+    out["gen0"], out["gen1"] = gen[0].numpy(), gen[1].numpy()
+    x1 = tuple(t[:1] for t in x[1])
+    torch.manual_seed(22)
+    out["u_sgen"] = torch.empty(N, 1, c["Lz"], c["Dz"]).uniform_(eps - 1, 1).numpy()
+    torch.manual_seed(22)
+    out["sgen"] = model.vaes[1].generate(N, x1).numpy()
+    path = os.path.join(outdir, f"gen_{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"gen_{name}: gen0 {out['gen0'].shape} gen1 {out['gen1'].shape} "
+          f"sgen {out['sgen'].shape} -> {path}")
+
+
 if __name__ == "__main__":
     outdir = sys.argv[1] if len(sys.argv) > 1 else HERE
     only = sys.argv[2:]
@@ -273,3 +303,7 @@ if __name__ == "__main__":
         if only and ("ckpt_" + name) not in only:
             continue
         run_ckpt(name, CASES[name], outdir)
+    for name in GEN_CASES:
+        if only and ("gen_" + name) not in only:
+            continue
+        run_generate(name, CASES[name], outdir)

@@ -56,9 +56,14 @@ def test_nonfinite_loss_raises_from_training_step():
     x = golden_x(g, "cuda")
     fn = lambda m, xx: m_iwae(m, xx, K=K)
     bad = [torch.full_like(u, float("nan")) for u in golden_us(g)]
+    before = opt.flat_params().clone()
     with rng.inject_uniform(bad), pytest.raises(RuntimeError, match="non-finite loss"):
         training_step(model, opt, [x], loss_fn=fn, multimodal=True)
     assert guard.status("cuda") == (False, False)       # cleared by the raise
+    # raised BEFORE the update (the reference stops before optimizer.step)
+    assert torch.equal(opt.flat_params(), before)
+    # a flag left by an unchecked eval call does not fail the next training batch
+    guard.flag("cuda")[0] = 1
     g2, model2, opt2 = _tiny()
     with rng.inject_uniform(golden_us(g)):
         assert np.isfinite(training_step(model2, opt2, [x], loss_fn=fn, multimodal=True))
@@ -142,9 +147,10 @@ def test_training_step_data_parallel_matches_full_batch():
 
 
 def _b16_grads(streams):
-    from VAESNe import rng
+    from VAESNe import _config, rng
     from VAESNe.losses import m_iwae
-    os.environ["VAESNE_STREAMS"] = streams
+    saved = _config.streams
+    _config.streams = streams == "1"
     try:
         g = load_golden("mmvae_cfg5_b16")
         c = g["config"]
@@ -156,7 +162,7 @@ def _b16_grads(streams):
         torch.cuda.synchronize()
         return {k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None}
     finally:
-        os.environ.pop("VAESNE_STREAMS", None)
+        _config.streams = saved
 
 
 def test_side_streams_bitwise_equal_single_stream_at_bench_config():

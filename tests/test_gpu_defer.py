@@ -5,7 +5,6 @@ one, so every gradient must be bit-identical to the immediate path; parameters
 that cannot be deferred safely (accumulating into an existing .grad, used twice)
 must fall back, and a parameter that also feeds a plain torch op must raise."""
 import ctypes as C
-import os
 
 import pytest
 import torch
@@ -17,9 +16,10 @@ DEV = "cuda"
 
 
 def _grads(case, defer, streams="1"):
-    from VAESNe import _defer, rng
+    from VAESNe import _config, _defer, rng
     from VAESNe.losses import m_iwae
-    os.environ["VAESNE_STREAMS"] = streams
+    saved = _config.streams
+    _config.streams = streams == "1"
     try:
         g = load_golden(case)
         c = g["config"]
@@ -32,7 +32,7 @@ def _grads(case, defer, streams="1"):
         torch.cuda.synchronize()
         return {k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None}
     finally:
-        os.environ.pop("VAESNE_STREAMS", None)
+        _config.streams = saved
 
 
 @pytest.mark.parametrize("case,streams", [("mmvae_cfg5_b16", "1"), ("mmvae_cfg5_b16", "0"),
@@ -126,3 +126,35 @@ def test_parameter_also_used_by_a_torch_op_raises():
     lin.bias.grad = None
     (lin(x).square().sum() + lin.weight.square().sum()).backward()
     assert torch.isfinite(lin.weight.grad).all()
+
+
+def test_backward_that_raises_leaves_no_stale_deferred_state():
+    """A backward that raises after some ops deferred their sums (before the flush
+    callback ran) must not leave the deferral armed: the next backward queues its own
+    flush and its gradients equal the immediate path bit for bit."""
+    from VAESNe import _defer, rng
+    from VAESNe.losses import m_iwae
+    g = load_golden("mmvae_tiny")
+    c = g["config"]
+    model = build_model(c)
+    model.train()
+    # the photometry encoder's bottleneck queries are read first in the forward, so
+    # their gradient arrives late in the backward, after the decoders deferred theirs
+    p0 = model.vaes[0].enc.inference_transformer.initbottleneck
+
+    def boom(_):
+        raise RuntimeError("boom in backward")
+    h = p0.register_hook(boom)
+    with pytest.raises(RuntimeError, match="boom in backward"):
+        with _defer.deferred(True):
+            with rng.inject_uniform(golden_us(g)):
+                loss = -m_iwae(model, golden_x(g, "cuda"), K=c["K"])
+            loss.backward()
+    h.remove()
+    torch.cuda.synchronize()
+    assert _defer._S.clist.count == 0 and not _defer._S.armed and not _defer._S.pending
+    now = _grads("mmvae_tiny", False)
+    later = _grads("mmvae_tiny", True)
+    assert set(now) == set(later)
+    for k in now:
+        assert torch.equal(now[k], later[k]), k

@@ -33,9 +33,9 @@ def _mask(B, L, p, g):
 
 
 def _run(blocks, x, ctx, mask, go, chain, monkeypatch, defer=False):
-    from VAESNe import _defer, rng
+    from VAESNe import _config, _defer, rng
     from VAESNe.util_layers import encoder_stack
-    monkeypatch.setenv("VAESNE_ENC_CHAIN", "1" if chain else "0")
+    monkeypatch.setattr(_config, "enc_chain", bool(chain))
     rng.manual_seed(1234)
     blocks.zero_grad(set_to_none=True)
     xx = x.clone().requires_grad_(True)
@@ -147,8 +147,9 @@ def test_chain_fully_masked_row_gives_nan_like_reference(monkeypatch):
     mask = torch.zeros(B, Lc, dtype=torch.bool)
     mask[1] = True
     mask = mask.to(DEV)
+    from VAESNe import _config
     from VAESNe.util_layers import encoder_stack
-    monkeypatch.setenv("VAESNE_ENC_CHAIN", "1")
+    monkeypatch.setattr(_config, "enc_chain", True)
     with torch.no_grad():
         out = encoder_stack(blocks, x, ctx, context_mask=mask)
     assert torch.isnan(out[1]).all()

@@ -4,7 +4,8 @@
   and VAE.encode(x, mean) (PhotometricVAE.py:179-186, SpectraVAE.py:167-176) against the
   reference's golden vectors (same parameters / inputs / injected noise, dropout off);
 * reconstruct at the scripts' K = 100 (batched, eval mode) against the oracle;
-* generate (mmVAE.py:108-118): shapes, finiteness, decoder-scale semantics;
+* generate (mmVAE.py:108-118, SpectraVAE.py:198-206) against the reference's outputs
+  for its recorded prior draws, and shapes / finiteness at other sizes;
 * VAEregressionHead (regression.py:9-26) forward/backward against an fp64 restatement
   on the oracle's encoder, with the VAE frozen;
 * whole-module torch.save / torch.load round trip of the build's own model
@@ -68,6 +69,30 @@ def test_reconstruct_K100_matches_oracle():
         for d in range(2):
             assert rec[e][d].shape == px[e][d].loc.shape
             assert _rel(rec[e][d], px[e][d].loc) < 1e-4, (e, d)
+
+
+@pytest.mark.parametrize("name", ["mmvae_tiny", "mmvae_cfg5"])
+def test_generate_matches_reference(name):
+    """photospecMMVAE.generate(N, x) (mmVAE.py:108-118: ONE prior draw [N, B, Lz, Dz]
+    decoded by both modalities) and SpectraVAE.generate(N, x1) (SpectraVAE.py:198-206:
+    draws [N, 1, Lz, Dz], one conditioning spectrum) against the reference's outputs for
+    its recorded uniform draws (tests/golden/gen_*.npz)."""
+    from VAESNe import rng
+    g = load_golden("gen_" + name)
+    c = g["config"]
+    model = build_model(c)
+    model.train()                         # generate() switches to eval itself
+    x = golden_x(load_golden(name), "cuda")
+    N = int(g["N"])
+    with rng.inject_uniform([torch.from_numpy(g["u_gen"])]):
+        gen = model.generate(N, x)
+    assert not model.training
+    for d in range(2):
+        assert tuple(gen[d].shape) == g[f"gen{d}"].shape
+        assert _rel(gen[d], g[f"gen{d}"]) < 1e-4, d
+    with rng.inject_uniform([torch.from_numpy(g["u_sgen"])]):
+        s = model.vaes[1].generate(N, tuple(t[:1] for t in x[1]))
+    assert tuple(s.shape) == g["sgen"].shape and _rel(s, g["sgen"]) < 1e-4
 
 
 def test_generate_shapes_and_scales():

@@ -527,9 +527,9 @@ def test_fused_encoder_stack_matches_per_op(selfattn, B, T, Lc):
 @pytest.mark.parametrize("B,Lc,defer", [(16, 983, False), (3, 70, True)])
 def test_merged_context_paths_match_per_block(B, Lc, defer, monkeypatch):
     """The blocks' context self-attention paths batch-stacked into one attention
-    launch (util_layers._merged_context_paths, VAESNE_CTX_MERGE) against one path
+    launch (util_layers._merged_context_paths, _config.ctx_merge) against one path
     per block: outputs and every gradient (cfg-5 shape: 4 blocks, 983 tokens)."""
-    from VAESNe import _defer
+    from VAESNe import _config, _defer
     from VAESNe.util_layers import encoder_stack
     blocks = _encoder_blocks(4, B + Lc + 1, True).to(DEV)
     blocks.train()
@@ -540,7 +540,7 @@ def test_merged_context_paths_match_per_block(B, Lc, defer, monkeypatch):
     go = torch.randn(B, 8, 32, generator=g).to(DEV)
     res = []
     for merge in ("1", "0"):
-        monkeypatch.setenv("VAESNE_CTX_MERGE", merge)
+        monkeypatch.setattr(_config, "ctx_merge", merge == "1")
         blocks.zero_grad(set_to_none=True)
         xx = x.clone().requires_grad_(True)
         cc = ctx.clone().requires_grad_(True)
@@ -639,42 +639,6 @@ def test_keep_bits_generator_matches_forward_and_bits_in_forward(geo, B, H, Lq, 
         lib.attn_force_geometry(0, 0)
 
 
-def test_prefetched_decoder_bitmaps_give_the_hashing_result():
-    """decoder_stack with KeepBits prefetched on the side stream equals the
-    in-kernel hashing path for the same call ids (forward and every gradient)."""
-    from VAESNe import _ops, rng
-    from VAESNe.util_layers import _gen_stream, decoder_stack
-    blocks = _decoder_blocks(2, 3).to(DEV)
-    for b in blocks:     # attention-probability dropout only (the tails draw no ids)
-        b.train()
-        b.self_attn.dropout = 0.1
-    N, L, Lc = 6, 300, 5
-    x0 = torch.randn(N, L, 32, device=DEV)
-    ctx0 = torch.randn(N, Lc, 32, device=DEV)
-    mask = torch.rand(N, L, device=DEV) < 0.1
-    mask[:, 0] = False
-    outs = []
-    for pre in (False, True):
-        x = x0.clone().requires_grad_(True)
-        ctx = ctx0.clone().requires_grad_(True)
-        for b in blocks:
-            b.zero_grad()
-        rng._call = 500
-        keep = None
-        if pre:   # the call ids the hashing path draws for the two self-attentions: 501, 502
-            keep = [_ops.KeepBits(N, 4, L, L, 0.1, x.device, _gen_stream(x.device))
-                    for _ in range(2)]
-        y = decoder_stack(blocks, x, ctx, mask, keep=keep)
-        (y * torch.sin(torch.arange(y.numel(), device=DEV).view_as(y) * 1e-3)).sum().backward()
-        outs.append((y.detach(), x.grad, ctx.grad,
-                     [p.grad.clone() for b in blocks for p in b.parameters() if p.grad is not None]))
-    (y0, dx0, dc0, g0), (y1, dx1, dc1, g1) = outs
-    assert torch.equal(y0, y1)
-    assert torch.equal(dx0, dx1) and torch.equal(dc0, dc1)
-    for a, b in zip(g0, g1):
-        assert torch.equal(a, b)
-
-
 @pytest.mark.parametrize("M,with_h,defer", [(982 * 3, True, False), (251392, True, True),
                                             (77, False, False), (1, True, False)])
 def test_fused_mlp_head_matches_two_linears(M, with_h, defer, monkeypatch):
@@ -683,7 +647,7 @@ def test_fused_mlp_head_matches_two_linears(M, with_h, defer, monkeypatch):
     against the two-linear path (fc1 + ReLU, fc2), forward and every gradient.
     Tokens with a pre-activation within 1e-3 of the ReLU kink get dy = 0: the two
     paths sum in different orders, so there a ReLU decision may legitimately flip."""
-    from VAESNe import _defer
+    from VAESNe import _config, _defer
     from VAESNe.util_layers import singlelayerMLP
     g = torch.Generator().manual_seed(M)
     head = singlelayerMLP(32, 1)
@@ -698,7 +662,7 @@ def test_fused_mlp_head_matches_two_linears(M, with_h, defer, monkeypatch):
     h0 = None if h0 is None else h0.to(DEV)
     res = []
     for fused in ("0", "1"):
-        monkeypatch.setenv("VAESNE_FUSED_HEAD", fused)
+        monkeypatch.setattr(_config, "fused_head", fused == "1")
         head.zero_grad(set_to_none=True)
         x = x0.clone().requires_grad_(True)
         h = None if h0 is None else h0.clone().requires_grad_(True)

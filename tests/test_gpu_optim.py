@@ -61,3 +61,44 @@ def test_state_dict_round_trip_between_optimizers(src, dst):
     ref, _ = _run(torch.optim.AdamW, 5)
     for a, b in zip(cont, ref):
         assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), (a - b).abs().max()
+
+
+def test_flagged_step_changes_nothing():
+    """A set non-finite guard flag (VAESNe.guard: NaN posterior / non-finite loss of
+    this step) makes the update kernels no-ops: parameters, moments and step counts
+    unchanged, as inside a captured step where nothing on the host can intervene.
+    Clearing the flag lets the next step update as usual."""
+    from VAESNe import guard
+    from VAESNe.optim import FusedAdamW
+    ps = [torch.nn.Parameter(t.clone().to(DEV)) for t in _params(0)]
+    opt = FusedAdamW(ps, lr=1e-2)
+    for p, gr in zip(ps, _grads(1, 0)):
+        p.grad = gr.to(DEV)
+    fl = opt._flat[0]
+    before = [fl[k].clone() for k in ("flat", "m", "v", "steps")]
+    guard.flag(DEV)[1] = 1
+    try:
+        opt.step()
+        torch.cuda.synchronize()
+        for k, b in zip(("flat", "m", "v", "steps"), before):
+            assert torch.equal(fl[k], b), k
+    finally:
+        guard.reset(DEV)
+    opt.step()
+    torch.cuda.synchronize()
+    assert not torch.equal(fl["flat"], before[0]) and float(fl["steps"].max()) == 1.0
+
+
+def test_load_state_dict_refuses_amsgrad_and_maximize():
+    from VAESNe.optim import FusedAdamW
+    for k in ("amsgrad", "maximize"):
+        ps = [torch.nn.Parameter(t.clone().to(DEV)) for t in _params(0)]
+        sd = torch.optim.AdamW(ps, lr=1e-2, **{k: True}).state_dict()
+        with pytest.raises(ValueError, match=k):
+            FusedAdamW(ps, lr=1e-2).load_state_dict(sd)
+    ps = [torch.nn.Parameter(t.clone().to(DEV)) for t in _params(0)]
+    sd = torch.optim.AdamW(ps, lr=3e-3, betas=(0.8, 0.9), foreach=False).state_dict()
+    opt = FusedAdamW(ps, lr=1e-2)
+    opt.load_state_dict(sd)
+    g = opt.param_groups[0]
+    assert g["lr"] == 3e-3 and tuple(g["betas"]) == (0.8, 0.9) and "foreach" not in g

@@ -168,3 +168,27 @@ def test_training_step_api():
     l1 = training_step(model, opt, loader, loss_fn=lambda m, xx: m_iwae(m, xx, K=2),
                        multimodal=True)
     assert np.isfinite(l1)
+
+
+@pytest.mark.parametrize("name", ["mmvae_tiny", "mmvae_cfg4", "elbo_spec_cfg2"])
+def test_identical_seeds_reproduce_reference_loss(name):
+    """North_star's "identical inputs/seeds" without injected noise: with
+    rng.set_mode("torch_cpu") the sampler draws u from torch's CPU generator exactly as
+    the reference does on CPU (laplace.py:83, photometry first), so torch.manual_seed(7)
+    -- the seed the fixture's loss was computed under (gen_golden.py run_case) -- gives
+    the reference's loss."""
+    from VAESNe import rng
+    from VAESNe.losses import elbo, m_iwae
+    g = load_golden(name)
+    c = g["config"]
+    model = build_model(c)
+    model.train()
+    x = golden_x(g, "cuda")
+    rng.set_mode("torch_cpu")
+    try:
+        torch.manual_seed(7)
+        with torch.no_grad():
+            loss = -(m_iwae(model, x, K=c["K"]) if c["kind"] == "mmvae" else elbo(model, x, K=c["K"]))
+    finally:
+        rng.set_mode("device")
+    assert _rel(loss, g["loss"]) < LOSS_TOL, (loss.item(), float(g["loss"]))

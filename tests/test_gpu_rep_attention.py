@@ -126,7 +126,7 @@ def test_rep_backward_equals_summed_plain_backward(cfg, Bd, R, L, pm, p):
 
 def test_rep_decoder_stack_and_model_step_equal_expanded_path(monkeypatch):
     """A cfg-5-shaped MMVAE training step (dropout on) with the repeated first-block
-    attention against VAESNE_REP_ATTN=0 (expanded input, plain kernels): the same
+    attention against _config.rep_attn off (expanded input, plain kernels): the same
     dropout call ids, so the loss agrees to fp32 summation order (1e-5) and so do
     the gradients, up to the importance weights: lw sums ~10^3 log-probabilities, so
     a 1e-7 relative change in a decoder location moves lw by ~1e-4 and the softmax
@@ -136,7 +136,7 @@ def test_rep_decoder_stack_and_model_step_equal_expanded_path(monkeypatch):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
-    from VAESNe import rng
+    from VAESNe import _config, rng
     from VAESNe.losses import m_iwae
     torch.manual_seed(3)
     model = bench.make_model(DEV, 0.1)
@@ -144,7 +144,7 @@ def test_rep_decoder_stack_and_model_step_equal_expanded_path(monkeypatch):
     x = bench.synthetic_batch(2, 5, DEV)
     outs = []
     for flag in ("0", "1", "1"):
-        monkeypatch.setenv("VAESNE_REP_ATTN", flag)
+        monkeypatch.setattr(_config, "rep_attn", flag == "1")
         model.zero_grad(set_to_none=True)
         rng.manual_seed(77)
         loss = -m_iwae(model, x, K=3)

@@ -86,3 +86,23 @@ def test_oracle_adamw_trajectory(name):
             # +-lr steps, so it is chaotic in any implementation.  Skipped.
             continue
         assert abs(p[k].detach().norm().item() - n) <= 1e-5 * max(n, 1.0), k
+
+
+@pytest.mark.parametrize("name", ["mmvae_tiny", "mmvae_cfg5"])
+def test_oracle_generate_matches_reference(name):
+    """photospecMMVAE.generate (mmVAE.py:108-118) and SpectraVAE.generate
+    (SpectraVAE.py:198-206) with the reference's recorded prior draws."""
+    g = load_golden("gen_" + name)
+    c = g["config"]
+    cfg = oracle_cfg(c)
+    p = O.make_params(cfg, fill_rule.fill)
+    x = golden_x(load_golden(name))
+    N = int(g["N"])
+    with torch.no_grad():
+        gen = O.mmvae_generate(p, cfg, x, N, torch.from_numpy(g["u_gen"]))
+        sgen = O.spectra_generate(p, "vaes.1.", cfg.spec, tuple(t[:1] for t in x[1]), N,
+                                  torch.from_numpy(g["u_sgen"]))
+    for d in range(2):
+        assert gen[d].shape == g[f"gen{d}"].shape
+        assert _rel(gen[d], g[f"gen{d}"]) < 1e-5, d
+    assert sgen.shape == g["sgen"].shape and _rel(sgen, g["sgen"]) < 1e-5

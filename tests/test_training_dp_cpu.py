@@ -8,7 +8,9 @@
 * mean objectives (elbo) weight each rank's gradient by its batch share, sum
   objectives (m_iwae-style) SUM: after two epochs the parameters equal a single
   process training on the full batches;
-* every rank draws its own device noise / dropout streams (rng.rank_seed).
+* every rank draws its own device noise / dropout streams (rng.rank_seed);
+* a non-finite loss on ONE rank makes every rank raise RuntimeError before the
+  update (the verdict rides the loss all-reduce), parameters unchanged.
 
 The model is a small deterministic host-side VAE (no sampling), so a full batch
 and its shards compose exactly; elbo runs through losses.elbo's host branch.
@@ -42,6 +44,9 @@ class _ToyVAE(nn.Module):
         self._pz_params = nn.ParameterList([nn.Parameter(torch.zeros(1, 2), requires_grad=False),
                                             nn.Parameter(torch.ones(1, 2), requires_grad=False)])
         self.llik_scaling = 2.0
+        # a trainable parameter the loss never reaches: every rank must leave its .grad
+        # None (distributed.agree_grad_pattern), also the rank with an empty slice
+        self.unused = nn.Parameter(torch.ones(3))
 
     @property
     def pz_params(self):
@@ -142,3 +147,47 @@ def test_split_bounds_even():
     x = [(torch.arange(10),), (torch.arange(10) * 2,)]
     parts = [shard(x, r, 3) for r in range(3)]
     assert torch.equal(torch.cat([p[1][0] for p in parts]), x[1][0])
+
+
+def _fail_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(ws), LOCAL_RANK=str(rank))
+    try:
+        from VAESNe.losses import elbo
+        from VAESNe.training_util import training_step
+        torch.set_num_threads(1)
+        torch.distributions.Distribution.set_default_validate_args(False)   # NaN gets to the loss
+        torch.manual_seed(0)
+        model = _ToyVAE()
+        x, y = _data(4, nb=1)[0]
+        x = x.clone()
+        x[2:] = float("nan")          # rows 2..3: the slice of rank 1 only
+        before = [p.detach().clone() for p in model.parameters()]
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+        try:
+            training_step(model, opt, [(x, y)], loss_fn=elbo)
+            q.put((rank, False, "", True))
+        except RuntimeError as e:
+            same = all(torch.equal(a, p.detach()) for a, p in zip(before, model.parameters()))
+            q.put((rank, True, str(e), same))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_nonfinite_loss_on_one_rank_raises_on_every_rank():
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(120)
+        assert pr.exitcode == 0, f"rank exit code {pr.exitcode} (a hang ends in -15 / None)"
+    res = sorted(q.get() for _ in range(ws))
+    for rank, raised, msg, unchanged in res:
+        assert raised, f"rank {rank} did not raise"
+        assert "non-finite" in msg, msg
+        assert unchanged, f"rank {rank}: parameters changed by a rejected step"

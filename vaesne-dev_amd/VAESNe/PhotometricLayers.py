@@ -46,9 +46,9 @@ class photometricTransformerDecoder(nn.Module):
                           first=first)
         return self.get_photo(x_out, h).squeeze(-1)   # get_photo(x + h)
 
-    def prepare(self, time, band, mask=None, repeat=1, lc=1, attend=True):
+    def prepare(self, time, band, mask=None, repeat=1, lc=1):
         """The part of forward() that does not read the latents: the time / band
-        embedding and, on the fused path, block 1's in-projection and (attend)
+        embedding and, on the fused path, block 1's in-projection and
         its masked self-attention.  lc: context tokens (latent_len)."""
         if self.donotmask:
             mask = None
@@ -58,7 +58,7 @@ class photometricTransformerDecoder(nn.Module):
         x_res, x_qkv, x_out, rep = decoder_inputs(x, repeat, self.transformerblocks, lc)
         first = None
         if x_res.dim() == 3 and decoder_fusable(self.transformerblocks, lc):
-            first = decoder_stack_first(self.transformerblocks, x_res, mask, None, x_qkv, rep, attend)
+            first = decoder_stack_first(self.transformerblocks, x_res, mask, x_qkv, rep)
         return x_res, x_qkv, x_out, rep, first
 
 

@@ -118,14 +118,14 @@ class PhotometricVAE(VAE):
         return None if mask is None else \
             mask.unsqueeze(0).unsqueeze(0).expand(K, groups, B, L).reshape(-1, L)
 
-    def decode_prepare(self, x, K, groups=1, attend=True):
+    def decode_prepare(self, x, K, groups=1):
         """The latent-independent part of decode_params(zs, x, groups) for K samples
-        (embedding, block 1's in-projection and, with attend, its self-attention):
+        (embedding, block 1's in-projection and self-attention):
         -> `prepared` for decode_params."""
         _, time, band, _ = x
         mask = self._dec_mask(x, K, groups)
         return (K, groups, mask, self.dec.generativetransformer.prepare(
-            time, band, mask, repeat=K * groups, lc=self.latent_len, attend=attend))
+            time, band, mask, repeat=K * groups, lc=self.latent_len))
 
     def decode_params(self, zs, x, groups=1, prepared=None):
         """(loc, scale) [K, groups*B, L] for latents zs [K, groups*B, Lz, Dz]

@@ -37,18 +37,17 @@ class spectraTransformerDecoder(nn.Module):
         the embedding MLP runs on the B rows and is broadcast (its gradient is the
         sum over the copies), the rest of the decoder on N.  `prepared`: this call's
         prepare() result, computed ahead (photospecMMVAE.forward: beside the encoders)."""
-        keep = self.__dict__.pop("_keep_prefetch", None)   # util_layers.prefetch_decoder_dropout
         if prepared is None:
-            prepared = self.prepare(wavelength, phase, mask, repeat, bottleneck.shape[1] + 1, keep)
+            prepared = self.prepare(wavelength, phase, mask, repeat, bottleneck.shape[1] + 1)
         x_res, x_qkv, x_out, rep, phase_embd, first = prepared
         bottleneck = torch.cat([self.contextfc(bottleneck), phase_embd], dim=1)
-        h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, keep=keep, x_qkv=x_qkv,
+        h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, x_qkv=x_qkv,
                           rep=rep, first=first)
         return self.get_flux(x_out, h).squeeze(-1)   # get_flux(x + h)
 
-    def prepare(self, wavelength, phase, mask=None, repeat=1, lc=1, keep=None, attend=True):
+    def prepare(self, wavelength, phase, mask=None, repeat=1, lc=1):
         """The part of forward() that does not read the latents: the wavelength and
-        phase embeddings and, on the fused path, block 1's in-projection and (attend)
+        phase embeddings and, on the fused path, block 1's in-projection and
         its masked self-attention (util_layers.decoder_stack_first).  lc: context tokens
         (latent_len + 1)."""
         x = self.wavelength_embd_layer(wavelength)
@@ -57,7 +56,7 @@ class spectraTransformerDecoder(nn.Module):
         x_res, x_qkv, x_out, rep = decoder_inputs(x, repeat, self.transformerblocks, lc)
         first = None
         if x_res.dim() == 3 and decoder_fusable(self.transformerblocks, lc):
-            first = decoder_stack_first(self.transformerblocks, x_res, mask, keep, x_qkv, rep, attend)
+            first = decoder_stack_first(self.transformerblocks, x_res, mask, x_qkv, rep)
         return x_res, x_qkv, x_out, rep, phase_embd, first
 
 

@@ -10,7 +10,7 @@ from torch import nn
 from . import _chain, _ops
 from .SpectraLayers import spectraTransformerDecoder, spectraTransformerEncoder
 from .base_vae import VAE, check_laplace
-from .util_layers import MLP, prefetch_decoder_dropout
+from .util_layers import MLP
 
 
 class SpectraEnc(nn.Module):
@@ -79,9 +79,6 @@ class SpectraVAE(VAE):
 
     def forward(self, x, K=1):
         """SpectraVAE.py:148-165 -> (qz_x, px_z, zs)."""
-        # decoder dropout bitmaps drawn beside the encoder (util_layers.prefetch_decoder_dropout)
-        prefetch_decoder_dropout(self.dec.generativetransformer, K * x[1].shape[0],
-                                 x[1].shape[-1], x[1].device)
         qz_x, zs = self.posterior(x, K)
         px_z = self.decode(zs, x)
         return qz_x, px_z, zs
@@ -125,13 +122,13 @@ class SpectraVAE(VAE):
         return (wavelength, phase.unsqueeze(0).unsqueeze(0).expand(K, groups, B).reshape(-1),
                 None if mask is None else rep(mask))
 
-    def decode_prepare(self, x, K, groups=1, attend=True):
+    def decode_prepare(self, x, K, groups=1):
         """The latent-independent part of decode_params(zs, x, groups) for K samples
-        (embeddings, block 1's in-projection and, with attend, its self-attention):
+        (embeddings, block 1's in-projection and self-attention):
         -> `prepared` for decode_params."""
         wavelength, phase, mask = self._dec_inputs(x, K, groups)
         return (K, groups, mask, self.dec.generativetransformer.prepare(
-            wavelength, phase, mask, repeat=K * groups, lc=self.latent_len + 1, attend=attend))
+            wavelength, phase, mask, repeat=K * groups, lc=self.latent_len + 1))
 
     def decode_params(self, zs, x, groups=1, prepared=None):
         """(loc, scale) [K, groups*B, L] for latents zs [K, groups*B, Lz, Dz]

@@ -21,9 +21,8 @@ def _select_local_gpu():
         return
     import torch
     if torch.cuda.is_available():
-        lr = int(_os.environ["LOCAL_RANK"])
-        if lr < torch.cuda.device_count():
-            torch.cuda.set_device(lr)
+        # more ranks than GPUs (VAESNE_DP_BACKEND=gloo rehearsals): ranks share them
+        torch.cuda.set_device(int(_os.environ["LOCAL_RANK"]) % max(1, torch.cuda.device_count()))
 
 
 _select_local_gpu()

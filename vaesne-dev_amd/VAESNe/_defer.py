@@ -22,10 +22,10 @@ from __future__ import annotations
 
 import contextlib
 import ctypes as C
-import os
 
 import torch
 
+from . import _config
 from ._lib import lib
 
 
@@ -64,9 +64,9 @@ def active() -> bool:
 @contextlib.contextmanager
 def deferred(enabled=None):
     """Defer the parameter-gradient sums of the backward passes run inside
-    (enabled None: on unless VAESNE_DEFER_GRADS=0)."""
+    (enabled None: _config.defer_grads, on unless VAESNE_DEFER_GRADS=0)."""
     if enabled is None:
-        enabled = os.environ.get("VAESNE_DEFER_GRADS", "1") != "0"
+        enabled = _config.defer_grads
     if not enabled:
         yield
         return
@@ -79,6 +79,19 @@ def deferred(enabled=None):
         _S.depth -= 1
         if _S.depth == 0:
             _S.uses.clear()
+            if _S.armed or _S.clist.count or _S.pending:
+                # a backward raised before its final callback (the flush) ran: drop
+                # the queued sums, so the next backward arms a fresh flush and never
+                # touches the freed partial buffers of this one.  The gradients it
+                # had deferred hold no values: the caller's next zero_grad (or the
+                # exception) discards them.
+                _reset()
+
+
+def _reset():
+    _S.clist.count = 0
+    _S.pending, _S.keep, _S.streams = [], [], []
+    _S.armed = False
 
 
 def count_uses(*params):

@@ -105,8 +105,8 @@ SIGNATURES = {
     "vaesne_elbo_bwd": (I32, [P, I32, F32, P, P, P, P, P, P, I32, I32, I32, P, P, P, P, P]),
     "vaesne_infonce_fwd": (I32, [P, P, I32, I32, F32, P, P, P, P, P, P]),
     "vaesne_infonce_bwd": (I32, [P, P, P, I32, I32, F32, P, P, P, P]),
-    "vaesne_adamw": (I32, [P, P, P, P, I64, P, P, F32, F32, F32, F32, F32, P]),
-    "vaesne_adamw_steps_advance": (I32, [P, P, I32, P]),
+    "vaesne_adamw": (I32, [P, P, P, P, I64, P, P, F32, F32, F32, F32, F32, P, P]),
+    "vaesne_adamw_steps_advance": (I32, [P, P, I32, P, P]),
     "vaesne_step_advance": (I32, [P, P, P]),
     "vaesne_pack": (I32, [PP, C.POINTER(I64), C.POINTER(I64), I32, P, I32, P]),
 }

@@ -8,11 +8,10 @@ from __future__ import annotations
 
 import ctypes as C
 import math
-import os
 
 import torch
 
-from . import _defer, _lib, guard, rng
+from . import _config, _defer, _lib, guard, rng
 from ._lib import lib, ptr, stream
 
 ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
@@ -164,6 +163,9 @@ class MlpHeadFn(torch.autograd.Function):
                               ctx.ldx2, M, E, E, dW1.data_ptr(), db1.data_ptr(), 0, ws1.data_ptr(),
                               dfr, s)
         ds = ds.view(ctx.xshape)
+        # d(x + h)/dx = d(x + h)/dh: ONE tensor is both inputs' gradient.  Invariant: its
+        # consumers (FanoutFn's sum into a new buffer, DecTailFn's read) never modify an
+        # incoming gradient in place, so the aliasing is safe without a copy.
         return (ds if ctx.needs_input_grad[0] else None,
                 ds if ctx.needs_input_grad[1] else None, dW1, db1, dW2, db2)
 
@@ -171,7 +173,7 @@ class MlpHeadFn(torch.autograd.Function):
 def mlp_head_ok(x, fc1, fc2):
     return (x.shape[-1] == 32 and fc1.weight.shape == (32, 32) and fc2.weight.shape == (1, 32)
             and fc1.bias is not None and fc2.bias is not None and x.is_cuda
-            and os.environ.get("VAESNE_FUSED_HEAD", "1") != "0")
+            and _config.fused_head)
 
 
 def mlp_head(x, x2, fc1, fc2):
@@ -501,65 +503,37 @@ def used_on(stream, *ts):
             t.record_stream(stream)
 
 
+# bench.py's in-step kernel timing: an object with run(name, work, fn) that brackets
+# fn (one kernel launch) with HIP events on the current stream, or None (the default)
+launch_timer = None
+
+
+def _timed(name, work, fn):
+    t = launch_timer
+    return fn() if t is None else t.run(name, work, fn)
+
+
 def _attn_ws(B, H, Lq, Lk, dh, bwd, dev):
     """Workspace of a chunked (split) attention launch, or None (not needed)."""
     n = lib.attn_workspace(B, H, Lq, Lk, dh, bwd)
     return _ws(n, dev) if n > 0 else None
 
 
-class KeepBits:
-    """The dropout keep bitmap of one query-tiled attention forward (Lq > 16),
-    generated ahead of it (vaesne_attn_keep_bits) on `gen_stream`: it depends on
-    the RNG key and the shape only, so it can be drawn while the inputs are still
-    being computed (the decoders' self-attention bitmaps beside the latency-bound
-    encoders).  The forward then reads the bits instead of hashing them."""
-
-    def __init__(self, B, H, Lq, Lk, p, device, gen_stream=None):
-        self.shape = (int(B), int(H), int(Lq), int(Lk))
-        self.p = float(p)
-        self.st = rng.state(device)
-        self.cid = rng.next_call_id()
-        n = lib.attn_keep_bits_size(B, H, Lq, Lk)
-        self.bits = torch.empty((n + 3) // 4, dtype=torch.int32, device=device)
-        self.event = None
-        if gen_stream is not None:
-            gen_stream.wait_stream(torch.cuda.current_stream())
-            used_on(gen_stream, self.bits, self.st)
-            with torch.cuda.stream(gen_stream):
-                lib.attn_keep_bits(B, H, Lq, Lk, self.p, self.st.data_ptr(), self.cid,
-                                   self.bits.data_ptr(), stream())
-                self.event = torch.cuda.Event()
-                self.event.record(gen_stream)
-        else:
-            lib.attn_keep_bits(B, H, Lq, Lk, self.p, self.st.data_ptr(), self.cid,
-                               self.bits.data_ptr(), stream())
-
-    def take(self, B, H, Lq, Lk, p):
-        """Make the current stream wait for the bits; check they fit this launch."""
-        if self.shape != (B, H, Lq, Lk) or abs(self.p - float(p)) > 0:
-            raise RuntimeError(f"prefetched keep bits are for {self.shape}, p={self.p}; "
-                               f"launch is {(B, H, Lq, Lk)}, p={p}")
-        if self.event is not None:
-            torch.cuda.current_stream().wait_event(self.event)
-        return self.bits, self.st, self.cid
-
-
-def _attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, kbias, B, H, Lq, Lk, dh, p, dev, keep=None):
+def _attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, kbias, B, H, Lq, Lk, dh, p, dev):
     E = H * dh
     o = torch.empty((B, Lq, E), dtype=torch.float32, device=dev)
     lse = torch.empty((B, H, Lq), dtype=torch.float32, device=dev)
     st = rng.state(dev) if p > 0 else None
-    cid = rng.next_call_id() if p > 0 and keep is None else 0
+    cid = rng.next_call_id() if p > 0 else 0
     bits = None
-    if p > 0 and keep is not None:
-        bits, st, cid = keep.take(B, H, Lq, Lk, p)
-    elif p > 0:
+    if p > 0:
         n = lib.attn_keep_bits_size(B, H, Lq, Lk)
         bits = torch.empty((n + 3) // 4, dtype=torch.int32, device=dev)
     ws = _attn_ws(B, H, Lq, Lk, dh, 0, dev)
-    lib.attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, ptr(kbias), Lk, o.data_ptr(), Lq * E, E,
-                 lse.data_ptr(), B, H, Lq, Lk, dh, float(p), ptr(st), cid, ptr(bits),
-                 int(keep is not None and p > 0), ptr(ws), stream())
+    _timed("attn_fwd", B * H * Lq * Lk, lambda: lib.attn_fwd(
+        q, qb, ql, k, kb, kl, v, vb, vl, ptr(kbias), Lk, o.data_ptr(), Lq * E, E,
+        lse.data_ptr(), B, H, Lq, Lk, dh, float(p), ptr(st), cid, ptr(bits), 0, ptr(ws),
+        stream()))
     return o, lse, bits, st, cid
 
 
@@ -567,7 +541,7 @@ class SelfAttnFn(torch.autograd.Function):
     """Packed qkv [B, L, 3E] -> o [B, L, E] (self-attention, additive key bias)."""
 
     @staticmethod
-    def forward(ctx, qkv, kbias, H, p, keep=None):
+    def forward(ctx, qkv, kbias, H, p):
         _lib.require_device(qkv)
         qkv = qkv.contiguous()
         B, L, E3 = qkv.shape
@@ -576,7 +550,7 @@ class SelfAttnFn(torch.autograd.Function):
         base = qkv.data_ptr()
         o, lse, bits, st, cid = _attn_fwd(base, L * E3, E3, base + 4 * E, L * E3, E3,
                                           base + 8 * E, L * E3, E3, kbias, B, H, L, L, dh, p,
-                                          qkv.device, keep)
+                                          qkv.device)
         ctx.dims = (B, L, E, H, dh, float(p), cid)
         ctx.save_for_backward(qkv, kbias, o, lse, bits, st)
         return o
@@ -589,12 +563,13 @@ class SelfAttnFn(torch.autograd.Function):
         E3 = 3 * E
         dqkv = torch.empty_like(qkv)
         b, d = qkv.data_ptr(), dqkv.data_ptr()
-        lib.attn_bwd(b, L * E3, E3, b + 4 * E, L * E3, E3, b + 8 * E, L * E3, E3, ptr(kbias), L,
-                     o.data_ptr(), L * E, E, lse.data_ptr(), do.data_ptr(), L * E, E,
-                     d, L * E3, E3, d + 4 * E, L * E3, E3, d + 8 * E, L * E3, E3,
-                     B, H, L, L, dh, p, ptr(st), cid, ptr(bits),
-                     ptr(_attn_ws(B, H, L, L, dh, 1, qkv.device)), stream())
-        return dqkv, None, None, None, None
+        ws = _attn_ws(B, H, L, L, dh, 1, qkv.device)
+        _timed("attn_bwd", B * H * L * L, lambda: lib.attn_bwd(
+            b, L * E3, E3, b + 4 * E, L * E3, E3, b + 8 * E, L * E3, E3, ptr(kbias), L,
+            o.data_ptr(), L * E, E, lse.data_ptr(), do.data_ptr(), L * E, E,
+            d, L * E3, E3, d + 4 * E, L * E3, E3, d + 8 * E, L * E3, E3,
+            B, H, L, L, dh, p, ptr(st), cid, ptr(bits), ptr(ws), stream()))
+        return dqkv, None, None, None
 
 
 class CrossAttnFn(torch.autograd.Function):
@@ -640,18 +615,25 @@ class SelfAttnRepFn(torch.autograd.Function):
     backward returns the copies' summed d(qkv)."""
 
     @staticmethod
-    def forward(ctx, qkv, kbias, H, p, R, early=None):
+    def forward(ctx, qkv, kbias, H, p, R):
         _lib.require_device(qkv)
         qkv = qkv.contiguous()
         Bd, L, E3 = qkv.shape
         E = E3 // 3
         dh = E // H
-        if early is None:
-            early = RepAttnStart(qkv, kbias, H, p, R)
-        elif early.qkv is not qkv:
-            raise RuntimeError("SelfAttnRepFn: `early` was started for another input")
-        early.launch(early.done, early.nparts)      # the rows not yet computed
-        o, lse, bits, st, cid = early.o, early.lse, early.bits, early.st, early.cid
+        N = R * Bd
+        dev = qkv.device
+        o = torch.empty((N, L, E), dtype=torch.float32, device=dev)
+        lse = torch.empty((Bd, H, L), dtype=torch.float32, device=dev)
+        st = rng.state(dev) if p > 0 else None
+        cid = rng.next_call_id() if p > 0 else 0
+        bits = None
+        if p > 0:
+            n = lib.attn_keep_bits_size(N, H, L, L)
+            bits = torch.empty((n + 3) // 4, dtype=torch.int32, device=dev)
+        lib.attn_rep_fwd(qkv.data_ptr(), L * E3, E3, ptr(kbias), L, o.data_ptr(), L * E, E,
+                         lse.data_ptr(), Bd, R, H, L, dh, float(p), ptr(st), cid, ptr(bits),
+                         stream())
         ctx.dims = (Bd, R, L, E, H, dh, float(p), cid)
         ctx.save_for_backward(qkv, kbias, o, lse, bits, st)
         return o
@@ -667,65 +649,23 @@ class SelfAttnRepFn(torch.autograd.Function):
         lib.attn_rep_bwd(qkv.data_ptr(), L * E3, E3, ptr(kbias), L, o.data_ptr(), L * E, E,
                          lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(), Bd, R, H, L, dh, p,
                          ptr(st), cid, ptr(bits), ptr(ws), stream())
-        return dqkv, None, None, None, None, None
-
-
-class RepAttnStart:
-    """The outputs of one SelfAttnRepFn forward, with query-row parts launched ahead
-    (vaesne_attn_rep_fwd_part): launch(0, k) beside other work, the rest when
-    SelfAttnRepFn runs (it draws no second call id: one call id for all parts)."""
-
-    def __init__(self, qkv, kbias, H, p, R, nparts=1):
-        qkv = qkv.contiguous()
-        self.qkv, self.kbias, self.H, self.p, self.R = qkv, kbias, H, float(p), int(R)
-        Bd, L, E3 = qkv.shape
-        E = E3 // 3
-        N = R * Bd
-        dev = qkv.device
-        self.o = torch.empty((N, L, E), dtype=torch.float32, device=dev)
-        self.lse = torch.empty((Bd, H, L), dtype=torch.float32, device=dev)
-        self.st = rng.state(dev) if p > 0 else None
-        self.cid = rng.next_call_id() if p > 0 else 0
-        self.bits = None
-        if p > 0:
-            n = lib.attn_keep_bits_size(N, H, L, L)
-            self.bits = torch.empty((n + 3) // 4, dtype=torch.int32, device=dev)
-        self.nparts, self.done = int(nparts), 0
-
-    def launch(self, p0, p1):
-        if p1 <= p0:
-            return
-        qkv = self.qkv
-        Bd, L, E3 = qkv.shape
-        E = E3 // 3
-        lib.attn_rep_fwd_part(qkv.data_ptr(), L * E3, E3, ptr(self.kbias), L, self.o.data_ptr(),
-                              L * E, E, self.lse.data_ptr(), Bd, self.R, self.H, L, E // self.H,
-                              self.p, ptr(self.st), self.cid, ptr(self.bits), p0, p1,
-                              self.nparts, stream())
-        self.done = max(self.done, p1)
-
-    def tensors(self):
-        return [t for t in (self.qkv, self.kbias, self.o, self.lse, self.bits, self.st)
-                if t is not None]
+        return dqkv, None, None, None, None
 
 
 def rep_attention_ok(qkv, num_heads, R):
     """Shapes vaesne_attn_rep_* take: head_dim 8, L > 16 (query-tiled), R >= 1."""
     return (qkv.dim() == 3 and qkv.shape[-1] == 3 * 8 * num_heads and qkv.shape[1] > 16
-            and R >= 1 and os.environ.get("VAESNE_REP_ATTN", "1") != "0")
+            and R >= 1 and _config.rep_attn)
 
 
-def self_attention_rep(qkv, kbias, num_heads, p, R, early=None):
-    """kbias: the key bias of the Bd distinct sequences (key_bias of their mask) or None;
-    early: a RepAttnStart for these arguments with some rows already launched."""
-    return SelfAttnRepFn.apply(qkv, kbias, num_heads, float(p), int(R), early)
+def self_attention_rep(qkv, kbias, num_heads, p, R):
+    """kbias: the key bias of the Bd distinct sequences (key_bias of their mask) or None."""
+    return SelfAttnRepFn.apply(qkv, kbias, num_heads, float(p), int(R))
 
 
-def self_attention(qkv, mask, num_heads, p, kbias=None, keep=None):
-    """mask: bool key_padding_mask (True = ignore) or None; kbias: a prebuilt key_bias;
-    keep: a KeepBits prefetched for this launch (dropout only)."""
-    return SelfAttnFn.apply(qkv, _bias_of(mask, kbias), num_heads, float(p),
-                            keep if p > 0 else None)
+def self_attention(qkv, mask, num_heads, p, kbias=None):
+    """mask: bool key_padding_mask (True = ignore) or None; kbias: a prebuilt key_bias."""
+    return SelfAttnFn.apply(qkv, _bias_of(mask, kbias), num_heads, float(p))
 
 
 def cross_attention(q, kv, mask, num_heads, p, kbias=None):

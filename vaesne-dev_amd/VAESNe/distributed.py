@@ -49,17 +49,35 @@ def init_from_env():
     the cannon scripts never call init_process_group (training_util.py:17-53 has
     no distributed code), so `torchrun --nproc-per-node N script.py` with the
     script unchanged reaches here from training_step.  Backend "nccl" (RCCL over
-    xGMI) when the ranks drive GPUs, "gloo" otherwise.  Returns (rank, world)."""
+    xGMI) when the ranks drive GPUs, "gloo" otherwise; VAESNE_DP_BACKEND overrides
+    it (gloo lets several ranks share one GPU, which RCCL refuses).  Rank r drives
+    GPU LOCAL_RANK mod the visible device count.  Returns (rank, world)."""
     if not dist.is_available() or dist.is_initialized():
         return world()
     rank, ws = env_world()
     if ws <= 1:
         return 0, 1
-    backend = "nccl" if torch.cuda.is_available() else "gloo"
-    if backend == "nccl":
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0") or 0))
+    backend = dp_backend()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_device_index())
     dist.init_process_group(backend)
     return world()
+
+
+def local_device_index():
+    """The GPU this rank drives: LOCAL_RANK mod the visible device count."""
+    n = max(1, torch.cuda.device_count())
+    return int(os.environ.get("LOCAL_RANK", "0") or 0) % n
+
+
+def dp_backend():
+    """VAESNE_DP_BACKEND if set, else "nccl" (RCCL) with GPUs and "gloo" without."""
+    b = os.environ.get("VAESNE_DP_BACKEND", "").strip().lower()
+    if b:
+        if b not in ("nccl", "gloo"):
+            raise ValueError(f"VAESNE_DP_BACKEND={b!r}: expected nccl or gloo")
+        return b
+    return "nccl" if torch.cuda.is_available() else "gloo"
 
 
 def split_bounds(B, rank=None, world_size=None):
@@ -132,6 +150,24 @@ class GradAllReduce:
         if self.reduction == "mean":
             flat_grad.mul_(self.weight if self.weight is not None else 1.0 / ws)
         dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=self.group)
+
+
+def agree_grad_pattern(params):
+    """Make every rank hold a gradient for the same parameters before the gradient
+    all-reduce: one MAX all-reduce of a has-gradient mask; a parameter some rank has
+    a gradient for and this rank does not (an empty batch slice, or a branch the
+    loss does not reach here) gets a zero gradient.  Keeps the all-reduce sizes and
+    FusedAdamW's per-parameter step counts identical on every rank."""
+    ws = world()[1]
+    params = list(params)
+    if ws == 1 or not params:
+        return
+    dev = params[0].device
+    mask = torch.tensor([p.grad is not None for p in params], dtype=torch.int32, device=dev)
+    dist.all_reduce(mask, op=dist.ReduceOp.MAX)
+    for p, m in zip(params, mask.tolist()):
+        if m and p.grad is None:
+            p.grad = torch.zeros_like(p)
 
 
 def allreduce_grads(params, reduction="sum", weight=None):

@@ -50,10 +50,9 @@ def _elbo_host(model, x, K, qz_x, px_z, debug=False):
     kld = torch.distributions.kl_divergence(qz_x, model.pz(*model.pz_params))
     if debug:
         print(f"kl: {kld.sum((-1, -2)).mean()}, llk: {-lpx.sum(-1).mean()}")
-    loss = (lpx.sum(-1) - kld.sum((-1, -2))[None, :]).mean()
-    if not torch.isfinite(loss):
-        raise RuntimeError("elbo: non-finite loss")
-    return loss
+    # a non-finite value is returned as the reference does; training_step raises on
+    # it on every rank together (a raise here would be rank-local)
+    return (lpx.sum(-1) - kld.sum((-1, -2))[None, :]).mean()
 
 
 def _m_iwae(model, x, K=1):

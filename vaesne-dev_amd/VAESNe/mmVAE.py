@@ -1,42 +1,25 @@
 """Mixture-of-experts multimodal VAE over (light curve, spectrum) pairs,
 MI355X build (reference: mmVAE.py:71-132, photospecMMVAE)."""
 import contextlib
-import os
 
 import torch
 import torch.distributions as dist
 import torch.nn as nn
 
-from . import _chain, _ops
-from .util_layers import prefetch_decoder_dropout
+from . import _config, _ops
 
 
 _SIDE = {}
 
 
 def _side_stream(t):
-    """A second HIP stream for the photometry branch (VAESNE_STREAMS=0 turns it off)."""
-    if not t.is_cuda or os.environ.get("VAESNE_STREAMS", "1") == "0":
+    """A second HIP stream for the photometry branch (_config.streams off: none)."""
+    if not t.is_cuda or not _config.streams:
         return None
     dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
     st = _SIDE.get(dev)
     if st is None:
         st = _SIDE[dev] = torch.cuda.Stream(device=dev)
-    return st
-
-
-_PREP = {}
-
-
-def _prep_stream(t):
-    """The stream the decoders' latent-independent first parts run on, beside the
-    encoders (VAESNE_STREAMS=0: none, they run first on the current stream)."""
-    if not t.is_cuda or os.environ.get("VAESNE_STREAMS", "1") == "0":
-        return None
-    dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
-    st = _PREP.get(dev)
-    if st is None:
-        st = _PREP[dev] = torch.cuda.Stream(device=dev)
     return st
 
 
@@ -130,86 +113,35 @@ class photospecMMVAE(nn.Module):
         side = _side_stream(x[0][0]) if n == 2 else None
         merged = all((v.latent_len, v.latent_dim) == (self.vaes[0].latent_len,
                                                        self.vaes[0].latent_dim) for v in self.vaes)
-        if merged:
-            # the decoders' dropout bitmaps only depend on the RNG key: draw them now,
-            # beside the latency-bound encoders (util_layers.prefetch_decoder_dropout)
-            B = x[0][0].shape[0]
-            for d, vae in enumerate(self.vaes):
-                prefetch_decoder_dropout(vae.dec.generativetransformer, K * n * B,
-                                         x[d][1].shape[-1], x[d][1].device)
-        # The decoders' input embeddings and first in-projections read only the decoder
-        # input grids (util_layers.decoder_stack_first), not the latents: they run on
-        # their own stream beside the latency-bound encoders
-        # The decoders' input embeddings and first in-projections (and, mode 2 / 4,
-        # block 1's self-attention) read only the decoder input grids
-        # (util_layers.decoder_stack_first), not the latents.  VAESNE_DEC_PREPARE
-        # (A/B, ms per step at cfg 5): 0 = in the decoders (10.15); 1 / 2 = on a
-        # stream of their own beside the encoders (10.60 / 10.49: one more graph
-        # branch costs more than the overlap gains); 3 / 4 (default) = on the
-        # photometry stream after its (shorter) encoder, beside the spectra encoder
-        # (10.05 / 9.79); 5 = 4 with the spectra decoder's part issued first; 6
-        # (default) = 4 with the parts issued BEFORE the photometry encoder: autograd
-        # runs the later-created of two ready nodes first, so the photometry encoder's
-        # backward then goes ahead of the block-1 attention backwards on that stream
-        # instead of queueing behind them (A/B 9.51 / 9.50 -> 9.43 / 9.48).
-        mode = os.environ.get("VAESNE_DEC_PREPARE", "6")
-        preps, prep_ev = [None] * n, None
-        prep_ok = merged and mode != "0" and \
-            all(hasattr(v, "decode_prepare") for v in self.vaes) and \
-            not any("_keep_prefetch" in v.dec.generativetransformer.__dict__ for v in self.vaes)
-        attend = mode in ("2", "4", "5", "6")
-
-        def prepare_all():
-            order = range(n - 1, -1, -1) if mode == "5" else range(n)
-            for d in order:
-                preps[d] = self.vaes[d].decode_prepare(x[d], K, groups=n, attend=attend)
-
-        if prep_ok and mode in ("1", "2"):
-            ps = _prep_stream(x[0][0])
-            if ps is not None:
-                ps.wait_stream(torch.cuda.current_stream())
-                _ops.used_on(ps, *[t for xd in x for t in xd if isinstance(t, torch.Tensor)])
-            with torch.cuda.stream(ps) if ps is not None else contextlib.nullcontext():
-                prepare_all()
-                if ps is not None:
-                    prep_ev = torch.cuda.Event()
-                    prep_ev.record(ps)
+        # The decoders' input embeddings, first in-projections and block-1 self-attention
+        # read only the decoder input grids (util_layers.decoder_stack_first), not the
+        # latents: they are issued on the photometry stream BEFORE the photometry encoder,
+        # so they run beside the latency-bound spectra encoder (A/B 9.96 -> 9.61 ms per
+        # step), and autograd (which runs the later-created of two ready nodes first)
+        # issues the photometry encoder's backward ahead of the block-1 attention
+        # backwards on that stream (A/B 9.51 -> 9.43 ms).  Without a side stream they
+        # run first on the current stream.
+        preps = [None] * n
+        prep_ok = merged and all(hasattr(v, "decode_prepare") for v in self.vaes)
         qz_xs, zss = [None] * n, [None] * n
-        if os.environ.get("VAESNE_ENC_GROUP", "0") == "1" and \
-                all(hasattr(v, "posterior_steps") for v in self.vaes):
-            # both encoders on this stream, their fused latent chains in ONE launch
-            # (a captured graph runs side-stream branches one after the other anyway)
-            res = _chain.drive([vae.posterior_steps(x[m], K=K) for m, vae in enumerate(self.vaes)])
-            for m in range(n):
-                qz_xs[m], zss[m] = res[m]
-        else:
-            with _Branches(side) as br:
-                br.to_side(*x[0])
-                for m, vae in enumerate(self.vaes):
-                    with br.on(m):
-                        if m == 0 and prep_ok and mode == "6":
-                            br.to_side(*x[1])
-                            prepare_all()
-                        qz_xs[m], zss[m] = vae.posterior(x[m], K=K)
-                        if m == 0 and prep_ok and mode in ("3", "4", "5"):
-                            br.to_side(*x[1])
-                            prepare_all()
-                br.to_main(qz_xs[0].loc, qz_xs[0].scale, zss[0], *_tensors(preps))
+        with _Branches(side) as br:
+            br.to_side(*x[0])
+            for m, vae in enumerate(self.vaes):
+                with br.on(m):
+                    if m == 0 and prep_ok:
+                        br.to_side(*x[1])
+                        for d in range(n):
+                            preps[d] = self.vaes[d].decode_prepare(x[d], K, groups=n)
+                    qz_xs[m], zss[m] = vae.posterior(x[m], K=K)
+            br.to_main(qz_xs[0].loc, qz_xs[0].scale, zss[0], *_tensors(preps))
         px_zs = _CellMatrix([[None for _ in range(n)] for _ in range(n)])
         if all(z.shape == zss[0].shape for z in zss):
             B = zss[0].shape[1]
             zcat = torch.cat(zss, dim=1)
             px_zs.merged = [None] * n
-            order = list(range(n))
-            if os.environ.get("VAESNE_DEC_ORDER", "") == "rev":
-                order.reverse()       # the long spectra decoder issued first
-            if prep_ev is not None:
-                main = torch.cuda.current_stream()
-                main.wait_event(prep_ev)
-                _ops.used_on(main, *_tensors(preps))
             with _Branches(side) as br:
                 br.to_side(zcat, *_tensors(preps))
-                for d in order:
+                for d in range(n):
                     vae = self.vaes[d]
                     with br.on(d):
                         px_zs.merged[d] = vae.decode_params(zcat, x[d], groups=n,

@@ -10,7 +10,12 @@ flat fp32 parameter buffer on the device.
 * As in torch.optim.AdamW, every parameter has its own step count, advanced only
   when it has a gradient, and parameters whose .grad is None are skipped.
 * state_dict() / load_state_dict() use torch.optim.AdamW's format (per-parameter
-  "step", "exp_avg", "exp_avg_sq"), so checkpoints move between the two.
+  "step", "exp_avg", "exp_avg_sq"), so checkpoints move between the two.  Only
+  lr / betas / eps / weight_decay are taken from a loaded group; a group saved with
+  amsgrad or maximize set is refused (the kernel implements neither).
+* Non-finite guard: the update kernels read the device flag of VAESNe.guard and
+  apply nothing (parameters, moments and step counts unchanged) when the step's
+  forward flagged a NaN posterior or a non-finite loss; training_step raises on it.
 """
 from __future__ import annotations
 
@@ -18,7 +23,7 @@ import ctypes as C
 
 import torch
 
-from . import _lib
+from . import _lib, guard
 from ._lib import lib, stream
 
 
@@ -97,15 +102,16 @@ class FusedAdamW(torch.optim.Optimizer):
             if fl is None:
                 continue
             b1, b2 = group["betas"]
+            skip = guard.ptr(fl["flat"])
             lib.adamw_steps_advance(fl["steps"].data_ptr(), self._active(fl), len(fl["params"]),
-                                    stream())
+                                    skip, stream())
             runs = self._runs(fl)
             for o, n in runs:
                 lib.adamw(fl["flat"].data_ptr() + 4 * o, fl["grad"].data_ptr() + 4 * o,
                           fl["m"].data_ptr() + 4 * o, fl["v"].data_ptr() + 4 * o, n,
                           fl["steps"].data_ptr(), fl["pidx"].data_ptr() + 4 * o,
                           float(group["lr"]), float(b1), float(b2),
-                          float(group["eps"]), float(group["weight_decay"]), stream())
+                          float(group["eps"]), float(group["weight_decay"]), skip, stream())
 
     @staticmethod
     def _active(fl):
@@ -150,9 +156,13 @@ class FusedAdamW(torch.optim.Optimizer):
             if len(saved["params"]) != len(group["params"]):
                 raise ValueError("loaded state dict contains a parameter group that doesn't "
                                  "match the size of optimizer's group")
-            for k, v in saved.items():
-                if k != "params":
-                    group[k] = v
+            for k in ("amsgrad", "maximize"):
+                if saved.get(k, False):
+                    raise ValueError(f"FusedAdamW: the loaded optimizer state has {k}=True, "
+                                     "which the fused AdamW kernel does not implement")
+            for k in ("lr", "betas", "eps", "weight_decay"):
+                if k in saved:
+                    group[k] = tuple(saved[k]) if k == "betas" else saved[k]
             if fl is None:
                 continue
             where = {id(p): j for j, p in enumerate(fl["params"])}

@@ -10,14 +10,20 @@ gradients are all-reduced once per step (VAESNe.distributed): SUM for
 sum-over-batch objectives (m_iwae, the multimodal default) and, for mean
 objectives (elbo, the single-modality default), each rank's gradient weighted by
 its share of the batch before the SUM.  A rank whose slice is empty (B < world)
-joins the all-reduce with a zero gradient for every trainable parameter, so all
-ranks apply the same update.  Each rank draws its own noise / dropout streams
+joins the all-reduce with zero gradients, and every rank holds a gradient for the
+same parameters (distributed.agree_grad_pattern), so all ranks apply the same update.  Each rank draws its own noise / dropout streams
 (rng.rank_seed).  The returned value is the mean full-batch loss on every rank.
 
-Non-finite values: the HIP kernels flag a NaN / Inf posterior or loss on the
-device (VAESNe.guard); it is read after the `.item()` the loop already does
-(training_util.py:46) and raises RuntimeError where the reference would stop in
-pdb (PhotometricVAE.py:160-161)."""
+Non-finite values (VAESNe.guard): the HIP kernels flag a NaN posterior or a
+NaN / Inf loss on the device.  The flag is cleared before each batch's forward
+and read, with the loss, at ONE sync placed before `optimizer.step()` (the
+reference's `.item()`, training_util.py:46, moves ahead of the update): under data
+parallelism the loss and both flag words travel in one all-reduce, so every rank
+sees the same verdict and all raise RuntimeError together (a rank-local raise
+would leave the others blocked in the next all-reduce).  The update is never
+applied for a flagged batch, as the reference stops before its update
+(PhotometricVAE.py:160-161).  A non-finite loss also raises (stricter than the
+reference, which would train on it)."""
 import math
 
 import torch
@@ -41,10 +47,12 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
     device = next(network.parameters()).device
     rank, ws = D.init_from_env()
     reduction = grad_reduction or ("sum" if multimodal else "mean")
+    fused = isinstance(optimizer, FusedAdamW)
     if ws > 1:
         D.sync_parameters_once(network)
-        if isinstance(optimizer, FusedAdamW) and optimizer.grad_hook is None:
+        if fused and optimizer.grad_hook is None:
             optimizer.grad_hook = D.GradAllReduce(reduction)
+    params = [p for p in network.parameters() if p.requires_grad]
     for x in data_loader:
         optimizer.zero_grad()
         if multimodal:
@@ -58,27 +66,43 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
             lo, hi = D.split_bounds(B, rank, ws)
             empty = hi == lo
             w = (hi - lo) / B if reduction == "mean" else 1.0
-            if isinstance(optimizer, FusedAdamW) and isinstance(optimizer.grad_hook, D.GradAllReduce):
+            if fused and isinstance(optimizer.grad_hook, D.GradAllReduce):
                 optimizer.grad_hook.weight = w if reduction == "mean" else None
             x = D.shard(x, rank, ws)
+        guard.reset(device)       # a flag left by an unchecked eval call is not this batch's
         if empty:
             loss = torch.zeros((), dtype=torch.float32, device=device)
-            for p in network.parameters():
-                if p.requires_grad:
-                    p.grad = torch.zeros_like(p)
         else:
             # parameter-gradient sums batched into one launch at the end of backward
             with _defer.deferred():
                 loss = -loss_fn(network, x)
                 loss.backward()
-        if ws > 1 and not isinstance(optimizer, FusedAdamW):
-            D.allreduce_grads(network.parameters(), reduction, weight=w)
-        optimizer.step()
         if ws > 1:
-            loss = loss.detach().clone() * w
-            torch.distributed.all_reduce(loss)
-        total_loss += loss.detach().cpu().item()
-        guard.check(device, "training_step")
+            # every rank all-reduces the same set of gradients (an empty slice, or a
+            # parameter the loss does not reach on some rank, gets zeros)
+            D.agree_grad_pattern(params)
+            if fused:
+                optimizer.pack_grads()
+                optimizer.reduce_grads()
+            else:
+                D.allreduce_grads(params, reduction, weight=w)
+        # the one sync per batch, before the update: loss and the guard words
+        stat = torch.cat([(loss.detach().float() * w).reshape(1), guard.words(device)])
+        if ws > 1:
+            torch.distributed.all_reduce(stat)
+        loss_v, post_bad, loss_bad = stat.tolist()
+        if post_bad or loss_bad or not math.isfinite(loss_v):
+            if ws > 1:
+                # every rank reached the same verdict: leave together, so no rank tears the
+                # group down while another still completes the all-reduce above
+                torch.distributed.barrier()
+            guard.raise_for(device, (post_bad > 0, loss_bad > 0 or not math.isfinite(loss_v)),
+                            "training_step")
+        if fused and ws > 1:
+            optimizer.apply_update()       # gradients already packed and all-reduced
+        else:
+            optimizer.step()
+        total_loss += loss_v
         num_batches += 1.
         if release_memory:
             del x

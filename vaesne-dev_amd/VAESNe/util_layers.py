@@ -17,12 +17,11 @@ from __future__ import annotations
 
 import contextlib
 import math
-import os
 
 import torch
 from torch import nn
 
-from . import _chain, _ops
+from . import _chain, _config, _ops
 
 
 class Linear(nn.Linear):
@@ -199,46 +198,6 @@ def _fusable_decoder_block(blk):
             and all(ln.eps == 1e-5 for ln in (blk.layernorm1, blk.layernorm2, blk.layernorm3)))
 
 
-_GEN_STREAMS = {}
-
-
-def _gen_stream(dev):
-    """Side stream the decoders' dropout bitmaps are drawn on (VAESNE_STREAMS=0: none)."""
-    if os.environ.get("VAESNE_STREAMS", "1") == "0":
-        return None
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    st = _GEN_STREAMS.get(idx)
-    if st is None:
-        st = _GEN_STREAMS[idx] = torch.cuda.Stream(device=idx)
-    return st
-
-
-def prefetch_decoder_dropout(decoder, N, L, device):
-    """Draw, ahead of the decoder's forward, the keep bitmaps of its blocks' masked
-    self-attention dropout (N sequences x L tokens) on a side stream, and hand them
-    to the decoder's next forward.  The bitmaps depend on the RNG key only, so at the
-    start of a step they can be drawn while the latency-bound encoders leave the chip
-    mostly idle, and the attention forwards read them instead of hashing (their
-    dropout VALU work falls by ~85 %, 27 % of the forward's VALU instructions).
-    OFF by default (VAESNE_PREFETCH_DROPOUT=1 enables it): measured on MI355X the
-    forward held the same time (0.63 ms: it runs power-limited, and with fewer VALU
-    instructions the chip clocks lower, 2.08 vs 2.28 GHz), while the generator's
-    0.19 ms per layer delayed the encoders, 12.8 vs 12.5 ms per step (profiles/r02_prefetch).
-    No-op outside training, without dropout, or for short sequences (L < 128)."""
-    blocks = list(getattr(decoder, "transformerblocks", []))
-    if (not blocks or not decoder.training or L < 128 or not device.type == "cuda"
-            or os.environ.get("VAESNE_PREFETCH_DROPOUT", "0") != "1"
-            or not all(_fusable_decoder_block(b) for b in blocks)):
-        return
-    gs = _gen_stream(device)
-    keep = []
-    for blk in blocks:
-        p = blk.self_attn.dropout
-        keep.append(_ops.KeepBits(N, blk.self_attn.num_heads, L, L, p, device, gs)
-                    if p > 0 else None)
-    decoder._keep_prefetch = keep
-
-
 def decoder_fusable(blocks, context):
     """Whether decoder_stack runs these blocks as fused kernels (else per op).
     `context`: the context tensor [N, Lc, E], or its token count Lc."""
@@ -271,83 +230,42 @@ def decoder_inputs(xd, repeat, blocks, context):
 
 class DecoderFirst:
     """What a fused decoder stack computes before it needs the context: block 1's
-    in-projection (and, with attend, its masked self-attention) read only the
-    decoder input (the embedding of the wavelength / time grid,
-    SpectraLayers.py:54-62, PhotometricLayers.py:59-67), not the latents, so they
-    can run while the encoders still work (photospecMMVAE.forward issues them on
-    their own stream)."""
-    __slots__ = ("N", "L", "kbias", "qkv", "rep", "O1", "keep", "early")
+    in-projection and masked self-attention read only the decoder input (the
+    embedding of the wavelength / time grid, SpectraLayers.py:54-62,
+    PhotometricLayers.py:59-67), not the latents, so they run while the encoders
+    still work (photospecMMVAE.forward issues them on the photometry stream)."""
+    __slots__ = ("N", "L", "kbias", "O1")
 
-    def __init__(self, N, L, kbias, qkv, rep, O1, keep):
-        self.N, self.L, self.kbias, self.qkv, self.rep = N, L, kbias, qkv, rep
-        self.O1, self.keep, self.early = O1, keep, None
+    def __init__(self, N, L, kbias, O1):
+        self.N, self.L, self.kbias, self.O1 = N, L, kbias, O1
 
     def tensors(self):
-        ts = [t for t in (self.kbias, self.qkv, self.O1) if t is not None]
-        return ts + (self.early.tensors() if self.early is not None else [])
-
-    def start(self, blocks, k, n):
-        """Launch query parts [0, k) of n of block 1's repeated-sequence self-attention
-        now; attend() launches the rest (one call id for all parts)."""
-        if self.O1 is not None or self.rep <= 1 or self.early is not None:
-            return
-        b0 = blocks[0].self_attn
-        p_attn = b0.dropout if blocks[0].training else 0.0
-        Bd = self.N // self.rep
-        self.early = _ops.RepAttnStart(self.qkv, None if self.kbias is None else self.kbias[:Bd],
-                                       b0.num_heads, p_attn, self.rep, nparts=n)
-        self.early.launch(0, k)
-
-    def attend(self, blocks):
-        """Block 1's masked self-attention (once)."""
-        if self.O1 is None:
-            b0 = blocks[0].self_attn
-            p_attn = b0.dropout if blocks[0].training else 0.0
-            if self.rep > 1:
-                Bd = self.N // self.rep
-                self.O1 = _ops.self_attention_rep(self.qkv, None if self.kbias is None
-                                                  else self.kbias[:Bd], b0.num_heads, p_attn,
-                                                  self.rep, self.early)
-                self.early = None
-            else:
-                self.O1 = _ops.self_attention(self.qkv, None, b0.num_heads, p_attn,
-                                              kbias=self.kbias,
-                                              keep=None if self.keep is None else self.keep[0])
-            self.qkv = None
-        return self.O1
+        return [t for t in (self.kbias, self.O1) if t is not None]
 
 
-def decoder_stack_first(blocks, x, mask=None, keep=None, x_qkv=None, rep=1, attend=True):
-    """Block 1's in-projection and (attend) self-attention of a fused decoder stack
+def decoder_stack_first(blocks, x, mask=None, x_qkv=None, rep=1):
+    """Block 1's in-projection and masked self-attention of a fused decoder stack
     (see decoder_stack): -> DecoderFirst."""
     blocks = list(blocks)
     E = 32
     L = x.shape[1]
     N = x.shape[0]
     b0 = blocks[0].self_attn
+    p_attn = b0.dropout if blocks[0].training else 0.0
     qkv = _ops.linear(x if x_qkv is None else x_qkv, b0.in_proj_weight, b0.in_proj_bias)
     kbias = _ops.key_bias(mask)          # one mask conversion for all layers
-    if keep is not None and (len(keep) != len(blocks) or any(
-            k is not None and k.shape != (N, blk.self_attn.num_heads, L, L)
-            for k, blk in zip(keep, blocks))):
-        keep = None      # prefetched for another shape: draw in the kernels
-    rep_attn = rep > 1 and (keep is None or keep[0] is None) and \
-        _ops.rep_attention_ok(qkv, b0.num_heads, rep)
-    if rep > 1 and not rep_attn:
-        qkv = _ops.repeat_batch(qkv, rep).reshape(N, L, 3 * E)
-    first = DecoderFirst(N, L, kbias, qkv, rep if rep_attn else 1, None, keep)
-    if attend:
-        # VAESNE_REP_EARLY="k/n": only query parts [0, k) of n now, the rest in
-        # decoder_stack (A/B tuning of how much of it overlaps the encoders)
-        k, n = (int(v) for v in os.environ.get("VAESNE_REP_EARLY", "1/1").split("/"))
-        if rep_attn and 0 < k < n:
-            first.start(blocks, k, n)
-        else:
-            first.attend(blocks)
-    return first
+    if rep > 1 and _ops.rep_attention_ok(qkv, b0.num_heads, rep):
+        Bd = N // rep
+        O1 = _ops.self_attention_rep(qkv, None if kbias is None else kbias[:Bd], b0.num_heads,
+                                     p_attn, rep)
+    else:
+        if rep > 1:
+            qkv = _ops.repeat_batch(qkv, rep).reshape(N, L, 3 * E)
+        O1 = _ops.self_attention(qkv, None, b0.num_heads, p_attn, kbias=kbias)
+    return DecoderFirst(N, L, kbias, O1)
 
 
-def decoder_stack(blocks, x, context, mask=None, keep=None, x_qkv=None, rep=1, first=None):
+def decoder_stack(blocks, x, context, mask=None, x_qkv=None, rep=1, first=None):
     """`for blk in blocks: x = blk(x, context, mask=mask)` for the decoders
     (SpectraLayers.py:61-62, PhotometricLayers.py:66-67).  With the reference's
     decoder shape (E 32, 4 heads, ff 32, no context self-attention) each block
@@ -370,10 +288,10 @@ def decoder_stack(blocks, x, context, mask=None, keep=None, x_qkv=None, rep=1, f
             x = blk(x, context, mask=mask)
         return x
     if first is None:
-        first = decoder_stack_first(blocks, x, mask, keep, x_qkv, rep)
+        first = decoder_stack_first(blocks, x, mask, x_qkv, rep)
     elif first.N != x.shape[0] or first.L != x.shape[1]:
         raise RuntimeError("decoder_stack: `first` was computed for another input")
-    L, kbias, keep = first.L, first.kbias, first.keep
+    L, kbias = first.L, first.kbias
     # every block's cross-attention reads the context: one gradient sum for all
     ctxs = _ops.fanout(context, len(blocks))
     qkv = None
@@ -381,10 +299,9 @@ def decoder_stack(blocks, x, context, mask=None, keep=None, x_qkv=None, rep=1, f
         p_attn = blk.self_attn.dropout if blk.training else 0.0
         p = blk.dropout.p if blk.training else 0.0
         if i == 0:
-            O = first.attend(blocks)
+            O = first.O1
         else:
-            O = _ops.self_attention(qkv, None, blk.self_attn.num_heads, p_attn, kbias=kbias,
-                                    keep=None if keep is None else keep[i])
+            O = _ops.self_attention(qkv, None, blk.self_attn.num_heads, p_attn, kbias=kbias)
         nxt = blocks[i + 1].self_attn if i + 1 < len(blocks) else None
         x, qkv = _ops.DecTailFn.apply(
             L, p, x, O, ctxs[i], blk.cross_attn.in_proj_weight, blk.cross_attn.in_proj_bias,
@@ -405,11 +322,11 @@ def _ctx_stream(t, i=0):
     """The stream block i's context self-attention path runs on: VAESNE_CTX_STREAMS
     streams (default 2: A/B 12.43 vs 12.60 ms per step with 1, 12.59 with 4) shared
     round-robin, so in the backward (issued last) the paths run two at a time
-    (VAESNE_STREAMS=0 turns the extra streams off)."""
-    if not t.is_cuda or os.environ.get("VAESNE_STREAMS", "1") == "0":
+    (_config.streams off: none)."""
+    if not t.is_cuda or not _config.streams:
         return None
     dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
-    i %= max(1, int(os.environ.get("VAESNE_CTX_STREAMS", "2")))
+    i %= _config.ctx_streams
     st = _CTX_STREAMS.setdefault(dev, {})
     if i not in st:
         st[i] = torch.cuda.Stream(device=dev)
@@ -463,7 +380,7 @@ def _context_paths(blocks, context, context_mask):
 
 
 def _mergeable_context_paths(blocks, context):
-    if len(blocks) < 2 or os.environ.get("VAESNE_CTX_MERGE", "1") == "0":
+    if len(blocks) < 2 or not _config.ctx_merge:
         return False
     m0 = blocks[0].context_self_attn
     if m0 is None or context.dim() != 3:
@@ -519,7 +436,7 @@ def encoder_stack(blocks, x, context, context_mask=None, x_qkv=None):
     encoders (SpectraLayers.py:135-136, PhotometricLayers.py:141-143: unmasked
     latent tokens x, the ORIGINAL data tokens as every block's context).  With the
     reference's shape the latent side of all blocks is ONE fused chain launch
-    (VAESNe._chain; VAESNE_ENC_CHAIN=0 selects the per-block path: latent
+    (VAESNe._chain; _config.enc_chain off selects the per-block path: latent
     self-attention core -> PRE (out_proj, LN1, cross q) + context k|v projection ->
     cross-attention core -> POST (out_proj, LN2, FFN, LN3, next in_proj)).  The
     optional context self-attention (spectra `selfattn`) runs ahead of the latent
@@ -538,7 +455,7 @@ def encoder_stack_steps(blocks, x, context, context_mask=None, x_qkv=None):
         for blk in blocks:
             x = blk(x, context, context_mask=context_mask)
         return x
-    chain = _chain.fusable(blocks, x) and os.environ.get("VAESNE_ENC_CHAIN", "1") != "0"
+    chain = _chain.fusable(blocks, x) and _config.enc_chain
     if chain and not any(b.context_self_attn is not None for b in blocks):
         # every block reads the original context: one input, its gradient summed in the op
         spec = _chain.make_spec(blocks, context_mask, shared=True)

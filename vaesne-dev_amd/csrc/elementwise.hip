@@ -88,8 +88,10 @@ __global__ __launch_bounds__(NT) void embed_bwd_kernel(const int64_t* __restrict
   }
 }
 
-// bottleneck [B, 2*Lz, Dz] -> mu [B, Lz*Dz], scale [B, Lz*Dz].  A non-finite mu or
-// scale sets nonfinite[0] = 1 (the reference stops there: PhotometricVAE.py:160-161).
+// bottleneck [B, 2*Lz, Dz] -> mu [B, Lz*Dz], scale [B, Lz*Dz].  A NaN mu or scale sets
+// nonfinite[0] = 1: the reference stops there (PhotometricVAE.py:160-161 tests isnan
+// only; an Inf posterior goes on and is caught by the loss flag if it makes the loss
+// non-finite).
 __global__ void latent_head_fwd_kernel(const float* __restrict__ bott, int B, int n,
                                        float* __restrict__ mu, float* __restrict__ scale,
                                        int* __restrict__ nonfinite) {
@@ -102,7 +104,7 @@ __global__ void latent_head_fwd_kernel(const float* __restrict__ bott, int B, in
   float x = bott[b * 2 * n + n + j];
   const float sc = x > 20.f ? x : log1pf(expf(x));
   scale[t] = sc;
-  if (nonfinite && !(isfinite(m) && isfinite(sc))) nonfinite[0] = 1;
+  if (nonfinite && (isnan(m) || isnan(sc))) nonfinite[0] = 1;
 }
 
 __global__ void latent_head_bwd_kernel(const float* __restrict__ bott, int B, int n,
@@ -175,11 +177,16 @@ __global__ void mask_scale_kernel(const uint8_t* __restrict__ mask, int64_t n, i
 // torch.optim.AdamW single-tensor arithmetic (torch/optim/adamw.py ->
 // adam.py _single_tensor_adam with decoupled decay): step counter on device.
 // pidx (nullable): element t belongs to parameter pidx[t], whose step count is
-// step[pidx[t]] (torch.optim.AdamW keeps one step per parameter); else one step
+// step[pidx[t]] (torch.optim.AdamW keeps one step per parameter); else one step.
+// skip (nullable): the non-finite guard flag int32[2] (VAESNe/guard.py); when either
+// word is set the update is not applied (a NaN / Inf posterior or loss never reaches
+// the parameters, as the reference stops before its update, PhotometricVAE.py:160-161)
 __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                              float* __restrict__ m, float* __restrict__ v, int64_t n,
                              const float* __restrict__ step, const int32_t* __restrict__ pidx,
-                             float lr, float b1, float b2, float eps, float wd) {
+                             float lr, float b1, float b2, float eps, float wd,
+                             const int32_t* __restrict__ skip) {
+  if (skip && (skip[0] | skip[1])) return;
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float st = pidx ? -1.f : step[0];
   float step_size = 0.f, bc2s = 0.f;
@@ -269,7 +276,8 @@ __global__ __launch_bounds__(64 * SHIFT_ROWS) void bright_shift_bwd_kernel(
 }
 
 __global__ void steps_advance_kernel(float* __restrict__ steps, const uint8_t* __restrict__ active,
-                                     int P) {
+                                     int P, const int32_t* __restrict__ skip) {
+  if (skip && (skip[0] | skip[1])) return;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < P && (!active || active[i])) steps[i] += 1.f;
 }
@@ -501,19 +509,19 @@ VAESNE_API int vaesne_bright_shift_bwd(const float* g, int64_t R, int L, float* 
 
 VAESNE_API int vaesne_adamw(float* p, const float* g, float* m, float* v, int64_t n,
                             const float* step, const int32_t* pidx, float lr, float b1, float b2,
-                            float eps, float wd, void* stream) {
+                            float eps, float wd, const int32_t* skip, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(adamw_kernel, dim3(blocks_for(n, NT, 4096)), dim3(NT), 0,
-                     (hipStream_t)stream, p, g, m, v, n, step, pidx, lr, b1, b2, eps, wd);
+                     (hipStream_t)stream, p, g, m, v, n, step, pidx, lr, b1, b2, eps, wd, skip);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
 
 VAESNE_API int vaesne_adamw_steps_advance(float* steps, const uint8_t* active, int P,
-                                          void* stream) {
+                                          const int32_t* skip, void* stream) {
   if (P <= 0) return 0;
   hipLaunchKernelGGL(steps_advance_kernel, dim3((P + NT - 1) / NT), dim3(NT), 0,
-                     (hipStream_t)stream, steps, active, P);
+                     (hipStream_t)stream, steps, active, P, skip);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
