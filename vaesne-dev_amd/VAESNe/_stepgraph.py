@@ -1,0 +1,174 @@
+"""Captured training steps for `training_step` (the cannon scripts' own loop).
+
+The scripts call `training_step(model, AdamW, loader, loss_fn=lambda m, x:
+m_iwae(m, x, K=K), multimodal=True)` (cannon/ZTF_photospect.py:119-128): an eager
+loop that launches every forward and backward kernel from Python, one batch at a
+time.  At the reference's batch (16 pairs) the host side of ~450 launches per step
+costs several times the GPU time of the step.  Here the forward + backward of a
+batch signature is captured ONCE as a hipGraph and replayed for every later batch
+of that signature: the batch is copied into the graph's static inputs, the graph
+replays, the parameter gradients appear in the tensors the capture allocated, and
+the user's optimizer steps eagerly on them, exactly as before.
+
+Signature (everything the captured arithmetic depends on): the loss function's code,
+closure values and the scalar globals it names (e.g. a script's `K`), the input
+shapes / dtypes, every parameter's storage and requires_grad, and every module's
+scalar attributes (training flags, dropout p, llik_scaling, ...).  A change of any
+of them is a new signature; up to MAX_GRAPHS are kept per network (a loader's full
+batches + its ragged last batch).  A signature is captured after WARMUP eager
+batches; a capture that fails (a loss function that synchronises, say) marks the
+signature eager for good.
+
+Not captured (always eager): injected or torch-CPU-generator noise
+(rng.inject_uniform / rng.set_mode("torch_cpu"): the parity paths), host tensors,
+VAESNE_STEP_GRAPH=0.  Randomness: training_step restarts the RNG call ids at every
+batch and advances the device counter after it, so a replayed batch draws exactly
+what the same batch would draw eagerly (tests/test_gpu_stepgraph.py: bitwise).
+"""
+from __future__ import annotations
+
+import sys
+import weakref
+
+import torch
+
+from . import _config, _defer, rng
+
+WARMUP = 2
+MAX_GRAPHS = 3
+
+_SCALARS = (int, float, bool, str)
+
+
+class _Entry:
+    __slots__ = ("seen", "graph", "static_x", "loss", "params", "grads", "failed")
+
+    def __init__(self):
+        self.seen, self.graph, self.static_x, self.loss = 0, None, None, None
+        self.params, self.grads, self.failed = None, None, False
+
+
+_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+_warned = set()
+
+
+def _value_key(v):
+    """Scalars by value; anything else (functions, modules, tensors, containers) by
+    identity."""
+    if type(v) in _SCALARS or v is None:
+        return v
+    return ("id", id(v))
+
+
+def _fn_key(fn):
+    code = getattr(fn, "__code__", None)
+    if code is None:
+        return ("obj", id(fn))
+    cells = tuple(_value_key(c.cell_contents) for c in (fn.__closure__ or ()))
+    g = getattr(fn, "__globals__", {})
+    names = tuple((n, g[n]) for n in code.co_names if n in g and type(g[n]) in _SCALARS)
+    defaults = tuple(_value_key(d) for d in (fn.__defaults__ or ()))
+    kw = tuple(sorted((k, _value_key(v)) for k, v in (fn.__kwdefaults__ or {}).items()))
+    return (code, cells, names, defaults, kw, _value_key(getattr(fn, "__self__", None)))
+
+
+def _module_scalars(network):
+    return tuple(v for m in network.modules() for v in m.__dict__.values() if type(v) in _SCALARS)
+
+
+def _flat(x, multimodal):
+    return [t for m in x for t in m] if multimodal else list(x)
+
+
+def _unflat(ts, x, multimodal):
+    if not multimodal:
+        return tuple(ts)
+    out, i = [], 0
+    for m in x:
+        out.append(tuple(ts[i:i + len(m)]))
+        i += len(m)
+    return out
+
+
+def eligible(device) -> bool:
+    return (_config.step_graph and torch.device(device).type == "cuda" and rng.capturable()
+            and torch.is_grad_enabled())
+
+
+def _signature(network, loss_fn, xs, multimodal, params):
+    return (_fn_key(loss_fn), multimodal, tuple((tuple(t.shape), t.dtype) for t in xs),
+            tuple((p.data_ptr(), p.requires_grad) for p in params), _module_scalars(network))
+
+
+def step(network, loss_fn, x, multimodal):
+    """The batch's loss (a device scalar) with every parameter gradient set, from a
+    replay of the captured step; None when this batch must run eagerly (warm-up,
+    an uncapturable signature)."""
+    params = list(network.parameters())
+    xs = _flat(x, multimodal)
+    if not all(t.is_cuda for t in xs):
+        return None
+    key = _signature(network, loss_fn, xs, multimodal, params)
+    graphs = _CACHE.setdefault(network, {})
+    ent = graphs.get(key)
+    if ent is None:
+        while len(graphs) >= MAX_GRAPHS:
+            graphs.pop(next(iter(graphs)))
+        ent = graphs[key] = _Entry()
+    if ent.failed:
+        return None
+    if ent.graph is None:
+        ent.seen += 1
+        if ent.seen <= WARMUP:
+            return None
+        if not _capture(ent, network, loss_fn, x, xs, multimodal, params):
+            return None
+    for s, t in zip(ent.static_x, xs):
+        s.copy_(t, non_blocking=True)
+    ent.graph.replay()
+    for p, g in zip(ent.params, ent.grads):
+        p.grad = g
+    return ent.loss
+
+
+def _capture(ent, network, loss_fn, x, xs, multimodal, params) -> bool:
+    static_x = [t.clone() for t in xs]
+    sx = _unflat(static_x, x, multimodal)
+    for p in params:
+        p.grad = None                     # gradients are allocated in the graph's pool
+    g = torch.cuda.CUDAGraph()
+    try:
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):
+            with _defer.deferred():
+                loss = -loss_fn(network, sx)
+                loss.backward()
+            sloss = loss.detach()
+    except Exception as e:   # noqa: BLE001 -- any capture failure: this signature stays eager
+        ent.failed = True
+        for p in params:
+            p.grad = None
+        torch.cuda.synchronize()
+        if type(e).__name__ not in _warned:
+            _warned.add(type(e).__name__)
+            print(f"[VAESNe] training_step: the step could not be captured as a hipGraph "
+                  f"({type(e).__name__}: {e}); running it eagerly", file=sys.stderr)
+        return False
+    # the VAEs keep their last posterior parameters (the reference's _qz_x_params):
+    # detached, they no longer hold the captured autograd graph alive
+    for m in network.modules():
+        q = getattr(m, "_qz_x_params", None)
+        if isinstance(q, (tuple, list)):
+            m._qz_x_params = type(q)(t.detach() if torch.is_tensor(t) else t for t in q)
+    ent.graph, ent.static_x, ent.loss = g, static_x, sloss
+    ent.params = [p for p in params if p.grad is not None]
+    ent.grads = [p.grad for p in ent.params]
+    return True
+
+
+def clear(network=None):
+    """Drop the captured steps (of one network, or all)."""
+    if network is None:
+        _CACHE.clear()
+    else:
+        _CACHE.pop(network, None)

@@ -101,6 +101,12 @@ def advance(device, step: torch.Tensor | None = None):
     _lib.lib.step_advance(_lib.ptr(step), st.data_ptr(), _lib.stream())
 
 
+def capturable() -> bool:
+    """Whether the next draws may be captured in a hipGraph (device counter-based:
+    no injected draws queued, not the host generator mode)."""
+    return _mode == "device" and not _queue
+
+
 def set_mode(mode: str):
     global _mode
     if mode not in ("device", "torch_cpu"):

@@ -14,6 +14,14 @@ joins the all-reduce with zero gradients, and every rank holds a gradient for th
 same parameters (distributed.agree_grad_pattern), so all ranks apply the same update.  Each rank draws its own noise / dropout streams
 (rng.rank_seed).  The returned value is the mean full-batch loss on every rank.
 
+Captured steps (VAESNe._stepgraph): after two eager batches of one signature
+(input shapes, loss function, parameters), the forward + backward is captured
+once as a hipGraph and replayed for every later batch of that signature; the
+optimizer steps eagerly on the gradients as before.  Each batch draws its noise
+and dropout masks under the same call ids and a per-batch device counter, so a
+replayed batch computes exactly what the eager batch would (VAESNE_STEP_GRAPH=0:
+always eager).
+
 Non-finite values (VAESNe.guard): the HIP kernels flag a NaN posterior or a
 NaN / Inf loss on the device.  The flag is cleared before each batch's forward
 and read, with the loss, at ONE sync placed before `optimizer.step()` (the
@@ -28,7 +36,7 @@ import math
 
 import torch
 
-from . import _defer, guard
+from . import _defer, _stepgraph, guard, rng
 from . import distributed as D
 from .losses import elbo
 from .optim import FusedAdamW
@@ -70,9 +78,14 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
                 optimizer.grad_hook.weight = w if reduction == "mean" else None
             x = D.shard(x, rank, ws)
         guard.reset(device)       # a flag left by an unchecked eval call is not this batch's
+        rng.reset_call_ids()      # every batch draws under call ids 1.. (eager or replayed)
+        loss = None
         if empty:
             loss = torch.zeros((), dtype=torch.float32, device=device)
-        else:
+        elif _stepgraph.eligible(device):
+            # replay of the captured forward + backward of this batch signature
+            loss = _stepgraph.step(network, loss_fn, x, multimodal)
+        if loss is None:
             # parameter-gradient sums batched into one launch at the end of backward
             with _defer.deferred():
                 loss = -loss_fn(network, x)
@@ -102,6 +115,8 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
             optimizer.apply_update()       # gradients already packed and all-reduced
         else:
             optimizer.step()
+        if device.type == "cuda":
+            rng.advance(device)            # the next batch draws fresh noise / dropout
         total_loss += loss_v
         num_batches += 1.
         if release_memory:
