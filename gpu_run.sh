@@ -9,7 +9,7 @@ ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 1 = assertion failures, not a GPU
 STAGES="${STAGES:-tests smoke bench prof}"
 for s in $STAGES; do
   case $s in
-    tests) timeout -k 10 900 python -m pytest tests -m gpu -q -rf --timeout 300 ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1; rc=$?;;
+    tests) timeout -k 10 1100 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1; rc=$?;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?;;
     bench) timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?;;
     bench2) VAESNE_DP_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 10 --warmup 3 > gpurun_out/bench2.json 2> gpurun_out/bench2.err; rc=$?;;

@@ -32,18 +32,29 @@ def _free_port():
 
 
 def _spawn(target, ws, *args, timeout=300):
+    """Run target(rank, ws, port, q, *args) in ws fresh processes; the results are read
+    BEFORE joining (a rank blocks in put() until its result leaves the pipe)."""
+    import queue
     ctx = mp.get_context("spawn")
-    q = ctx.SimpleQueue()
+    q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=target, args=(r, ws, port, q) + args) for r in range(ws)]
     for pr in procs:
         pr.start()
+    res = []
+    try:
+        for _ in range(ws):
+            res.append(q.get(timeout=timeout))
+    except queue.Empty:
+        pass
     for pr in procs:
-        pr.join(timeout)
+        pr.join(60)
         if pr.exitcode is None:
             pr.kill()
-        assert pr.exitcode == 0, f"rank exit code {pr.exitcode} (None: hung)"
-    return sorted((q.get() for _ in range(ws)), key=lambda r: r[0])
+            pr.join(10)
+    codes = [pr.exitcode for pr in procs]
+    assert codes == [0] * ws and len(res) == ws, f"rank exit codes {codes}, {len(res)} results"
+    return sorted(res, key=lambda r: r[0])
 
 
 def _bench_steps(case, world, rank, us_list, graph, n_eager=3):

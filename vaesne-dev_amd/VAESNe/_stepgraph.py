@@ -131,9 +131,22 @@ def step(network, loss_fn, x, multimodal):
     return ent.loss
 
 
+def _drop_autograd_refs(network):
+    """The VAEs keep their last posterior parameters (the reference's _qz_x_params).
+    Detached, they no longer hold the previous step's autograd graph alive: its
+    AccumulateGrad nodes are bound to the eager step's stream and must not be reused
+    by a capture (torch then syncs the capture with that stream and the capture
+    breaks)."""
+    for m in network.modules():
+        q = getattr(m, "_qz_x_params", None)
+        if isinstance(q, (tuple, list)):
+            m._qz_x_params = type(q)(t.detach() if torch.is_tensor(t) else t for t in q)
+
+
 def _capture(ent, network, loss_fn, x, xs, multimodal, params) -> bool:
     static_x = [t.clone() for t in xs]
     sx = _unflat(static_x, x, multimodal)
+    _drop_autograd_refs(network)
     for p in params:
         p.grad = None                     # gradients are allocated in the graph's pool
     g = torch.cuda.CUDAGraph()
@@ -154,12 +167,7 @@ def _capture(ent, network, loss_fn, x, xs, multimodal, params) -> bool:
             print(f"[VAESNe] training_step: the step could not be captured as a hipGraph "
                   f"({type(e).__name__}: {e}); running it eagerly", file=sys.stderr)
         return False
-    # the VAEs keep their last posterior parameters (the reference's _qz_x_params):
-    # detached, they no longer hold the captured autograd graph alive
-    for m in network.modules():
-        q = getattr(m, "_qz_x_params", None)
-        if isinstance(q, (tuple, list)):
-            m._qz_x_params = type(q)(t.detach() if torch.is_tensor(t) else t for t in q)
+    _drop_autograd_refs(network)
     ent.graph, ent.static_x, ent.loss = g, static_x, sloss
     ent.params = [p for p in params if p.grad is not None]
     ent.grads = [p.grad for p in ent.params]
