@@ -677,7 +677,6 @@ class RepAttnForward:
                          ptr(self.bits), stream())
         self.qkv, self.kbias = qkv, kbias
         self.dims = (Bd, R, L, E, H, dh, float(p), self.cid)
-        self.stream = torch.cuda.current_stream()
 
     def tensors(self):
         return [t for t in (self.qkv, self.kbias, self.o, self.lse, self.bits, self.st)

@@ -228,6 +228,17 @@ def decoder_inputs(xd, repeat, blocks, context):
     return x_res, x_qkv, x_out, 1
 
 
+_REP_STREAMS = {}
+
+
+def _rep_stream(dev):
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    st = _REP_STREAMS.get(idx)
+    if st is None:
+        st = _REP_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return st
+
+
 class DecoderFirst:
     """What a fused decoder stack computes before it needs the context: block 1's
     in-projection and masked self-attention read only the decoder input (the
@@ -235,9 +246,8 @@ class DecoderFirst:
     PhotometricLayers.py:59-67), not the latents, so they run while the encoders
     still work (photospecMMVAE.forward issues them on the photometry stream).
     With _config.rep_late the repeated-sequence attention is launched here but its
-    autograd node is created by output() where the decoder consumes it (after the
-    encoders): autograd then issues its backward FIRST, on the stream the forward ran
-    on (the photometry stream), beside the spectra encoder's backward chain."""
+    autograd node is created by output() where the decoder consumes it: its backward
+    is then issued first, on a stream of its own, beside the encoders' backward."""
     __slots__ = ("N", "L", "kbias", "O1", "qkv", "late")
 
     def __init__(self, N, L, kbias, O1, qkv=None, late=None):
@@ -251,16 +261,15 @@ class DecoderFirst:
     def output(self):
         """Block 1's self-attention output (creating the late node on first use)."""
         if self.O1 is None:
-            # the node lives on the launch stream: its saved tensors are that stream's
-            # allocations and its backward (rep_bwd) and the in-projection backward that
-            # consumes it stay there (no cross-stream use to record)
-            ls = self.late.stream
+            rs = _rep_stream(self.qkv.device) if _config.streams else None
             cur = torch.cuda.current_stream()
-            with torch.cuda.stream(ls):
+            if rs is not None:
+                rs.wait_stream(cur)
+                _ops.used_on(rs, *self.late.tensors())
+            with torch.cuda.stream(rs) if rs is not None else contextlib.nullcontext():
                 self.O1 = _ops.SelfAttnRepLateFn.apply(self.qkv, self.late)
-            if ls != cur:
-                cur.wait_stream(ls)
-                _ops.used_on(cur, self.O1)
+            if rs is not None:
+                cur.wait_stream(rs)
             self.qkv = None
         return self.O1
 
