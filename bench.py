@@ -107,7 +107,7 @@ class Step:
         self.loss_fn = loss_fn or (lambda m, x: m_iwae(m, x, K=CFG["K"]))
         self.rng = rng
         self.opt = FusedAdamW([p for p in model.parameters() if p.requires_grad],
-                              lr=lr or CFG["lr"],
+                              lr=CFG["lr"] if lr is None else lr,
                               grad_hook=GradAllReduce("sum") if world > 1 else None)
         self.loss = torch.zeros((), device=device)
         self.graphs = None

@@ -3,8 +3,8 @@ gloo, VAESNE_DP_BACKEND=gloo; RCCL refuses two ranks on one device):
 
 * bench.py's own DP step (hipGraph 1: forward + backward + pack; the eager flat-gradient
   all-reduce; hipGraph 2: FusedAdamW + RNG advance), each rank on its half of the
-  benchmarked B=16 golden batch and its half of the golden noise, gives the parameters
-  of the single-process full-batch step;
+  benchmarked B=16 golden batch and its half of the golden noise, gives the flat
+  gradient of the single-process full-batch step;
 * the device RNG folds the rank in (rng.rank_seed): without injected noise the two
   ranks draw different Laplace noise;
 * a NaN on ONE rank (its half of the noise) makes BOTH ranks raise RuntimeError from
@@ -59,7 +59,11 @@ def _spawn(target, ws, *args, timeout=300):
 
 def _bench_steps(case, world, rank, us_list, graph, n_eager=3):
     """bench.Step on this rank's slice: 3 eager steps (capture warm-up) + the captured
-    (or a 4th eager) step; every step consumes its own injected noise."""
+    (or a 4th eager) step; every step consumes its own injected noise.  lr = 0, so
+    every step sees the same parameters and the last step's all-reduced flat gradient
+    can be compared to the single-process one at summation-order precision (AdamW
+    would turn rounding-level differences of near-zero gradient elements into
+    +-lr steps)."""
     import sys
     sys.path.insert(0, ROOT)
     import bench
@@ -73,7 +77,7 @@ def _bench_steps(case, world, rank, us_list, graph, n_eager=3):
     lo, hi = D.split_bounds(B, rank, world)
     x = [tuple(t[lo:hi] for t in m) for m in x]
     us = [[u[:, lo:hi].contiguous().cuda() for u in step_us] for step_us in us_list]
-    step = bench.Step(model, x, torch.device("cuda", 0), world, use_graph=graph)
+    step = bench.Step(model, x, torch.device("cuda", 0), world, use_graph=graph, lr=0.0)
     flat = [u for step_us in us for u in step_us]
     with rng.inject_uniform(flat):
         if graph:
@@ -83,7 +87,7 @@ def _bench_steps(case, world, rank, us_list, graph, n_eager=3):
                 step()
         step()
     torch.cuda.synchronize()
-    return step.opt.flat_params().clone().cpu(), step.loss.item()
+    return step.opt.flat_grad().clone().cpu(), step.loss.item()
 
 
 def _us4(case):
@@ -98,7 +102,7 @@ def _dp_bench_worker(rank, ws, port, q, case):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
-        params, loss = _bench_steps(case, ws, rank, _us4(case), graph=True)
+        grad, loss = _bench_steps(case, ws, rank, _us4(case), graph=True)
         # rank-folded device RNG: without injection the ranks draw different noise
         from VAESNe import rng
         rng.manual_seed(1234)
@@ -106,7 +110,7 @@ def _dp_bench_worker(rank, ws, port, q, case):
         us = [torch.empty_like(u) for _ in range(ws)]
         dist.all_gather(us, u)
         # plain arrays through the queue (a tensor would be shared by fd, dead with the rank)
-        q.put((rank, params.numpy(), loss, [t.numpy() for t in us]))
+        q.put((rank, grad.numpy(), loss, [t.numpy() for t in us]))
     finally:
         dist.destroy_process_group()
 
@@ -116,8 +120,9 @@ def test_bench_dp_step_world2_matches_single_process():
     ref, ref_loss = _bench_steps(case, 1, 0, _us4(case), graph=True)
     res = _spawn(_dp_bench_worker, 2, case)
     ref = ref.numpy()
-    for rank, params, loss, us in res:
-        err = float(np.abs(params - ref).max() / np.abs(ref).max())
+    for rank, grad, loss, us in res:
+        # the all-reduced flat gradient of the replayed DP step = the full batch's
+        err = float(np.abs(grad - ref).max() / np.abs(ref).max())
         assert err < 1e-5, (rank, err)
         assert not np.array_equal(us[0], us[1])       # ranks draw their own noise
         assert np.array_equal(us[0], res[0][3][0]) and np.array_equal(us[1], res[1][3][1])

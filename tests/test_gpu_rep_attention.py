@@ -184,36 +184,3 @@ def test_rep_forward_in_parts_equals_one_launch(parts, Bd, R, L, p):
     assert torch.equal(o0, o1) and torch.equal(l0, l1)
     if p > 0:
         assert torch.equal(b0, b1)
-
-
-@pytest.mark.parametrize("streams", [True, False])
-def test_late_rep_node_bitwise_equal(streams, monkeypatch):
-    """_config.rep_late: block 1's repeated-sequence attention launched beside the
-    encoders but its autograd node created where the decoder consumes it (backward
-    issued first, on its own stream) -- the same kernels and call ids, so the loss and
-    every gradient equal the default path bit for bit (dropout on, B=16 bench shape)."""
-    import os
-    import sys
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    import bench
-    from VAESNe import _config, rng
-    from VAESNe.losses import m_iwae
-    monkeypatch.setattr(_config, "streams", streams)
-    torch.manual_seed(3)
-    model = bench.make_model(DEV, 0.1)
-    model.train()
-    x = bench.synthetic_batch(16, 5, DEV)
-    outs = []
-    for late in (False, True):
-        monkeypatch.setattr(_config, "rep_late", late)
-        model.zero_grad(set_to_none=True)
-        rng.manual_seed(77)
-        loss = -m_iwae(model, x, K=8)
-        loss.backward()
-        torch.cuda.synchronize()
-        outs.append((loss.item(), {k: p.grad.clone() for k, p in model.named_parameters()
-                                   if p.grad is not None}))
-    assert outs[0][0] == outs[1][0]
-    assert set(outs[0][1]) == set(outs[1][1])
-    for k in outs[0][1]:
-        assert torch.equal(outs[0][1][k], outs[1][1][k]), k

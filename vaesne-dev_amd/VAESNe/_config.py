@@ -19,8 +19,6 @@ monkeypatch.setattr, not the environment):
                                   once per distinct sequence (test_gpu_rep_attention.py)
   defer_grads VAESNE_DEFER_GRADS=0  parameter-gradient sums launched per op instead
                                   of one batched flush (test_gpu_defer.py)
-  rep_late    VAESNE_REP_LATE=1   decoder block 1's attention backward node created
-                                  after the encoders, on its own stream (A/B)
   step_graph  VAESNE_STEP_GRAPH=0  training_step runs every batch eagerly instead of
                                   replaying a captured hipGraph (_stepgraph.py;
                                   test_gpu_stepgraph.py: bitwise equal)
@@ -40,4 +38,3 @@ fused_head = _flag("VAESNE_FUSED_HEAD")
 rep_attn = _flag("VAESNE_REP_ATTN")
 defer_grads = _flag("VAESNE_DEFER_GRADS")
 step_graph = _flag("VAESNE_STEP_GRAPH")
-rep_late = _flag("VAESNE_REP_LATE", default=False)

@@ -652,57 +652,6 @@ class SelfAttnRepFn(torch.autograd.Function):
         return dqkv, None, None, None, None
 
 
-class RepAttnForward:
-    """vaesne_attn_rep_fwd launched AHEAD of its autograd node (the decoders' block-1
-    self-attention, computed beside the encoders), for SelfAttnRepLateFn."""
-
-    def __init__(self, qkv, kbias, H, p, R):
-        _lib.require_device(qkv)
-        qkv = qkv.contiguous()
-        Bd, L, E3 = qkv.shape
-        E = E3 // 3
-        dh = E // H
-        N = R * Bd
-        dev = qkv.device
-        self.o = torch.empty((N, L, E), dtype=torch.float32, device=dev)
-        self.lse = torch.empty((Bd, H, L), dtype=torch.float32, device=dev)
-        self.st = rng.state(dev) if p > 0 else None
-        self.cid = rng.next_call_id() if p > 0 else 0
-        self.bits = None
-        if p > 0:
-            n = lib.attn_keep_bits_size(N, H, L, L)
-            self.bits = torch.empty((n + 3) // 4, dtype=torch.int32, device=dev)
-        lib.attn_rep_fwd(qkv.data_ptr(), L * E3, E3, ptr(kbias), L, self.o.data_ptr(), L * E, E,
-                         self.lse.data_ptr(), Bd, R, H, L, dh, float(p), ptr(self.st), self.cid,
-                         ptr(self.bits), stream())
-        self.qkv, self.kbias = qkv, kbias
-        self.dims = (Bd, R, L, E, H, dh, float(p), self.cid)
-
-    def tensors(self):
-        return [t for t in (self.qkv, self.kbias, self.o, self.lse, self.bits, self.st)
-                if t is not None]
-
-
-class SelfAttnRepLateFn(torch.autograd.Function):
-    """The autograd node of a RepAttnForward, created where its output is consumed
-    (after the encoders), so the backward pass reaches it BEFORE the encoders' nodes
-    (autograd runs the latest-created ready node first) and issues its kernel on the
-    stream this node is created on.  Arithmetic = SelfAttnRepFn."""
-
-    @staticmethod
-    def forward(ctx, qkv, fwd):
-        if qkv.data_ptr() != fwd.qkv.data_ptr():
-            raise RuntimeError("SelfAttnRepLateFn: qkv is not the launched forward's input")
-        ctx.dims = fwd.dims
-        ctx.save_for_backward(fwd.qkv, fwd.kbias, fwd.o, fwd.lse, fwd.bits, fwd.st)
-        return fwd.o
-
-    @staticmethod
-    def backward(ctx, do):
-        dqkv = SelfAttnRepFn.backward(ctx, do)[0]
-        return dqkv, None
-
-
 def rep_attention_ok(qkv, num_heads, R):
     """Shapes vaesne_attn_rep_* take: head_dim 8, L > 16 (query-tiled), R >= 1."""
     return (qkv.dim() == 3 and qkv.shape[-1] == 3 * 8 * num_heads and qkv.shape[1] > 16

@@ -162,6 +162,7 @@ def _capture(ent, network, loss_fn, x, xs, multimodal, params) -> bool:
         for p in params:
             p.grad = None
         torch.cuda.synchronize()
+        rng.reset_call_ids()      # the eager rerun of this batch draws what it would have
         if type(e).__name__ not in _warned:
             _warned.add(type(e).__name__)
             print(f"[VAESNe] training_step: the step could not be captured as a hipGraph "

@@ -228,50 +228,19 @@ def decoder_inputs(xd, repeat, blocks, context):
     return x_res, x_qkv, x_out, 1
 
 
-_REP_STREAMS = {}
-
-
-def _rep_stream(dev):
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    st = _REP_STREAMS.get(idx)
-    if st is None:
-        st = _REP_STREAMS[idx] = torch.cuda.Stream(device=idx)
-    return st
-
-
 class DecoderFirst:
     """What a fused decoder stack computes before it needs the context: block 1's
     in-projection and masked self-attention read only the decoder input (the
     embedding of the wavelength / time grid, SpectraLayers.py:54-62,
     PhotometricLayers.py:59-67), not the latents, so they run while the encoders
-    still work (photospecMMVAE.forward issues them on the photometry stream).
-    With _config.rep_late the repeated-sequence attention is launched here but its
-    autograd node is created by output() where the decoder consumes it: its backward
-    is then issued first, on a stream of its own, beside the encoders' backward."""
-    __slots__ = ("N", "L", "kbias", "O1", "qkv", "late")
+    still work (photospecMMVAE.forward issues them on the photometry stream)."""
+    __slots__ = ("N", "L", "kbias", "O1")
 
-    def __init__(self, N, L, kbias, O1, qkv=None, late=None):
+    def __init__(self, N, L, kbias, O1):
         self.N, self.L, self.kbias, self.O1 = N, L, kbias, O1
-        self.qkv, self.late = qkv, late
 
     def tensors(self):
-        ts = [t for t in (self.kbias, self.O1, self.qkv) if t is not None]
-        return ts + (self.late.tensors() if self.late is not None else [])
-
-    def output(self):
-        """Block 1's self-attention output (creating the late node on first use)."""
-        if self.O1 is None:
-            rs = _rep_stream(self.qkv.device) if _config.streams else None
-            cur = torch.cuda.current_stream()
-            if rs is not None:
-                rs.wait_stream(cur)
-                _ops.used_on(rs, *self.late.tensors())
-            with torch.cuda.stream(rs) if rs is not None else contextlib.nullcontext():
-                self.O1 = _ops.SelfAttnRepLateFn.apply(self.qkv, self.late)
-            if rs is not None:
-                cur.wait_stream(rs)
-            self.qkv = None
-        return self.O1
+        return [t for t in (self.kbias, self.O1) if t is not None]
 
 
 def decoder_stack_first(blocks, x, mask=None, x_qkv=None, rep=1):
@@ -288,9 +257,6 @@ def decoder_stack_first(blocks, x, mask=None, x_qkv=None, rep=1):
     if rep > 1 and _ops.rep_attention_ok(qkv, b0.num_heads, rep):
         Bd = N // rep
         kb = None if kbias is None else kbias[:Bd]
-        if _config.rep_late and torch.is_grad_enabled() and qkv.requires_grad:
-            late = _ops.RepAttnForward(qkv, kb, b0.num_heads, p_attn, rep)
-            return DecoderFirst(N, L, kbias, None, late.qkv, late)
         O1 = _ops.self_attention_rep(qkv, kb, b0.num_heads, p_attn, rep)
     else:
         if rep > 1:
@@ -333,7 +299,7 @@ def decoder_stack(blocks, x, context, mask=None, x_qkv=None, rep=1, first=None):
         p_attn = blk.self_attn.dropout if blk.training else 0.0
         p = blk.dropout.p if blk.training else 0.0
         if i == 0:
-            O = first.output()
+            O = first.O1
         else:
             O = _ops.self_attention(qkv, None, blk.self_attn.num_heads, p_attn, kbias=kbias)
         nxt = blocks[i + 1].self_attn if i + 1 < len(blocks) else None
