@@ -2,7 +2,8 @@
 from a rocprofv3 kernel trace of bench.py.  The --stats summary averages every launch
 of an instantiation, and the spectra encoder's context self-attention (a split launch,
 grid y > 1) uses the decoder's instantiation too, so the decoder launches are picked
-by grid: N*H query/key blocks of 256 threads in x, one chunk in y.
+by grid: N*H query/key blocks of 256 threads in x, one chunk in y; only launches
+inside replayed (captured) training steps count.
     python profiles/roofline_launches.py <run_kernel_trace.csv> <out.json>"""
 import csv
 import json
@@ -15,9 +16,27 @@ KERNELS = {
 }
 
 
+def replayed_step_rows(rows):
+    """Rows of the captured (replayed) training steps: AdamW-to-AdamW windows no longer
+    than 1.2x the fastest (bench.py also runs eager steps for its in-step HIP-event timing
+    and isolated roofline launches; those are excluded)."""
+    rows = sorted(rows, key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
+    wins = [(int(rows[j]["End_Timestamp"]) - int(rows[i + 1]["Start_Timestamp"]), i, j)
+            for i, j in zip(idx[:-1], idx[1:]) if j - i > 50]
+    if not wins:
+        return rows
+    fastest = min(w[0] for w in wins)
+    out = []
+    for span, i, j in wins:
+        if span <= 1.2 * fastest:
+            out.extend(rows[i + 1: j + 1])
+    return out
+
+
 def main(path, out):
     res = {}
-    rows = list(csv.DictReader(open(path)))
+    rows = replayed_step_rows(list(csv.DictReader(open(path))))
     for key, inst in KERNELS.items():
         durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in rows
                 if inst in r["Kernel_Name"] and int(r["Grid_Size_X"]) == N * H * 256

@@ -1,18 +1,23 @@
-"""Per-kernel SQ counter summary of profiles/sq_pass.sh output:
-    python profiles/sq_summary.py gpurun_out/pmc_sq1/run_counter_collection.csv [...]"""
+"""Per-kernel SQ counter summary of profiles/sq_pass.sh / pmc_step.sh output:
+    python profiles/sq_summary.py [-k substr,substr] run_counter_collection.csv [...]"""
 import collections
 import csv
 import sys
 
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 dur = collections.defaultdict(list)
-for path in sys.argv[1:]:
+args = sys.argv[1:]
+keys = ("attn_fwd", "attn_bwd", "keep_bits")
+if args and args[0] == "-k":
+    keys = tuple(args[1].split(","))
+    args = args[2:]
+for path in args:
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
         agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
         dur[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for name, cs in agg.items():
-    if not any(k in name for k in ("attn_fwd", "attn_bwd", "keep_bits")):
+    if not any(k in name for k in keys):
         continue
     avg = {k: sum(v) / len(v) for k, v in cs.items()}
     print(f"{name}: {sum(dur[name]) / len(dur[name]):.1f} us avg over {len(dur[name])} rows")
