@@ -236,14 +236,37 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   const float* kbg = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
   uint32_t* bitp = DROP ? a.bits + (int64_t)bh * a.nw * a.Lq : nullptr;
   const int kbeg = blockIdx.y * a.kchunk, klim = min(a.Lk, kbeg + a.kchunk);
+  // ASYNC (dh 8, 256 threads): the next key tile's K / V rows and key bias are loaded
+  // into registers before this tile's compute and written to LDS after it
+  // (issue-early / write-late): thread t < 128 holds K float4 (row t/2, half t%2),
+  // t >= 128 the V float4 of row (t-128)/2, t < 64 the key bias of row t
+  constexpr bool ASYNC = DH == 8 && NTT == 256;
+  float4 rKV = make_float4(0.f, 0.f, 0.f, 0.f);
+  float rB = -INFINITY;
+  auto issue = [&](int kt) {
+    const int t = threadIdx.x, half = t & 1, row = (t & 127) >> 1;
+    const bool ok = kt + row < klim;
+    const int64_t kc = min(kt + row, klim - 1);
+    const float* src = t < 128 ? kg + kc * a.k_ls : vg + kc * a.v_ls;
+    rKV = ok ? *reinterpret_cast<const float4*>(src + 4 * half) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t < TK) rB = kt + t < klim ? (kbg ? kbg[kt + t] : 0.f) : -INFINITY;
+  };
+  if (ASYNC && kbeg < klim) issue(kbeg);
 
   for (int kt = kbeg; kt < klim; kt += TK) {
     __syncthreads();
-    stage<DH, NTT>(Ks, kg, a.k_ls, kt, klim, 1.f);
-    stage<DH, NTT>(Vs, vg, a.v_ls, kt, klim, 1.f);
-    for (int i = threadIdx.x; i < TK; i += NTT)
-      Kb[i] = kt + i < klim ? (kbg ? kbg[kt + i] : 0.f) : -INFINITY;
+    if (ASYNC) {
+      const int t = threadIdx.x, half = t & 1, row = (t & 127) >> 1;
+      *reinterpret_cast<float4*>((t < 128 ? Ks : Vs) + row * DH + 4 * half) = rKV;
+      if (t < TK) Kb[t] = rB;
+    } else {
+      stage<DH, NTT>(Ks, kg, a.k_ls, kt, klim, 1.f);
+      stage<DH, NTT>(Vs, vg, a.v_ls, kt, klim, 1.f);
+      for (int i = threadIdx.x; i < TK; i += NTT)
+        Kb[i] = kt + i < klim ? (kbg ? kbg[kt + i] : 0.f) : -INFINITY;
+    }
     __syncthreads();
+    if (ASYNC && kt + TK < klim) issue(kt + TK);   // next tile's loads fly under this compute
     const int kend = min(TK, klim - kt);
     uint32_t w[R];
 #pragma unroll
@@ -448,10 +471,16 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
   constexpr int NWB = (KB + 31) / 32;       // bitmap words of this key block
   constexpr int NWV = NTT / 64;             // waves
   static_assert(!DQ || DH == 8, "fused dQ reduces 8 components");
+  // ASYNC (dh 8, 256 threads: the decoders' launches): the next query tile's Q, dO, O,
+  // lse and keep words are loaded into registers BEFORE this tile's compute and written
+  // to LDS after it (issue-early / write-late), so their HBM latency hides under the
+  // compute instead of stalling every wave at each tile's start
+  constexpr bool ASYNC = DH == 8 && NTT == 256;
+  constexpr int NWBP = NWB + (ASYNC ? 1 : 0);   // padded row: conflict-free column writes
   __shared__ __attribute__((aligned(16))) float Qs[TK * DH];
   __shared__ __attribute__((aligned(16))) float Ds_[TK * DH];   // dO tile
   __shared__ float Ls[TK], Dd[TK];
-  __shared__ uint32_t Ws[TK * NWB];
+  __shared__ uint32_t Ws[TK * NWBP];
   __shared__ __attribute__((aligned(16))) float Qw[DQ ? NWV * TK * DH : 1];   // per-wave dQ
   // keep-bit lookup: 4 bits of the bitmap -> the two key pairs' 0/1 float masks
   // (one conflict-free ds_read_b128 instead of ~16 bit-extract / compare / select
@@ -502,32 +531,101 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
   // dO is staged pre-multiplied by 1/(1-p): dV = sum keep*P*dO/(1-p) and
   // dP = keep * (V . dO)/(1-p) come out scaled; D = rowsum(dO*O) uses the raw dO.
   const int qbeg = blockIdx.y * a.qchunk, qlim = min(a.Lq, qbeg + a.qchunk);
+  // ASYNC register stage: thread t < 128 holds dO and O float4 (row t/2, half t%2),
+  // thread t >= 128 the Q float4 of row (t-128)/2; t < 64 the lse of row t; every
+  // thread NWS keep words (word-major, 64 consecutive queries per word: coalesced)
+  constexpr int NWS = ASYNC && DROP ? (TK * NWB) / NTT : 1;
+  static_assert(!ASYNC || (TK * NWB) % NTT == 0, "keep words per thread");
+  float4 rA = make_float4(0.f, 0.f, 0.f, 0.f), rO = rA;
+  float rL = INFINITY;
+  uint32_t rW[NWS];
+  auto issue = [&](int qt) {     // loads of query tile qt (rows past qlim: zeros / +inf)
+    const int t = threadIdx.x, half = t & 1;
+    const int row = (t & 127) >> 1, qi = qt + row;
+    const bool ok = qi < qlim;
+    const int64_t qc = min(qi, qlim - 1);
+    if (t < 128) {
+      rA = ok ? *reinterpret_cast<const float4*>(dg + qc * a.do_ls + 4 * half) : make_float4(0.f, 0.f, 0.f, 0.f);
+      rO = ok ? *reinterpret_cast<const float4*>(og + qc * a.o_ls + 4 * half) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      rA = ok ? *reinterpret_cast<const float4*>(qg + qc * a.q_ls + 4 * half) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (t < TK) rL = qt + t < qlim ? lg[qt + t] : INFINITY;
+    if (DROP) {
+#pragma unroll
+      for (int j = 0; j < NWS; ++j) {
+        const int idx = j * NTT + t, i = idx % TK, wv = idx / TK;
+        const int word = wfirst + wv;
+        rW[j] = (qt + i < qlim && word < a.nw) ? bitp[(int64_t)word * a.Lq + qt + i] : 0u;
+      }
+    }
+  };
+  auto commit = [&]() {          // the staged registers -> LDS (after a barrier)
+    const int t = threadIdx.x, half = t & 1, row = (t & 127) >> 1;
+    if (t < 128) {
+      // D = rowsum(dO * O) in the sequential order of the fmaf chain over d = 0..7:
+      // the half-1 lane continues the half-0 lane's partial sum
+      float pd = fmaf(rA.x, rO.x, 0.f);
+      pd = fmaf(rA.y, rO.y, pd);
+      pd = fmaf(rA.z, rO.z, pd);
+      pd = fmaf(rA.w, rO.w, pd);
+      const float p0 = __shfl_xor(pd, 1);
+      if (half) {
+        float Di = fmaf(rA.x, rO.x, p0);
+        Di = fmaf(rA.y, rO.y, Di);
+        Di = fmaf(rA.z, rO.z, Di);
+        Di = fmaf(rA.w, rO.w, Di);
+        Dd[row] = Di;
+      }
+      const float m = a.inv_keep;
+      *reinterpret_cast<float4*>(Ds_ + row * DH + 4 * half) =
+          make_float4(rA.x * m, rA.y * m, rA.z * m, rA.w * m);
+    } else {
+      const float m = a.scale_log2;
+      *reinterpret_cast<float4*>(Qs + row * DH + 4 * half) =
+          make_float4(rA.x * m, rA.y * m, rA.z * m, rA.w * m);
+    }
+    if (t < TK) Ls[t] = rL;      // +inf for padding rows -> p = 0
+    if (DROP) {
+#pragma unroll
+      for (int j = 0; j < NWS; ++j) {
+        const int idx = j * NTT + t, i = idx % TK, wv = idx / TK;
+        Ws[i * NWBP + wv] = rW[j];
+      }
+    }
+  };
+  if (ASYNC && qbeg < qlim) issue(qbeg);
   for (int qt = qbeg; qt < qlim; qt += TK) {
     __syncthreads();
-    stage<DH, NTT>(Qs, qg, a.q_ls, qt, qlim, a.scale_log2);
-    stage<DH, NTT>(Ds_, dg, a.do_ls, qt, qlim, a.inv_keep);
-    for (int i = threadIdx.x; i < TK; i += NTT) {
-      const int qi = qt + i;
-      float Di = 0.f, li = INFINITY;
-      if (qi < qlim) {
-        float x[DH], y[DH];
-        ldr<DH>(dg + (int64_t)qi * a.do_ls, x);
-        ldr<DH>(og + (int64_t)qi * a.o_ls, y);
+    if (ASYNC) {
+      commit();
+    } else {
+      stage<DH, NTT>(Qs, qg, a.q_ls, qt, qlim, a.scale_log2);
+      stage<DH, NTT>(Ds_, dg, a.do_ls, qt, qlim, a.inv_keep);
+      for (int i = threadIdx.x; i < TK; i += NTT) {
+        const int qi = qt + i;
+        float Di = 0.f, li = INFINITY;
+        if (qi < qlim) {
+          float x[DH], y[DH];
+          ldr<DH>(dg + (int64_t)qi * a.do_ls, x);
+          ldr<DH>(og + (int64_t)qi * a.o_ls, y);
 #pragma unroll
-        for (int d = 0; d < DH; ++d) Di = fmaf(x[d], y[d], Di);
-        li = lg[qi];
+          for (int d = 0; d < DH; ++d) Di = fmaf(x[d], y[d], Di);
+          li = lg[qi];
+        }
+        Dd[i] = Di;
+        Ls[i] = li;     // +inf for padding rows -> p = 0
       }
-      Dd[i] = Di;
-      Ls[i] = li;     // +inf for padding rows -> p = 0
-    }
-    if (DROP) {
-      for (int idx = threadIdx.x; idx < TK * NWB; idx += NTT) {
-        const int i = idx / NWB, wv = idx - i * NWB;
-        const int qi = qt + i, word = wfirst + wv;
-        Ws[idx] = (qi < qlim && word < a.nw) ? bitp[(int64_t)word * a.Lq + qi] : 0u;
+      if (DROP) {
+        for (int idx = threadIdx.x; idx < TK * NWB; idx += NTT) {
+          const int i = idx / NWB, wv = idx - i * NWB;
+          const int qi = qt + i, word = wfirst + wv;
+          Ws[i * NWBP + wv] = (qi < qlim && word < a.nw) ? bitp[(int64_t)word * a.Lq + qi] : 0u;
+        }
       }
     }
     __syncthreads();
+    if (ASYNC && qt + TK < qlim) issue(qt + TK);   // next tile's loads fly under this compute
     const int qend = min(TK, qlim - qt);
     // two queries per trip (a padding row past qend has Ls = +inf -> p = 0 and
     // contributes nothing): explicit, as the wave reduction's cross-lane ops
@@ -542,7 +640,7 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
         const f2 li = bc(Ls[i]), Di = bc(Dd[i]);
         f2 km[2];
         if (DROP) {
-          const float4 t = Mt[(Ws[i * NWB + wl] >> sh) & 15u];
+          const float4 t = Mt[(Ws[i * NWBP + wl] >> sh) & 15u];
           km[0] = (f2){t.x, t.y};
           km[1] = (f2){t.z, t.w};
         }
