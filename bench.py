@@ -119,10 +119,16 @@ class Step:
             from VAESNe._defer import deferred
         except ImportError:            # an older package under profiles/ab_pkg.sh
             deferred = contextlib.nullcontext
+        try:
+            from VAESNe.training_util import backward_negated
+        except ImportError:
+            def backward_negated(v):
+                loss = -v
+                loss.backward()
+                return loss
         self.opt.zero_grad(set_to_none=True)
         with deferred():   # parameter-gradient sums: one batched launch at the end of backward
-            loss = -self.loss_fn(self.model, self.x)
-            loss.backward()
+            loss = backward_negated(self.loss_fn(self.model, self.x))   # = (-f).backward()
         # the VAEs keep their last posterior parameters (the reference's `_qz_x_params`),
         # which would keep this step's autograd graph -- and its AccumulateGrad nodes,
         # bound to this step's stream -- alive into the next (captured) step

@@ -89,11 +89,18 @@ class SpectraVAE(VAE):
 
     def posterior_steps(self, x, K=1):
         """posterior as a generator (VAESNe._chain.drive)."""
+        params = yield from self.encoder_steps(x)
+        return self.sample(params, K)
+
+    def encoder_steps(self, x):
+        """The encoder alone as a generator (-> (loc, scale) of q(z|x))."""
         flux, wavelength, phase, mask = x
-        self._qz_x_params = yield from self.enc.steps(flux, wavelength, phase, mask)
-        qz_x = self._dist(self.qz_x, *self._qz_x_params)
-        zs = _ops.laplace_rsample(*self._qz_x_params, K)
-        return qz_x, zs
+        return (yield from self.enc.steps(flux, wavelength, phase, mask))
+
+    def sample(self, params, K=1):
+        """q(z|x) of the encoder output `params` and its K reparameterised draws."""
+        self._qz_x_params = params
+        return self._dist(self.qz_x, *params), _ops.laplace_rsample(*params, K)
 
     def reconstruct(self, x, K=1):
         self.eval()

@@ -32,7 +32,7 @@ import weakref
 
 import torch
 
-from . import _config, _defer, rng
+from . import _config, _defer, rng, training_util
 
 WARMUP = 2
 MAX_GRAPHS = 3
@@ -154,9 +154,7 @@ def _capture(ent, network, loss_fn, x, xs, multimodal, params) -> bool:
         torch.cuda.synchronize()
         with torch.cuda.graph(g):
             with _defer.deferred():
-                loss = -loss_fn(network, sx)
-                loss.backward()
-            sloss = loss.detach()
+                sloss = training_util.backward_negated(loss_fn(network, sx))
     except Exception as e:   # noqa: BLE001 -- any capture failure: this signature stays eager
         ent.failed = True
         for p in params:

@@ -42,6 +42,27 @@ from .losses import elbo
 from .optim import FusedAdamW
 
 
+_SEEDS = {}
+
+
+def backward_negated(value):
+    """`loss = -value; loss.backward()` (training_util.py:42-44) with the gradient seed
+    -1 handed to `value` directly: the same gradients bit for bit (NegBackward
+    multiplies the seed 1 by -1 exactly), without the fill and negation launches that
+    sit between the forward and the backward of every step.  Returns -value
+    (detached), negated after the backward was issued."""
+    key = (value.device, value.dtype, tuple(value.shape))
+    seed = _SEEDS.get(key)
+    if seed is None:
+        if value.is_cuda and torch.cuda.is_current_stream_capturing():
+            loss = -value          # no persistent seed yet: never allocate one in a capture
+            loss.backward()
+            return loss.detach()
+        seed = _SEEDS[key] = torch.full(key[2], -1.0, dtype=value.dtype, device=value.device)
+    value.backward(seed)
+    return -value.detach()
+
+
 def safelog10(x):
     tmp = max(1e-10, x)
     return math.log10(tmp)
@@ -88,8 +109,7 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
         if loss is None:
             # parameter-gradient sums batched into one launch at the end of backward
             with _defer.deferred():
-                loss = -loss_fn(network, x)
-                loss.backward()
+                loss = backward_negated(loss_fn(network, x))
         if ws > 1:
             # every rank all-reduces the same set of gradients (an empty slice, or a
             # parameter the loss does not reach on some rank, gets zeros)
