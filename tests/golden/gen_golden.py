@@ -292,6 +292,20 @@ def run_generate(name, c, outdir, N=3):
           f"sgen {out['sgen'].shape} -> {path}")
 
 
+# Whole-module pickles (torch.save(model), the form photometry2goldstein_mmvae.py:36-37
+# and the other cannon scripts load): the filled reference model of the case, so its
+# loss is the case's recorded `loss` (seed 7 noise u0/u1).  Loading them executes
+# pickle code, so they are our own generated files, loaded only by tests.
+PICKLE_CASES = ["mmvae_tiny", "mmvae_tiny_noconcat", "elbo_spec_tiny_K3"]
+
+
+def run_pickle(name, c, outdir):
+    model = build(c)
+    path = os.path.join(outdir, f"pkl_{name}.pt")
+    torch.save(model, path)
+    print(f"pkl_{name}: whole-module pickle of {type(model).__name__} -> {path}")
+
+
 if __name__ == "__main__":
     outdir = sys.argv[1] if len(sys.argv) > 1 else HERE
     only = sys.argv[2:]
@@ -307,3 +321,7 @@ if __name__ == "__main__":
         if only and ("gen_" + name) not in only:
             continue
         run_generate(name, CASES[name], outdir)
+    for name in PICKLE_CASES:
+        if only and ("pkl_" + name) not in only:
+            continue
+        run_pickle(name, CASES[name], outdir)

@@ -192,3 +192,28 @@ def test_identical_seeds_reproduce_reference_loss(name):
     finally:
         rng.set_mode("device")
     assert _rel(loss, g["loss"]) < LOSS_TOL, (loss.item(), float(g["loss"]))
+
+
+@pytest.mark.parametrize("name", ["mmvae_tiny", "mmvae_tiny_noconcat", "elbo_spec_tiny_K3"])
+def test_reference_pickle_loss(name):
+    """A model the REFERENCE pickled whole (torch.save(model); cannon/test_spectra.py:94)
+    loaded with torch.load(map_location="cuda") runs on the HIP path and reproduces
+    the reference's loss and gradient norms of that model (test_pickle_compat.py: the
+    unpickled classes and state)."""
+    from test_pickle_compat import load_reference_pickle
+    from VAESNe import rng
+    from VAESNe.util_layers import Linear
+    g = load_golden(name)
+    c = g["config"]
+    model = load_reference_pickle(name, map_location="cuda")
+    assert all(type(m) is not torch.nn.Linear for m in model.modules())
+    assert any(type(m) is Linear for m in model.modules())
+    model.train()
+    x = golden_x(g, "cuda")
+    with rng.inject_uniform(golden_us(g)):
+        loss = _loss(c, model, x)
+    assert _rel(loss, g["loss"]) < LOSS_TOL, (loss.item(), float(g["loss"]))
+    loss.backward()
+    params = dict(model.named_parameters())
+    for k, n in zip(json.loads(str(g["grad_names"])), g["grad_norms"]):
+        assert abs(params[k].grad.norm().item() - n) <= 1e-3 * max(n, 1e-3), k

@@ -11,7 +11,7 @@ from torch import nn
 from . import _chain, _ops
 from .PhotometricLayers import photometricTransformerDecoder, photometricTransformerEncoder
 from .base_vae import VAE, check_laplace
-from .util_layers import MLP
+from .util_layers import MLP, ReferencePickle
 
 
 class PhotometricEnc(nn.Module):
@@ -56,7 +56,7 @@ class PhotometricDec(nn.Module):
         return x_rec, var
 
 
-class PhotometricVAE(VAE):
+class PhotometricVAE(ReferencePickle, VAE):
     def __init__(self, num_bands=6, latent_len=8, latent_dim=4, model_dim=64, num_heads=4,
                  ff_dim=64, num_layers=4, dropout=0.1, selfattn=False, concat=True, beta=1.,
                  prior=dist.Laplace, likelihood=dist.Laplace, posterior=dist.Laplace,

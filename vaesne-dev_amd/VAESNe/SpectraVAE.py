@@ -10,7 +10,7 @@ from torch import nn
 from . import _chain, _ops
 from .SpectraLayers import spectraTransformerDecoder, spectraTransformerEncoder
 from .base_vae import VAE, check_laplace
-from .util_layers import MLP
+from .util_layers import MLP, ReferencePickle
 
 
 class SpectraEnc(nn.Module):
@@ -55,7 +55,7 @@ class SpectraDec(nn.Module):
         return x_rec, var
 
 
-class SpectraVAE(VAE):
+class SpectraVAE(ReferencePickle, VAE):
     def __init__(self, latent_len=4, latent_dim=2, model_dim=32, num_heads=4, ff_dim=32,
                  num_layers=4, dropout=0.1, selfattn=False, concat=True, beta=1.,
                  prior=dist.Laplace, likelihood=dist.Laplace, posterior=dist.Laplace,

@@ -12,10 +12,10 @@ from torch import nn
 
 from .PhotometricLayers import photometricTransformerEncoder
 from .SpectraLayers import spectraTransformerEncoder
-from .util_layers import singlelayerMLP
+from .util_layers import ReferencePickle, singlelayerMLP
 
 
-class ContraPhotSpec(nn.Module):
+class ContraPhotSpec(ReferencePickle, nn.Module):
     """contrastive photometric and spectra pretraining"""
 
     def __init__(self, latent_len, latent_dim, proj_dim,

@@ -7,6 +7,7 @@ import torch.distributions as dist
 import torch.nn as nn
 
 from . import _config, _ops
+from .util_layers import ReferencePickle
 
 
 _SIDE = {}
@@ -79,7 +80,7 @@ class _CellMatrix(list):
         self.merged = []
 
 
-class photospecMMVAE(nn.Module):
+class photospecMMVAE(ReferencePickle, nn.Module):
     def __init__(self, vaes, prior_dist=dist.Laplace, beta=1., length_ratio=982 / 60):
         super().__init__()
         self.pz = prior_dist

@@ -14,10 +14,10 @@ from torch import nn
 
 from .PhotometricLayers import photometricTransformerEncoder
 from .SpectraLayers import spectraTransformerEncoder
-from .util_layers import MLP
+from .util_layers import MLP, ReferencePickle
 
 
-class VAEregressionHead(nn.Module):
+class VAEregressionHead(ReferencePickle, nn.Module):
     def __init__(self, vae, outdim, freeze_vae=True, MLPlatent=[64, 64]):
         super(VAEregressionHead, self).__init__()
         if freeze_vae:
@@ -32,7 +32,7 @@ class VAEregressionHead(nn.Module):
         return self.outfc(h)
 
 
-class contrasphotoregressionHead(nn.Module):
+class contrasphotoregressionHead(ReferencePickle, nn.Module):
     def __init__(self, contrastnet, outdim, freeze_contrastnet=True, MLPlatent=[64, 64]):
         super(contrasphotoregressionHead, self).__init__()
         if freeze_contrastnet:
@@ -48,7 +48,7 @@ class contrasphotoregressionHead(nn.Module):
         return self.outfc(h)
 
 
-class contrasspecregressionHead(nn.Module):
+class contrasspecregressionHead(ReferencePickle, nn.Module):
     def __init__(self, contrastnet, outdim, freeze_contrastnet=True, MLPlatent=[64, 64]):
         super(contrasspecregressionHead, self).__init__()
         if freeze_contrastnet:
@@ -64,7 +64,7 @@ class contrasspecregressionHead(nn.Module):
         return self.outfc(h)
 
 
-class photoend2endregression(nn.Module):
+class photoend2endregression(ReferencePickle, nn.Module):
     def __init__(self, outdim, num_bands=6, latent_len=4, latent_dim=4, model_dim=32,
                  num_heads=4, ff_dim=32, num_layers=4, dropout=0.1, selfattn=False,
                  MLPlatent=[64, 64]):
@@ -82,7 +82,7 @@ class photoend2endregression(nn.Module):
         return self.outfc(h)
 
 
-class specend2endregression(nn.Module):
+class specend2endregression(ReferencePickle, nn.Module):
     def __init__(self, outdim, latent_len=4, latent_dim=4, model_dim=32, num_heads=4,
                  num_layers=4, ff_dim=32, dropout=0.1, selfattn=False, MLPlatent=[64, 64]):
         super().__init__()

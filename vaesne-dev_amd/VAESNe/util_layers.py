@@ -31,6 +31,31 @@ class Linear(nn.Linear):
         return _ops.linear(x, self.weight, self.bias, act=act, x2=x2, base=base)
 
 
+class ReferencePickle:
+    """Mixin of the top-level models: a whole-module pickle written by the REFERENCE
+    (torch.save(model), cannon/test_spectra.py:94, loaded by torch.load in
+    cannon/try_spectra_model.py:29 and the other try_* / test/goldstein scripts)
+    unpickles into this package's classes by module path; its leaf layers are plain
+    torch nn.Linear / nn.MultiheadAttention.  After unpickling they are re-classed to
+    the HIP Linear / MultiheadAttention (same parameters, same state), so the loaded
+    model runs on the HIP path (tests/test_pickle_compat.py, tests/test_gpu_parity.py)."""
+
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        upgrade_reference_modules(self)
+
+
+def upgrade_reference_modules(root):
+    """Re-class torch nn.Linear / nn.MultiheadAttention leaves of `root` (in place)."""
+    for m in root.modules():
+        t = type(m)
+        if t is nn.Linear:
+            m.__class__ = Linear
+        elif t is nn.MultiheadAttention:
+            m.__class__ = MultiheadAttention
+    return root
+
+
 ########### simple MLPs ###############
 class singlelayerMLP(nn.Module):
     """fc2(relu(fc1(x))) — util_layers.py:9-18.  `x2` (optional) is added to x
@@ -84,6 +109,20 @@ class _DivTerm:
             self._dev[key] = d
         return d
 
+    def __getstate__(self):
+        return {"cpu": self.cpu}
+
+    def __setstate__(self, state):
+        self.cpu, self._dev = state["cpu"], {}
+
+
+def _restore_div(module, state):
+    """A reference pickle holds the tensor `div_term` (util_layers.py:122,138)."""
+    div = state.pop("div_term", None)
+    nn.Module.__setstate__(module, state)
+    if div is not None and "_div" not in module.__dict__:
+        module._div = _DivTerm(div.float().cpu())
+
 
 class SinusoidalPositionalEmbedding(nn.Module):
     """[sin(x*d), cos(x*d)] with d = exp(arange(0,dim,2) * -ln(1e4)/dim) — util_layers.py:113-129."""
@@ -93,6 +132,9 @@ class SinusoidalPositionalEmbedding(nn.Module):
         self.dim = dim
         self._div = _DivTerm(torch.exp(torch.arange(0, dim, 2).float() *
                                        (-torch.log(torch.tensor(10000.0)) / dim)))
+
+    def __setstate__(self, state):
+        _restore_div(self, state)
 
     @property
     def div_term(self):
@@ -113,6 +155,9 @@ class SinusoidalMLPPositionalEmbedding(nn.Module):
                                        (-torch.log(torch.tensor(10000.0)) / dim)))
         self.fc1 = Linear(2 * dim, dim)
         self.fc2 = Linear(dim, dim)
+
+    def __setstate__(self, state):
+        _restore_div(self, state)
 
     @property
     def div_term(self):
