@@ -198,8 +198,9 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   constexpr int R = 2 * NP;
   constexpr int QB = R * NTT;
   const int nqb = (a.Lq + QB - 1) / QB;
-  const int qb = blockIdx.x % nqb;
-  const int bh = blockIdx.x / nqb;
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int qb = wg % nqb;
+  const int bh = wg / nqb;
   const int b = bh / a.H, h = bh - b * a.H;
   int qi[R], qc[R];
 #pragma unroll
@@ -490,8 +491,9 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
     Mt[threadIdx.x] = make_float4((float)(threadIdx.x & 1), (float)((threadIdx.x >> 1) & 1),
                                   (float)((threadIdx.x >> 2) & 1), (float)((threadIdx.x >> 3) & 1));
   const int nkb = (a.Lk + KB - 1) / KB;
-  const int kb = blockIdx.x % nkb;
-  const int bh = blockIdx.x / nkb;
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int kb = wg % nkb;
+  const int bh = wg / nkb;
   const int b = bh / a.H, h = bh - b * a.H;
   const int key0 = kb * KB + R * threadIdx.x;
   f2 k[NP][DH], v[NP][DH], dk[NP][DH], dv[NP][DH], kbias[NP];
@@ -740,8 +742,9 @@ __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
   constexpr int R = 2 * NP;
   constexpr int QB = R * NTT;
   const int nqb = (a.Lq + QB - 1) / QB;
-  const int qb = blockIdx.x % nqb;
-  const int bh = blockIdx.x / nqb;
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int qb = wg % nqb;
+  const int bh = wg / nqb;
   const int b = bh / a.H, h = bh - b * a.H;
   int qi[R], qc[R];
 #pragma unroll
@@ -865,8 +868,9 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R, in
   constexpr int R2 = 2 * NP;              // queries per lane (pairs p = {2p, 2p + 1})
   constexpr int QB = R2 * NTT;
   constexpr int NC = DROP ? RC : 1;       // accumulator sets (no dropout: one for all copies)
-  const int qb = qb0 + blockIdx.x % nqbs;
-  const int bh = blockIdx.x / nqbs;       // distinct sequence x head
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int qb = qb0 + wg % nqbs;
+  const int bh = wg / nqbs;               // distinct sequence x head
   const int b = bh / a.H, h = bh - b * a.H;
   const int c0 = blockIdx.y * RC;
   int qi[R2], qc[R2];
@@ -1080,8 +1084,9 @@ void attn_rep_bwd_kernel(AttnArgs a, int R, int QS) {
   __shared__ uint32_t Ws[RC * NWB * WST];
   __shared__ __attribute__((aligned(16))) float Qw[NWV * TQR * DH];
   const int nkb = (a.Lk + KB - 1) / KB;
-  const int kb = blockIdx.x % nkb;
-  const int bh = blockIdx.x / nkb;
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int kb = wg % nkb;
+  const int bh = wg / nkb;
   const int b = bh / a.H, h = bh - b * a.H;
   const int qs = blockIdx.y % QS, cb = blockIdx.y / QS, ncb = gridDim.y / QS;
   const int c0 = cb * RC;
@@ -1571,6 +1576,12 @@ Geo g_split = [] {
   if (const char* e = getenv("VAESNE_ATTN_SPLIT_GEO")) sscanf(e, "%d,%d", &f.nt, &f.np);
   return f;
 }();
+// forward-only geometry override for unsplit launches (tuning: VAESNE_ATTN_FWD_GEO="nt,np")
+Geo g_fwd_geo = [] {
+  Geo f{0, 0};
+  if (const char* e = getenv("VAESNE_ATTN_FWD_GEO")) sscanf(e, "%d,%d", &f.nt, &f.np);
+  return f;
+}();
 Geo pick_geo(int64_t bh, int L) {
   if (g_forced.nt > 0) return g_forced;
   // among geometries with >= 1024 workgroups, the one wasting the fewest row
@@ -1778,7 +1789,7 @@ int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s, bool b
   } else {
     sp = {1, a.Lk};
   }
-  const Geo g = pick_geo((int64_t)a.B * a.H, a.Lq);
+  const Geo g = sp.n == 1 && g_fwd_geo.nt > 0 ? g_fwd_geo : pick_geo((int64_t)a.B * a.H, a.Lq);
   VAESNE_GEO_SWITCH(g, {
     const int nqb = (a.Lq + 2 * NP * NTT - 1) / (2 * NP * NTT);
     dim3 grid((unsigned)((int64_t)a.B * a.H * nqb), (unsigned)sp.n);

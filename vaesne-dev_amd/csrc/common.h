@@ -28,6 +28,16 @@ namespace vaesne {
 
 constexpr int WAVE = 64;
 
+// XCD-aware workgroup id (MI355X_MICROARCH.md §Workgroup dispatch; cdna_hip_programming.md
+// T1): consecutive workgroups are dealt round robin over the 8 XCDs, so block i shares an
+// XCD (and its L2) with i + 8, i + 16, ...  The remap gives every XCD one contiguous range
+// of logical ids (bijective for any count), so neighbouring work -- the four heads of a
+// sequence, whose q | k | v / O / dO slices share 128-byte rows -- runs behind one L2.
+__device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 // Cross-lane exchanges without the LDS: v_permlane32/16_swap (gfx950) and DPP.
 // (__shfl_xor lowers to ds_bpermute_b32: an LDS round trip per exchange.)
 // lane l: {v[l], v[l ^ 32]} as (r0, r1) in some order; r0 + r1 = v[l] + v[l ^ 32]

@@ -78,6 +78,18 @@ struct Tail {
   int mode;            // MODE_FULL (decoder block tail) / MODE_PRE / MODE_POST (encoder halves)
 };
 
+// dropout scale of bit `bit` of a keep word: ik where set, +0 where clear.  Bit
+// arithmetic instead of a lane mask per bit + select (the fused backward kept those
+// masks in SGPR pairs and spilled them into VGPR lanes).  Callers launder the word
+// right before use so the 16 scales are not all computed early and held.
+__device__ __forceinline__ float keep_sc(uint32_t k, int bit, float ik) {
+  return __int_as_float(((int)(k << (31 - bit)) >> 31) & __float_as_int(ik));
+}
+__device__ __forceinline__ uint32_t opaque(uint32_t k) {
+  asm volatile("" : "+v"(k));
+  return k;
+}
+
 // Encoder blocks (util_layers.py:285-309 with the cross-attention over the
 // ~60 / 984 data tokens, too many for the in-register cross attention of the
 // tail) run as two halves around the external cross-attention kernel:
@@ -1071,16 +1083,16 @@ constexpr int LT = 33;        // LDS tile row stride (floats)
 constexpr int TILE = 32 * LT;
 
 // token-major tile: lane (t, h) stores its feature-layout values of token t
-__device__ __forceinline__ void put_fl(float* tile, const float (&v)[16], int lane, bool valid) {
+__device__ __forceinline__ void put_fl(float* tile, const float (&v)[16], int lane) {
   const int t = lane & 31, h = lane >> 5;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) tile[t * LT + F(r, h)] = valid ? v[r] : 0.f;
+  for (int r = 0; r < 16; ++r) tile[t * LT + F(r, h)] = v[r];
 }
 // rows whose half h holds columns [16h, 16h + 16) in order (cross-attention ds / pd)
-__device__ __forceinline__ void put_half(float* tile, const float (&v)[16], int lane, bool valid) {
+__device__ __forceinline__ void put_half(float* tile, const float (&v)[16], int lane) {
   const int t = lane & 31, h = lane >> 5;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) tile[t * LT + 16 * h + k] = valid ? v[k] : 0.f;
+  for (int k = 0; k < 16; ++k) tile[t * LT + 16 * h + k] = v[k];
 }
 // MFMA operand layout: lane (c, h) reads column c of tokens 2s + h
 __device__ __forceinline__ void get_op(const float* tile, float (&o)[16], int lane) {
@@ -1097,9 +1109,8 @@ __device__ __forceinline__ void contract(f16v& acc, const float (&g)[16], const 
     acc = mfma(g[s], x[s], acc);
   }
 }
-__device__ __forceinline__ void colsum_tile(float* tile, const float (&v)[16], int lane, bool valid,
-                                            float& cs) {
-  put_fl(tile, v, lane, valid);
+__device__ __forceinline__ void colsum_tile(float* tile, const float (&v)[16], int lane, float& cs) {
+  put_fl(tile, v, lane);
   float o[16];
   get_op(tile, o, lane);
 #pragma unroll
@@ -1165,8 +1176,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       mv(S.Wo1, S.bo1, t, v, lane);
       load_row(a.x, row, h, t);
       if (DROP && have) {
+        const uint32_t kk = opaque(k0);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] *= ((k0 >> r) & 1u) ? a.inv_keep : 0.f;
+        for (int r = 0; r < 16; ++r) v[r] *= keep_sc(kk, r, a.inv_keep);
       } else if (DROP) {
         float sc[16];
         drop_res(site_key(key, 0), row, h, a.thr, a.inv_keep, sc);
@@ -1179,16 +1191,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       layernorm(v, rs1, xh1);
 #pragma unroll
       for (int r = 0; r < 16; ++r) t[r] = fmaf(xh1[r], S.g1[F(r, h)], S.be1[F(r, h)]);   // x1
-      put_fl(tX1, t, lane, valid);
+      put_fl(tX1, t, lane);
       mv(S.Wq, S.bq, t, q, lane);
-      put_fl(tQ, q, lane, valid);
+      put_fl(tQ, q, lane);
       cross_fwd<LC>(S.kv, a.Lc, q, h, site_key(key, 3), row, DROP, a.thr, a.inv_keep, p, km, c,
                     have);
-      put_fl(tC, c, lane, valid);
+      put_fl(tC, c, lane);
       mv(S.Wo2, S.bo2, c, v, lane);
       if (DROP && have) {
+        const uint32_t kk = opaque(k1);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] *= ((k1 >> r) & 1u) ? a.inv_keep : 0.f;
+        for (int r = 0; r < 16; ++r) v[r] *= keep_sc(kk, r, a.inv_keep);
       } else if (DROP) {
         float sc[16];
         drop_res(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
@@ -1201,15 +1214,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       layernorm(v, rs2, xh2);
 #pragma unroll
       for (int r = 0; r < 16; ++r) t[r] = fmaf(xh2[r], S.g2[F(r, h)], S.be2[F(r, h)]);   // x2
-      put_fl(tX2, t, lane, valid);
+      put_fl(tX2, t, lane);
       mv(S.W1, S.b1, t, f1, lane);
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = gelu(f1[r]);
-      put_fl(tGL, v, lane, valid);
+      put_fl(tGL, v, lane);
       mv(S.W2, S.b2, v, v, lane);
       if (DROP && have) {
+        const uint32_t kk = opaque(k2);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] *= ((k2 >> r) & 1u) ? a.inv_keep : 0.f;
+        for (int r = 0; r < 16; ++r) v[r] *= keep_sc(kk, r, a.inv_keep);
       } else if (DROP) {
         float sc[16];
         drop_res(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
@@ -1223,8 +1237,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
     float go[16], xo[16];
     // ---------------- backward -----------------
+    // tokens past the sequence end (last tile only) get a zero incoming gradient:
+    // every backward value of theirs is then zero, and each contraction / column-sum
+    // term (a backward value times a finite forward one) adds exactly nothing, so
+    // the tile stores need no per-element masks
     float d[16];
     load_row(a.dy, row, h, d);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) d[r] = valid ? d[r] : 0.f;
     if (NEXT) {   // (the next block's in_proj gradient reads only inputs: dec_tail_wgrad)
       f16v acc;
 #pragma unroll
@@ -1237,6 +1257,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           float4 t = *reinterpret_cast<const float4*>(a.dqkv + row * 3 * E + cc * E + 8 * g4 + 4 * h);
           g3[4 * g4] = t.x; g3[4 * g4 + 1] = t.y; g3[4 * g4 + 2] = t.z; g3[4 * g4 + 3] = t.w;
         }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) g3[r] = valid ? g3[r] : 0.f;
         mvt(S.Wn + cc * E * LP, g3, acc, lane);
       }
 #pragma unroll
@@ -1246,13 +1268,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     // LN3
 #pragma unroll
     for (int r = 0; r < 16; ++r) t[r] = d[r] * xh3[r];
-    colsum_tile(tT, d, lane, valid, cBE3);
-    colsum_tile(tT, t, lane, valid, cG3);
+    colsum_tile(tT, d, lane, cBE3);
+    colsum_tile(tT, t, lane, cG3);
     layernorm_bwd(d, xh3, S.g3, rs3, h, d);                 // dv3 (residual into x2)
     // FFN
+    {   // df2
+      const uint32_t kk = opaque(k2);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) t[r] = ((k2 >> r) & 1u) ? d[r] * ik : 0.f;   // df2
-    put_fl(tT, t, lane, valid);
+      for (int r = 0; r < 16; ++r) t[r] = d[r] * keep_sc(kk, r, ik);
+    }
+    put_fl(tT, t, lane);
     get_op(tT, go, lane);
     get_op(tGL, xo, lane);
     contract(aW2, go, xo, cB2);
@@ -1263,7 +1288,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
       for (int r = 0; r < 16; ++r) t[r] = acc[r] * gelu_erf_grad(f1[r]);   // df1
     }
-    put_fl(tT, t, lane, valid);
+    put_fl(tT, t, lane);
     get_op(tT, go, lane);
     get_op(tX2, xo, lane);
     contract(aW1, go, xo, cB1);
@@ -1279,12 +1304,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     // LN2
 #pragma unroll
     for (int r = 0; r < 16; ++r) t[r] = d[r] * xh2[r];
-    colsum_tile(tT, d, lane, valid, cBE2);
-    colsum_tile(tT, t, lane, valid, cG2);
+    colsum_tile(tT, d, lane, cBE2);
+    colsum_tile(tT, t, lane, cG2);
     layernorm_bwd(d, xh2, S.g2, rs2, h, d);                 // dv2 (residual into x1)
+    {   // da2
+      const uint32_t kk = opaque(k1);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) t[r] = ((k1 >> r) & 1u) ? d[r] * ik : 0.f;   // da2
-    put_fl(tT, t, lane, valid);
+      for (int r = 0; r < 16; ++r) t[r] = d[r] * keep_sc(kk, r, ik);
+    }
+    put_fl(tT, t, lane);
     get_op(tT, go, lane);
     get_op(tC, xo, lane);
     contract(aWO2, go, xo, cBO2);
@@ -1296,7 +1324,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
       for (int r = 0; r < 16; ++r) dc[r] = acc[r];
     }
-    put_fl(tC, dc, lane, valid);        // C is consumed: the slot now holds dC
+    put_fl(tC, dc, lane);        // C is consumed: the slot now holds dC
     // cross attention backward (dq -> t)
     {
       float dsv[16], pdv[16];
@@ -1336,18 +1364,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
       float unused = 0.f;
       // dk part: acc[f][j'] += q[t][f] ds[t][j'];  dv part: dC[t][f] pd[t][j']
-      put_half(tT, dsv, lane, valid);
+      put_half(tT, dsv, lane);
       get_op(tQ, go, lane);
       get_op(tT, xo, lane);
       contract(aK, go, xo, unused);
       asm volatile("" ::: "memory");
-      put_half(tT, pdv, lane, valid);
+      put_half(tT, pdv, lane);
       get_op(tC, go, lane);
       get_op(tT, xo, lane);
       contract(aV, go, xo, unused);
       asm volatile("" ::: "memory");
     }
-    put_fl(tT, t, lane, valid);         // dq
+    put_fl(tT, t, lane);         // dq
     get_op(tT, go, lane);
     get_op(tX1, xo, lane);
     contract(aWQ, go, xo, cBQ);
@@ -1363,13 +1391,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     // LN1
 #pragma unroll
     for (int r = 0; r < 16; ++r) t[r] = d[r] * xh1[r];
-    colsum_tile(tT, d, lane, valid, cBE1);
-    colsum_tile(tT, t, lane, valid, cG1);
+    colsum_tile(tT, d, lane, cBE1);
+    colsum_tile(tT, t, lane, cG1);
     layernorm_bwd(d, xh1, S.g1, rs1, h, d);                 // dv1 = dx
     if (valid) store_row(a.dx, row, E, 0, h, d);
+    {   // da1
+      const uint32_t kk = opaque(k0);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) t[r] = ((k0 >> r) & 1u) ? d[r] * ik : 0.f;   // da1
-    put_fl(tT, t, lane, valid);
+      for (int r = 0; r < 16; ++r) t[r] = d[r] * keep_sc(kk, r, ik);
+    }
+    put_fl(tT, t, lane);
     get_op(tT, go, lane);
     get_glob(a.O, E, 0, r0, rend, xo, lane);
     contract(aWO1, go, xo, cBO1);
@@ -1530,7 +1561,7 @@ int dispatch_fused(const Tail& a, int grid, hipStream_t s) {
   return launch_fused<LCV, false, false>(a, grid, s);
   // LC: the compile-time context-token bound (4: photometry decoder, latent_len tokens;
   // 5: spectra decoder, latent_len + the phase token; 8: anything else up to LCMAX)
-  if (a.Lc <= 4) { VAESNE_FUSED_CASE(4) }
+  if (a.Lc == 4) { VAESNE_FUSED_CASE(4) }
   if (a.Lc == 5) { VAESNE_FUSED_CASE(5) }
   VAESNE_FUSED_CASE(8)
 #undef VAESNE_FUSED_CASE
@@ -1557,7 +1588,7 @@ int dispatch(const Tail& a, int grid, float* scr, hipStream_t s) {
   if (next) return FWD ? launch_fwd<LCV, true, false>(a, grid, scr, s) : launch_bwd<LCV, true, false>(a, grid, scr, s);       \
   if (drop) return FWD ? launch_fwd<LCV, false, true>(a, grid, scr, s) : launch_bwd<LCV, false, true>(a, grid, scr, s);       \
   return FWD ? launch_fwd<LCV, false, false>(a, grid, scr, s) : launch_bwd<LCV, false, false>(a, grid, scr, s);
-  if (a.Lc <= 4) { VAESNE_TAIL_CASE(4) }
+  if (a.Lc == 4) { VAESNE_TAIL_CASE(4) }
   if (a.Lc == 5) { VAESNE_TAIL_CASE(5) }
   VAESNE_TAIL_CASE(8)
 #undef VAESNE_TAIL_CASE
