@@ -1062,7 +1062,8 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R, in
 // Backward with dropout (head_dim 8, dQ fused as in attn_bwd_kv_kernel).  Lane owns
 // 2*NP adjacent keys of a distinct sequence; query tiles of TQR queries stream
 // through LDS with, per copy, its dO rows (pre-multiplied by 1/(1-p)) and keep
-// words.  grid.x = Bd*H*key blocks, grid.y = query chunks x copy batches (RC
+// words.  Per score the copies enter only through G = sum_c keep_c dO_c: dV += P G,
+// dS = P (G . V - sum_c D_c).  grid.x = Bd*H*key blocks, grid.y = query chunks x copy batches (RC
 // copies each); several of either write partial dK / dV (slot y) and dQ (slot
 // kb * copy batches + batch) into the workspace, summed in fixed order afterwards.
 constexpr int TQR = 16;
@@ -1189,35 +1190,45 @@ void attn_rep_bwd_kernel(AttnArgs a, int R, int QS) {
 #pragma unroll
           for (int d = 0; d < DH; ++d) s = fma2ru<DH>(k[p][d], qr, d, s);
           pr[p] = ex2(s - li);
-          acc[p] = pr[p] * nD;          // - P sum_c D_c
         }
         // every copy's keep word of this query first (one LDS wait, not one per copy)
         uint32_t wk[RC];
 #pragma unroll
         for (int c = 0; c < RC; ++c) wk[c] = Ws[(c * NWB + wl) * WST + i];
-        // sum over the copies of keep * P * dP (dS = P (keep dP - D), summed)
+        // G = sum over the copies of keep_c * dO_c (dO pre-scaled by 1/(1-p)), per key:
+        // dV += P G and sum_c keep_c dP_c = G . V, so each copy costs its masked dO sum
+        // only (8 packed FMAs per key pair) instead of its own dP and dV terms
+        f2 G[NP][DH];
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+          for (int d = 0; d < DH; ++d) G[p][d] = bc(0.f);
 #pragma unroll
         for (int c = 0; c < RC; ++c) {
           f2 dr[DH / 2];
           lrow2<DH>(Dos + (c * TQR + i) * DH, dr);
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
-            // dP = V . dO as two half chains (even / odd features): no 8-long dependency
-            f2 g0 = mul2_lo(v[p][0], dr[0]), g1 = mul2_hi(v[p][1], dr[0]);
-#pragma unroll
-            for (int d = 2; d < DH; d += 2) {
-              g0 = fma2ru<DH>(v[p][d], dr, d, g0);
-              g1 = fma2ru<DH>(v[p][d + 1], dr, d + 1, g1);
-            }
-            // keep bit -> all-ones / zero mask on P's bits (sign-extending bit extract)
+            // keep bit -> 1.0f / 0.0f (sign-extending bit extract AND the bits of 1.0f)
             const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)wk[c], sh + 2 * p, 1);
             const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)wk[c], sh + 2 * p + 1, 1);
-            const f2 aP = (f2){__uint_as_float(__float_as_uint(pr[p].x) & m0),
-                               __uint_as_float(__float_as_uint(pr[p].y) & m1)};
-            acc[p] = fma2(aP, g0 + g1, acc[p]);
+            const f2 mk = (f2){__uint_as_float(m0 & 0x3f800000u), __uint_as_float(m1 & 0x3f800000u)};
 #pragma unroll
-            for (int d = 0; d < DH; ++d) dv[p][d] = fma2ru<DH>(aP, dr, d, dv[p][d]);
+            for (int d = 0; d < DH; ++d) G[p][d] = fma2ru<DH>(mk, dr, d, G[p][d]);
           }
+        }
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          // dS = P (sum_c keep_c dP_c - sum_c D_c); G . V as two half chains
+          f2 g0 = G[p][0] * v[p][0], g1 = G[p][1] * v[p][1];
+#pragma unroll
+          for (int d = 2; d < DH; d += 2) {
+            g0 = fma2(G[p][d], v[p][d], g0);
+            g1 = fma2(G[p][d + 1], v[p][d + 1], g1);
+          }
+          acc[p] = pr[p] * ((g0 + g1) + nD);
+#pragma unroll
+          for (int d = 0; d < DH; ++d) dv[p][d] = fma2(pr[p], G[p][d], dv[p][d]);
         }
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
@@ -1576,12 +1587,6 @@ Geo g_split = [] {
   if (const char* e = getenv("VAESNE_ATTN_SPLIT_GEO")) sscanf(e, "%d,%d", &f.nt, &f.np);
   return f;
 }();
-// forward-only geometry override for unsplit launches (tuning: VAESNE_ATTN_FWD_GEO="nt,np")
-Geo g_fwd_geo = [] {
-  Geo f{0, 0};
-  if (const char* e = getenv("VAESNE_ATTN_FWD_GEO")) sscanf(e, "%d,%d", &f.nt, &f.np);
-  return f;
-}();
 Geo pick_geo(int64_t bh, int L) {
   if (g_forced.nt > 0) return g_forced;
   // among geometries with >= 1024 workgroups, the one wasting the fewest row
@@ -1789,7 +1794,7 @@ int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s, bool b
   } else {
     sp = {1, a.Lk};
   }
-  const Geo g = sp.n == 1 && g_fwd_geo.nt > 0 ? g_fwd_geo : pick_geo((int64_t)a.B * a.H, a.Lq);
+  const Geo g = pick_geo((int64_t)a.B * a.H, a.Lq);
   VAESNE_GEO_SWITCH(g, {
     const int nqb = (a.Lq + 2 * NP * NTT - 1) / (2 * NP * NTT);
     dim3 grid((unsigned)((int64_t)a.B * a.H * nqb), (unsigned)sp.n);
