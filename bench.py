@@ -95,6 +95,15 @@ def synthetic_batch(B, seed, device, num_bands=None):
     return [(T(pf), T(pt), T(pb), T(pm)), (T(sf), T(sw), T(sp), T(sm))]
 
 
+def _mark(name):
+    """Device wall-clock stamp of a phase boundary (VAESNE_STAMPS=1, tools/stamps.py)."""
+    try:
+        from VAESNe import _stamps
+    except ImportError:            # an older package under profiles/ab_pkg.sh
+        return
+    _stamps.mark(name)
+
+
 class Step:
     """fwd + bwd + pack (graph 1) | all-reduce (N>1) | AdamW update + RNG advance (graph 2)."""
 
@@ -127,8 +136,12 @@ class Step:
                 loss.backward()
                 return loss
         self.opt.zero_grad(set_to_none=True)
+        _mark("step")
         with deferred():   # parameter-gradient sums: one batched launch at the end of backward
-            loss = backward_negated(self.loss_fn(self.model, self.x))   # = (-f).backward()
+            value = self.loss_fn(self.model, self.x)
+            _mark("loss")
+            loss = backward_negated(value)   # = (-f).backward()
+        _mark("backward")
         # the VAEs keep their last posterior parameters (the reference's `_qz_x_params`),
         # which would keep this step's autograd graph -- and its AccumulateGrad nodes,
         # bound to this step's stream -- alive into the next (captured) step
@@ -141,6 +154,7 @@ class Step:
     def update(self):
         self.opt.apply_update()
         self.rng.advance(self.device)   # fresh sampler / dropout draws next step
+        _mark("update")
 
     def eager(self):
         self.fwd_bwd()

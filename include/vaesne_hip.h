@@ -509,6 +509,11 @@ int vaesne_adamw(float* p, const float* g, float* m, float* v, int64_t n, const 
 int vaesne_adamw_steps_advance(float* steps, const uint8_t* active, int P, const int32_t* skip,
                                void* stream);
 int vaesne_step_advance(float* step, int64_t* rng_state, void* stream);
+/* measurement utility (no reference counterpart): when the stream reaches this node,
+ * buf[slot] = the device's constant 100 MHz wall clock.  tools/stamps.py places such
+ * nodes at phase boundaries of the captured training step (VAESNE_STAMPS=1) to time
+ * them without a tracer's per-dispatch cost. */
+int vaesne_stamp(uint64_t* buf, int slot, void* stream);
 /* gather (unpack=0) / scatter (unpack=1) `count` tensors to/from a flat buffer */
 int vaesne_pack(const float* const* srcs, const int64_t* offs, const int64_t* ns, int count,
                 float* dst, int unpack, void* stream);

@@ -22,7 +22,7 @@ import ctypes as C
 
 import torch
 
-from . import _defer, _lib, rng
+from . import _defer, _lib, _stamps, rng
 from . import _ops
 from ._ops import _ws, key_bias_of
 from ._lib import lib, ptr, stream
@@ -244,6 +244,7 @@ class EncChainFn(torch.autograd.Function):
             pos_in += 1 + nctx + 18 * nb
         dfr = _defer.target(all_params, all_out, keep, entries=sum(
             5 * w[0].nb + 2 for w in work) + 2)
+        _stamps.mark("enc_chain_bwd" + "_".join(str(w[2]) for w in work))
         lib.enc_chain_bwd(G, groups, dfr, s)
         grads = []
         for sp, B, Lk, nctx, ctxs, params, dkv, gflat, gviews, wsk, dx0, dy in work:

@@ -22,6 +22,9 @@ monkeypatch.setattr, not the environment):
   step_graph  VAESNE_STEP_GRAPH=0  training_step runs every batch eagerly instead of
                                   replaying a captured hipGraph (_stepgraph.py;
                                   test_gpu_stepgraph.py: bitwise equal)
+  stamps      VAESNE_STAMPS=1     measurement only: device wall-clock stamps at the
+                                  step's phase boundaries (_stamps.py, tools/stamps.py);
+                                  off by default (no extra launches)
 """
 import os
 
@@ -38,3 +41,4 @@ fused_head = _flag("VAESNE_FUSED_HEAD")
 rep_attn = _flag("VAESNE_REP_ATTN")
 defer_grads = _flag("VAESNE_DEFER_GRADS")
 step_graph = _flag("VAESNE_STEP_GRAPH")
+stamps = _flag("VAESNE_STAMPS", default=False)

@@ -108,6 +108,7 @@ SIGNATURES = {
     "vaesne_adamw": (I32, [P, P, P, P, I64, P, P, F32, F32, F32, F32, F32, P, P]),
     "vaesne_adamw_steps_advance": (I32, [P, P, I32, P, P]),
     "vaesne_step_advance": (I32, [P, P, P]),
+    "vaesne_stamp": (I32, [P, I32, P]),
     "vaesne_pack": (I32, [PP, C.POINTER(I64), C.POINTER(I64), I32, P, I32, P]),
 }
 

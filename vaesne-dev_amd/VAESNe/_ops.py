@@ -11,7 +11,7 @@ import math
 
 import torch
 
-from . import _config, _defer, _lib, guard, rng
+from . import _config, _defer, _lib, _stamps, guard, rng
 from ._lib import lib, ptr, stream
 
 ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2}
@@ -646,6 +646,7 @@ class SelfAttnRepFn(torch.autograd.Function):
         E3 = 3 * E
         dqkv = torch.empty_like(qkv)
         ws = _ws(lib.attn_rep_workspace(Bd, R, H, L, dh, p), qkv.device)
+        _stamps.mark(f"rep_bwd{L}")
         lib.attn_rep_bwd(qkv.data_ptr(), L * E3, E3, ptr(kbias), L, o.data_ptr(), L * E, E,
                          lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(), Bd, R, H, L, dh, p,
                          ptr(st), cid, ptr(bits), ptr(ws), stream())
@@ -807,6 +808,7 @@ class LatentHeadFn(torch.autograd.Function):
         dmu = dmu.contiguous() if dmu is not None else None
         dsc = dsc.contiguous() if dsc is not None else None
         db = torch.empty_like(bott)
+        _stamps.mark(f"latent_bwd{bott.shape[-1]}")
         lib.latent_head_bwd(bott.data_ptr(), bott.shape[0], ctx.n, ptr(dmu), ptr(dsc),
                             db.data_ptr(), stream())
         return db, None
@@ -1214,6 +1216,7 @@ class DecTailFn(torch.autograd.Function):
                          _lib.ptr_array(w), p, ptr(st), cid, y.data_ptr(), dy.data_ptr(),
                          ptr(dqkv), ptr(masks), dx.data_ptr(), dO.data_ptr(), dctx.data_ptr(),
                          gflat.data_ptr(), ws.data_ptr(), dfr, stream())
+        _stamps.mark(f"tail_bwd{L}_end")       # the last one (block 1) wins the slot
         gw = gout[:4] + gout[6:]
         return (None, None, dx.view(xshape), dO, dctx, gout[4], gout[5], *gw)
 

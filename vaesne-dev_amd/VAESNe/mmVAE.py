@@ -6,7 +6,7 @@ import torch
 import torch.distributions as dist
 import torch.nn as nn
 
-from . import _config, _ops
+from . import _config, _ops, _stamps
 from .util_layers import ReferencePickle
 
 
@@ -125,6 +125,7 @@ class photospecMMVAE(ReferencePickle, nn.Module):
         preps = [None] * n
         prep_ok = merged and all(hasattr(v, "decode_prepare") for v in self.vaes)
         qz_xs, zss = [None] * n, [None] * n
+        _stamps.mark("fwd")
         with _Branches(side) as br:
             br.to_side(*x[0])
             for m, vae in enumerate(self.vaes):
@@ -133,8 +134,11 @@ class photospecMMVAE(ReferencePickle, nn.Module):
                         br.to_side(*x[1])
                         for d in range(n):
                             preps[d] = self.vaes[d].decode_prepare(x[d], K, groups=n)
+                        _stamps.mark("side:dec_prepare")
                     qz_xs[m], zss[m] = vae.posterior(x[m], K=K)
+                    _stamps.mark(f"enc{m}")
             br.to_main(qz_xs[0].loc, qz_xs[0].scale, zss[0], *_tensors(preps))
+        _stamps.mark("encoders_joined")
         px_zs = _CellMatrix([[None for _ in range(n)] for _ in range(n)])
         if all(z.shape == zss[0].shape for z in zss):
             B = zss[0].shape[1]
@@ -147,7 +151,9 @@ class photospecMMVAE(ReferencePickle, nn.Module):
                     with br.on(d):
                         px_zs.merged[d] = vae.decode_params(zcat, x[d], groups=n,
                                                             prepared=preps[d])
+                        _stamps.mark(f"dec{d}")
                 br.to_main(*px_zs.merged[0])
+            _stamps.mark("decoders_joined")
             for d, vae in enumerate(self.vaes):
                 loc, scale = px_zs.merged[d]
                 for e in range(n):

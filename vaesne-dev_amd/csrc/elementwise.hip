@@ -281,6 +281,8 @@ __global__ void steps_advance_kernel(float* __restrict__ steps, const uint8_t* _
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < P && (!active || active[i])) steps[i] += 1.f;
 }
+// one thread: the constant 100 MHz wall clock into slot `slot` (a vector store)
+__global__ void stamp_kernel(uint64_t* buf, int slot) { buf[slot] = wall_clock64(); }
 __global__ void incr_kernel(float* step, int64_t* rng_state) {
   if (step) *step += 1.f;
   if (rng_state) rng_state[1] += 1;
@@ -522,6 +524,13 @@ VAESNE_API int vaesne_adamw_steps_advance(float* steps, const uint8_t* active, i
   if (P <= 0) return 0;
   hipLaunchKernelGGL(steps_advance_kernel, dim3((P + NT - 1) / NT), dim3(NT), 0,
                      (hipStream_t)stream, steps, active, P, skip);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_stamp(uint64_t* buf, int slot, void* stream) {
+  if (!buf || slot < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, buf, slot);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
