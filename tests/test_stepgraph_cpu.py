@@ -1,5 +1,7 @@
 """The captured-step signature of training_step (VAESNe._stepgraph), on the CPU: what
 makes two batches replay the same hipGraph and what forces a new capture."""
+import os
+
 import torch
 from torch import nn
 
@@ -55,6 +57,23 @@ def test_module_scalars_and_parameters_key_the_network():
     assert SG._signature(net, _fn(1), [torch.zeros(5, 3)], False, params) != s0   # ragged batch
     net[0].weight.requires_grad_(False)             # frozen parameter
     assert SG._signature(net, _fn(1), x, False, params) != s0
+
+
+def test_walk_matches_module_and_parameter_order():
+    """_walk's single traversal gives Module.modules()' scalars and Module.parameters()
+    in their orders, shared submodules / parameters once."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    shared = nn.Linear(2, 2)
+    nets = [nn.Sequential(nn.Linear(3, 4), nn.Sequential(nn.Dropout(0.2), shared), shared),
+            bench.make_model("cpu", 0.1)]
+    for net in nets:
+        scal, params = SG._walk(net)
+        assert [id(p) for p in params] == [id(p) for p in net.parameters()]
+        ref = tuple(v for m in net.modules() for v in m.__dict__.values()
+                    if type(v) in SG._SCALARS)
+        assert scal == ref
 
 
 def test_host_tensors_and_parity_rng_modes_run_eagerly():

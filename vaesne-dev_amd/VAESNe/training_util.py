@@ -82,12 +82,18 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
         if fused and optimizer.grad_hook is None:
             optimizer.grad_hook = D.GradAllReduce(reduction)
     params = [p for p in network.parameters() if p.requires_grad]
-    for x in data_loader:
+    # the next batch is collated and copied to the device while this one runs (its copy
+    # queued behind this batch's work, from pinned memory): the host's DataLoader work
+    # leaves the per-batch idle window.  Not in the host-generator parity mode, where
+    # the model's draws and a dataset's share torch's CPU generator in the reference's
+    # order.
+    ahead = device.type == "cuda" and rng.capturable()
+    batches = iter(data_loader)
+    nxt = _fetch(batches, device, multimodal, ahead)
+    while nxt is not None:
+        x = nxt
+        nxt = None
         optimizer.zero_grad()
-        if multimodal:
-            x = [tuple(_x.to(device) for _x in modality) for modality in x]
-        else:
-            x = tuple(_x.to(device) for _x in x)
         w = 1.0
         empty = False
         if ws > 1:
@@ -110,6 +116,8 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
             # parameter-gradient sums batched into one launch at the end of backward
             with _defer.deferred():
                 loss = backward_negated(loss_fn(network, x))
+        if ahead:
+            nxt = _fetch(batches, device, multimodal, True)
         if ws > 1:
             # every rank all-reduces the same set of gradients (an empty slice, or a
             # parameter the loss does not reach on some rank, gets zeros)
@@ -142,4 +150,22 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
         if release_memory:
             del x
             torch.cuda.empty_cache()
+        if not ahead:
+            nxt = _fetch(batches, device, multimodal, False)
     return total_loss / num_batches
+
+
+def _fetch(batches, device, multimodal, pinned):
+    """The loader's next batch on `device` (training_util.py:38-41), or None at the end.
+    pinned: staged through page-locked memory and copied without blocking the host."""
+    x = next(batches, None)
+    if x is None:
+        return None
+
+    def move(t):
+        if pinned and t.device.type == "cpu":
+            return t.pin_memory().to(device, non_blocking=True)
+        return t.to(device)
+    if multimodal:
+        return [tuple(move(_x) for _x in modality) for modality in x]
+    return tuple(move(_x) for _x in x)
