@@ -222,6 +222,21 @@ __device__ __forceinline__ void drop_res(uint32_t key, int64_t row, int h, uint3
     sc[r] = (bits & 0xffffu) >= thr ? inv_keep : 0.f;
   }
 }
+// the decoder tails' residual dropout: one 32-bit hash per PAIR of adjacent features
+// (F(2k, h), F(2k, h) + 1), the attention kernels' two-round 24-bit-multiply hash over the
+// row's key (attn_pair_bits; 16-bit decisions, p_eff = round(65536 p) / 65536): 1 row
+// hash + 8 pair hashes per lane and site instead of 16 two-round 32-bit-multiply
+// rand_u32.  (The encoder halves keep drop_res: the fused encoder chain matches them.)
+__device__ __forceinline__ void drop_res_pairs(uint32_t key, int64_t row, int h, uint32_t thr,
+                                               float inv_keep, float (&sc)[16]) {
+  const uint32_t rk = attn_row_key(key, (uint32_t)row);
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    const uint32_t bits = attn_pair_bits(rk, (uint32_t)(F(r, h) >> 1));
+    sc[r] = (bits & 0xffffu) >= thr ? inv_keep : 0.f;
+    sc[r + 1] = (bits >> 16) >= thr ? inv_keep : 0.f;
+  }
+}
 __device__ __forceinline__ uint32_t site_key(uint32_t key, uint32_t site) {
   return mix32(key ^ (0x632be5abu * (site + 1)));
 }
@@ -269,22 +284,26 @@ __device__ __forceinline__ void cross_fwd(const float* kv, int Lc, const float (
                                           float inv_keep, float (&p)[H][LC], uint32_t& keepm,
                                           float (&c)[16], bool have_km = false) {
   if (!have_km) keepm = 0u;
+  // keep decisions: one hash per (head, pair of context tokens) over the row's key
+  const uint32_t rk = (drop && !have_km) ? attn_row_key(akey, (uint32_t)row) : 0u;
 #pragma unroll
   for (int hd = 0; hd < H; ++hd) {
     cross_probs<LC>(kv, Lc, q, h, hd, p[hd]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) c[4 * hd + i] = 0.f;
+    uint32_t pb = 0u;
 #pragma unroll
     for (int j = 0; j < LC; ++j) {
       const float pj = p[hd][j];
       float pd = pj;
+      if (drop && !have_km && (j & 1) == 0)
+        pb = attn_pair_bits(rk, (uint32_t)(hd * (LCMAX / 2) + (j >> 1)));
       if (drop && j < Lc) {
         bool kp;
         if (have_km) {
           kp = (keepm >> (hd * LCMAX + j)) & 1u;
         } else {
-          uint32_t bits = rand_u32(akey, ((uint64_t)row * H + hd) * LCMAX + j);
-          kp = (bits & 0xffffu) >= thr;
+          kp = ((j & 1) ? (pb >> 16) : (pb & 0xffffu)) >= thr;
           keepm |= (kp ? 1u : 0u) << (hd * LCMAX + j);
         }
         pd = kp ? pj * inv_keep : 0.f;
@@ -312,19 +331,30 @@ __global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
   __syncthreads();
   const uint32_t key = DROP ? key_of(a.rng, a.call_id) : 0u;
   const int t0 = ch * a.chunk, t1 = min(a.L, t0 + a.chunk);
+  // issue-early / write-late: a tile's O and x rows are loaded while the previous tile
+  // finishes (before its next-block projections), not at the top of its own chain
+  auto row_of = [&](int tt) {
+    const int tok = tt + (lane & 31);
+    return (int64_t)seq * a.L + (tok < t1 ? tok : t1 - 1);
+  };
+  float nO[16], nX[16];
+  if (t0 + wave * 32 < t1) {
+    load_row(a.O, row_of(t0 + wave * 32), h, nO);
+    load_row(a.x, row_of(t0 + wave * 32), h, nX);
+  }
   for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32) {
     const int tok = tt + (lane & 31);
     const bool valid = tok < t1;
-    const int64_t row = (int64_t)seq * a.L + (valid ? tok : t1 - 1);
+    const int64_t row = row_of(tt);
     float xin[16], v[16], xh[16], rs;
-    load_row(a.O, row, h, v);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { v[r] = nO[r]; xin[r] = nX[r]; }
     mv(S.Wo1, S.bo1, v, v, lane);                          // a1
-    load_row(a.x, row, h, xin);
     uint16_t* m16 = reinterpret_cast<uint16_t*>(a.masks) + row * 8 + h;
     const bool keep_masks = DROP && a.masks != nullptr && valid;
     if (DROP) {
       float sc[16];
-      drop_res(site_key(key, 0), row, h, a.thr, a.inv_keep, sc);
+      drop_res_pairs(site_key(key, 0), row, h, a.thr, a.inv_keep, sc);
       uint32_t m = 0u;
 #pragma unroll
       for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; m |= (sc[r] != 0.f ? 1u : 0u) << r; }
@@ -342,7 +372,7 @@ __global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
     mv(S.Wo2, S.bo2, c, v, lane);                           // a2
     if (DROP) {
       float sc[16];
-      drop_res(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
+      drop_res_pairs(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
       uint32_t m = 0u;
 #pragma unroll
       for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; m |= (sc[r] != 0.f ? 1u : 0u) << r; }
@@ -359,7 +389,7 @@ __global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
     mv(S.W2, S.b2, v, v, lane);                             // f
     if (DROP) {
       float sc[16];
-      drop_res(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
+      drop_res_pairs(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
       uint32_t m = 0u;
 #pragma unroll
       for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; m |= (sc[r] != 0.f ? 1u : 0u) << r; }
@@ -371,6 +401,10 @@ __global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = fmaf(xh[r], S.g3[F(r, h)], S.be3[F(r, h)]);    // y
     if (valid) store_row(a.y, row, E, 0, h, v);
+    if (tt + NW * 32 < t1) {
+      load_row(a.O, row_of(tt + NW * 32), h, nO);
+      load_row(a.x, row_of(tt + NW * 32), h, nX);
+    }
     if (NEXT) {
 #pragma unroll
       for (int cc = 0; cc < 3; ++cc) {
@@ -453,7 +487,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         for (int r = 0; r < 16; ++r) v[r] *= ((k0 >> r) & 1u) ? a.inv_keep : 0.f;
       } else if (DROP) {
         float sc[16];
-        drop_res(site_key(key, 0), row, h, a.thr, a.inv_keep, sc);
+        drop_res_pairs(site_key(key, 0), row, h, a.thr, a.inv_keep, sc);
         k0 = 0u;
 #pragma unroll
         for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; k0 |= (sc[r] != 0.f ? 1u : 0u) << r; }
@@ -479,7 +513,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         for (int r = 0; r < 16; ++r) v[r] *= ((k1 >> r) & 1u) ? a.inv_keep : 0.f;
       } else if (DROP) {
         float sc[16];
-        drop_res(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
+        drop_res_pairs(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
         k1 = 0u;
 #pragma unroll
         for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; k1 |= (sc[r] != 0.f ? 1u : 0u) << r; }
@@ -501,7 +535,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         for (int r = 0; r < 16; ++r) v[r] *= ((k2 >> r) & 1u) ? a.inv_keep : 0.f;
       } else if (DROP) {
         float sc[16];
-        drop_res(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
+        drop_res_pairs(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
         k2 = 0u;
 #pragma unroll
         for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; k2 |= (sc[r] != 0.f ? 1u : 0u) << r; }
@@ -1117,23 +1151,10 @@ __device__ __forceinline__ void colsum_tile(float* tile, const float (&v)[16], i
   for (int s = 0; s < 16; ++s) cs += o[s];
   asm volatile("" ::: "memory");
 }
-// operand-layout rows of a global [rows][ld] matrix (columns col0 + c), zero past rmax
-__device__ __forceinline__ void get_glob(const float* p, int ld, int col0, int64_t r0,
-                                         int64_t rmax, float (&o)[16], int lane) {
-  const int c = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const int64_t t = min(r0 + 2 * s + h, rmax - 1);
-    o[s] = p[t * ld + col0 + c];
-  }
-#pragma unroll
-  for (int s = 0; s < 16; ++s) o[s] = r0 + 2 * s + h < rmax ? o[s] : 0.f;
-}
-
 template <int LC, bool NEXT, bool DROP, bool MASKS>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void dec_tail_bwd_fused(Tail a) {
   __shared__ Smem S;
-  __shared__ float Lt[NW][6 * TILE];   // per wave: X1, C / dC, X2, GL, Q, transient
+  __shared__ float Lt[NW][7 * TILE];   // per wave: X1, C / dC, X2, GL, Q, transient, O
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
   const int seq = blockIdx.x;
   stage_all(S, a, NEXT);
@@ -1145,18 +1166,18 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   float* tGL = tX2 + TILE;
   float* tQ = tGL + TILE;
   float* tT = tQ + TILE;
+  float* tO = tT + TILE;      // the attention output rows, for the out-projection's dW
   const uint32_t key = DROP ? key_of(a.rng, a.call_id) : 0u;
   const float scale = 0.35355339059327373f;
   const float ik = DROP ? a.inv_keep : 1.f;
   f16v aWO1 = {}, aWQ = {}, aWO2 = {}, aW1 = {}, aW2 = {}, aK = {}, aV = {};
   float cBO1 = 0.f, cBQ = 0.f, cBO2 = 0.f, cB1 = 0.f, cB2 = 0.f;
   float cG1 = 0.f, cBE1 = 0.f, cG2 = 0.f, cBE2 = 0.f, cG3 = 0.f, cBE3 = 0.f;
-  const int64_t base = (int64_t)seq * a.L, rend = base + a.L;
+  const int64_t base = (int64_t)seq * a.L;
   for (int tt = wave * 32; tt < a.L; tt += NW * 32) {
     const int tok = tt + (lane & 31);
     const bool valid = tok < a.L;
     const int64_t row = base + (valid ? tok : a.L - 1);
-    const int64_t r0 = base + tt;
     // ---------------- forward recompute -----------------
     float xh1[16], xh2[16], xh3[16], f1[16], q[16];
     float rs1, rs2, rs3;
@@ -1173,6 +1194,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     {
       float v[16], t[16], c[16], p[H][LC];
       load_row(a.O, row, h, t);
+      put_fl(tO, t, lane);    // read back at the tile's end (the dW_o1 operand): LDS, not HBM
       mv(S.Wo1, S.bo1, t, v, lane);
       load_row(a.x, row, h, t);
       if (DROP && have) {
@@ -1181,7 +1203,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         for (int r = 0; r < 16; ++r) v[r] *= keep_sc(kk, r, a.inv_keep);
       } else if (DROP) {
         float sc[16];
-        drop_res(site_key(key, 0), row, h, a.thr, a.inv_keep, sc);
+        drop_res_pairs(site_key(key, 0), row, h, a.thr, a.inv_keep, sc);
         k0 = 0u;
 #pragma unroll
         for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; k0 |= (sc[r] != 0.f ? 1u : 0u) << r; }
@@ -1204,7 +1226,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         for (int r = 0; r < 16; ++r) v[r] *= keep_sc(kk, r, a.inv_keep);
       } else if (DROP) {
         float sc[16];
-        drop_res(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
+        drop_res_pairs(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
         k1 = 0u;
 #pragma unroll
         for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; k1 |= (sc[r] != 0.f ? 1u : 0u) << r; }
@@ -1226,7 +1248,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         for (int r = 0; r < 16; ++r) v[r] *= keep_sc(kk, r, a.inv_keep);
       } else if (DROP) {
         float sc[16];
-        drop_res(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
+        drop_res_pairs(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
         k2 = 0u;
 #pragma unroll
         for (int r = 0; r < 16; ++r) { v[r] *= sc[r]; k2 |= (sc[r] != 0.f ? 1u : 0u) << r; }
@@ -1402,7 +1424,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     }
     put_fl(tT, t, lane);
     get_op(tT, go, lane);
-    get_glob(a.O, E, 0, r0, rend, xo, lane);
+    get_op(tO, xo, lane);
     contract(aWO1, go, xo, cBO1);
     asm volatile("" ::: "memory");
     {
