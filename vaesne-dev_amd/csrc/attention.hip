@@ -92,6 +92,21 @@ __device__ __forceinline__ void lrow(const float* s, float (&r)[DH]) {
   }
 }
 
+// keep-bitmap assembly: w = 2 w + (this lane's bit of the lane mask m) -- one
+// v_addc with the compare's lane mask as carry-in, instead of select-to-0/1, shift, or.
+// Bits enter at the bottom, so after n pushes the first decision sits at bit n - 1:
+// keep_word() shifts and bit-reverses a word of n pushes into the bitmap layout (key j
+// of the word at bit j).
+__device__ __forceinline__ uint32_t push_bit(uint32_t w, uint64_t m) {
+  uint32_t r;
+  uint64_t co;
+  asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(w), "s"(m));
+  return r;
+}
+__device__ __forceinline__ uint32_t keep_word(uint32_t w, int n) {
+  return __builtin_bitreverse32(w << (32 - n));
+}
+
 // broadcast-operand packed FMA: c + a * {r_d, r_d} with r_d one half of an LDS
 // row held as register pairs.  The op_sel / op_sel_hi forms read the scalar
 // straight out of the pair (the compiler otherwise copies it into a fresh pair
@@ -347,18 +362,19 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
           }
         } else if (DROP) {
           const uint32_t kpm = attn_keypair_mix(skey, (uint32_t)((kt + g0 + u) >> 1));
-          const int sh = (g0 + u) & 31;
-          uint32_t kk[R];
+          bool klo[R], khi[R];
 #pragma unroll
           for (int t = 0; t < R; ++t) {
             const uint32_t bits = attn_pair_bits_mixed(rk[t], kpm);
-            kk[t] = ((bits & 0xffffu) >= a.thr ? 1u : 0u) | ((bits >> 16) >= a.thr ? 2u : 0u);
-            w[t] |= kk[t] << sh;
+            klo[t] = (bits & 0xffffu) >= a.thr;
+            khi[t] = (bits >> 16) >= a.thr;
+            w[t] = push_bit(push_bit(w[t], __builtin_amdgcn_ballot_w64(klo[t])),
+                            __builtin_amdgcn_ballot_w64(khi[t]));
           }
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
-            p0[p] = sel2(kk[2 * p] & 1u, kk[2 * p + 1] & 1u, p0[p]);
-            p1[p] = sel2(kk[2 * p] & 2u, kk[2 * p + 1] & 2u, p1[p]);
+            p0[p] = sel2(klo[2 * p], klo[2 * p + 1], p0[p]);
+            p1[p] = sel2(khi[2 * p], khi[2 * p + 1], p1[p]);
           }
         }
         f2 v0[DH / 2], v1[DH / 2];
@@ -374,10 +390,10 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
         }
       }
       if (DROP && !BITSIN && (((g0 + 8) & 31) == 0 || g0 + 8 >= kend)) {
-        const int word = (kt + g0) >> 5;
+        const int word = (kt + g0) >> 5, n = (g0 & 31) + 8;
 #pragma unroll
         for (int t = 0; t < R; ++t) {
-          if (qi[t] < a.Lq) bitp[(int64_t)word * a.Lq + qi[t]] = w[t];
+          if (qi[t] < a.Lq) bitp[(int64_t)word * a.Lq + qi[t]] = keep_word(w[t], n);
           w[t] = 0u;
         }
       }
@@ -982,20 +998,21 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R, in
         lrow2<DH>(Vs + (g0 + u + 1) * DH, v1);
         if (DROP) {
           const uint32_t kpm = attn_keypair_mix(skey, (uint32_t)((kt + g0 + u) >> 1));
-          const int sh = (g0 + u) & 31;
 #pragma unroll
           for (int c = 0; c < NC; ++c) {
-            uint32_t kk[R2];
+            bool klo[R2], khi[R2];
 #pragma unroll
             for (int t = 0; t < R2; ++t) {
               const uint32_t bits = attn_pair_bits_mixed(rk[c][t], kpm);
-              kk[t] = ((bits & 0xffffu) >= a.thr ? 1u : 0u) | ((bits >> 16) >= a.thr ? 2u : 0u);
-              w[c][t] |= kk[t] << sh;
+              klo[t] = (bits & 0xffffu) >= a.thr;
+              khi[t] = (bits >> 16) >= a.thr;
+              w[c][t] = push_bit(push_bit(w[c][t], __builtin_amdgcn_ballot_w64(klo[t])),
+                                 __builtin_amdgcn_ballot_w64(khi[t]));
             }
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
-              const f2 a0 = sel2(kk[2 * p] & 1u, kk[2 * p + 1] & 1u, p0[p]);
-              const f2 a1 = sel2(kk[2 * p] & 2u, kk[2 * p + 1] & 2u, p1[p]);
+              const f2 a0 = sel2(klo[2 * p], klo[2 * p + 1], p0[p]);
+              const f2 a1 = sel2(khi[2 * p], khi[2 * p + 1], p1[p]);
 #pragma unroll
               for (int d = 0; d < DH; ++d) {
                 o[c][p][d] = fma2r<DH>(a0, v0, d, o[c][p][d]);
@@ -1014,13 +1031,13 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R, in
         }
       }
       if (DROP && (((g0 + 8) & 31) == 0 || g0 + 8 >= kend)) {
-        const int word = (kt + g0) >> 5;
+        const int word = (kt + g0) >> 5, n = (g0 & 31) + 8;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           if (c0 + c < R) {
 #pragma unroll
             for (int t = 0; t < R2; ++t)
-              if (qi[t] < a.Lq) bitp[c][(int64_t)word * a.Lq + qi[t]] = w[c][t];
+              if (qi[t] < a.Lq) bitp[c][(int64_t)word * a.Lq + qi[t]] = keep_word(w[c][t], n);
           }
 #pragma unroll
           for (int t = 0; t < R2; ++t) w[c][t] = 0u;
