@@ -30,6 +30,11 @@ using namespace vaesne;
 namespace {
 
 constexpr int TK = 64;   // keys (or queries) per LDS tile
+// running-max origin of the forward kernels before any key is seen: finite, so neither
+// the exponent origin nor a rescale needs a -inf fix-up per group (a row's first finite
+// score always moves it, through the lazy rescale, before any exponential reads it;
+// fully masked rows keep it with l = 0 -> o = NaN, lse = -inf, as before)
+constexpr float M_INIT = -1e30f;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -143,6 +148,19 @@ __device__ __forceinline__ f2 mul2_hi(f2 a, f2 b) {
   asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+// the first FMA of a score chain: a * {b.x, b.x} + {c_H, c_H}, c = a pair of key biases
+// (H = 0: its first key, 1: its second) read straight out of the pair -- no register
+// copies to broadcast the bias into a fresh accumulator pair
+template <int H>
+__device__ __forceinline__ f2 fma2_bias(f2 a, f2 b, f2 c) {
+  f2 r;
+  if (H == 0)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]"
+        : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 template <int DH>
 __device__ __forceinline__ f2 fma2r(f2 a, const f2 (&r)[DH / 2], int d, f2 c) {
   return (d & 1) ? fma2_hi(a, r[d >> 1], c) : fma2_lo(a, r[d >> 1], c);
@@ -197,7 +215,7 @@ template <int DH, int NTT, int NP, bool DROP, bool BITSIN = false>
 __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Ks[TK * DH];
   __shared__ __attribute__((aligned(16))) float Vs[TK * DH];
-  __shared__ float Kb[TK];
+  __shared__ __attribute__((aligned(16))) float Kb[TK];
   __shared__ uint32_t Sp[BITSIN ? 256 : 1];              // byte -> bits at even positions
   __shared__ __attribute__((aligned(16))) float4 Mn[BITSIN ? 16 : 1];   // nibble -> masks
   if (BITSIN) {
@@ -236,7 +254,7 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
         q[p][d] = (f2){t0[d], t1[d]} * a.scale_log2;
         o[p][d] = bc(0.f);
       }
-      m[p] = bc(-INFINITY);
+      m[p] = bc(M_INIT);
       l[p] = bc(0.f);
     }
   }
@@ -304,12 +322,13 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
       for (int u = 0; u < 8; ++u) {
         f2 kr[DH / 2];
         lrow2<DH>(Ks + (g0 + u) * DH, kr);
-        const float kb = Kb[g0 + u];
+        const f2 kb2 = *reinterpret_cast<const f2*>(Kb + g0 + (u & ~1));
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
-          f2 acc = bc(kb);
+          // acc = kb + q . k, the chain's first FMA reading the bias from its pair
+          f2 acc = (u & 1) ? fma2_bias<1>(q[p][0], kr[0], kb2) : fma2_bias<0>(q[p][0], kr[0], kb2);
 #pragma unroll
-          for (int d = 0; d < DH; ++d) acc = fma2r<DH>(q[p][d], kr, d, acc);
+          for (int d = 1; d < DH; ++d) acc = fma2r<DH>(q[p][d], kr, d, acc);
           s[p][u] = acc;
           x[p] = __builtin_elementwise_max(x[p], acc);
         }
@@ -323,10 +342,7 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
       if (__any(move)) {
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
-          // rows whose keys are all masked so far keep m = -inf: exponent origin 0
-          const f2 mo = (f2){m[p].x == -INFINITY ? 0.f : m[p].x, m[p].y == -INFINITY ? 0.f : m[p].y};
-          const f2 mn = (f2){x[p].x == -INFINITY ? 0.f : x[p].x, x[p].y == -INFINITY ? 0.f : x[p].y};
-          const f2 c = ex2(mo - mn);
+          const f2 c = ex2(m[p] - x[p]);     // 0 from M_INIT
           m[p] = x[p];
           l[p] *= c;
 #pragma unroll
@@ -336,7 +352,7 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
       f2 mu[NP];
 #pragma unroll
       for (int p = 0; p < NP; ++p)
-        mu[p] = (f2){m[p].x == -INFINITY ? 0.f : m[p].x, m[p].y == -INFINITY ? 0.f : m[p].y};
+        mu[p] = m[p];
       uint32_t z[NP];   // BITSIN: rows (2p, 2p+1) keep bits of these 8 keys, interleaved
       if (DROP && BITSIN) {
         const int ws = g0 >> 5, sh = g0 & 31;
@@ -368,9 +384,13 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
             const uint32_t bits = attn_pair_bits_mixed(rk[t], kpm);
             klo[t] = (bits & 0xffffu) >= a.thr;
             khi[t] = (bits >> 16) >= a.thr;
+          }
+          // every row's compares first: the lane masks are read by the v_addc a few
+          // instructions after they are written (no hazard wait states)
+#pragma unroll
+          for (int t = 0; t < R; ++t)
             w[t] = push_bit(push_bit(w[t], __builtin_amdgcn_ballot_w64(klo[t])),
                             __builtin_amdgcn_ballot_w64(khi[t]));
-          }
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
             p0[p] = sel2(klo[2 * p], klo[2 * p + 1], p0[p]);
@@ -754,7 +774,7 @@ template <int DH, int NTT, int NP, bool DROP>
 __global__ __launch_bounds__(NTT) void attn_bwd_q_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Ks[TK * DH];
   __shared__ __attribute__((aligned(16))) float Vs[TK * DH];
-  __shared__ float Kb[TK];
+  __shared__ __attribute__((aligned(16))) float Kb[TK];
   constexpr int R = 2 * NP;
   constexpr int QB = R * NTT;
   const int nqb = (a.Lq + QB - 1) / QB;
@@ -880,7 +900,7 @@ template <int DH, int NTT, int NP, int RC, bool DROP>
 __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R, int qb0, int nqbs) {
   __shared__ __attribute__((aligned(16))) float Ks[TK * DH];
   __shared__ __attribute__((aligned(16))) float Vs[TK * DH];
-  __shared__ float Kb[TK];
+  __shared__ __attribute__((aligned(16))) float Kb[TK];
   constexpr int R2 = 2 * NP;              // queries per lane (pairs p = {2p, 2p + 1})
   constexpr int QB = R2 * NTT;
   constexpr int NC = DROP ? RC : 1;       // accumulator sets (no dropout: one for all copies)
@@ -909,7 +929,7 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R, in
       for (int c = 0; c < NC; ++c)
 #pragma unroll
         for (int d = 0; d < DH; ++d) o[c][p][d] = bc(0.f);
-      m[p] = bc(-INFINITY);
+      m[p] = bc(M_INIT);
       l[p] = bc(0.f);
     }
   }
@@ -952,12 +972,13 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R, in
       for (int u = 0; u < 8; ++u) {
         f2 kr[DH / 2];
         lrow2<DH>(Ks + (g0 + u) * DH, kr);
-        const float kb = Kb[g0 + u];
+        const f2 kb2 = *reinterpret_cast<const f2*>(Kb + g0 + (u & ~1));
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
-          f2 acc = bc(kb);
+          // acc = kb + q . k, the chain's first FMA reading the bias from its pair
+          f2 acc = (u & 1) ? fma2_bias<1>(q[p][0], kr[0], kb2) : fma2_bias<0>(q[p][0], kr[0], kb2);
 #pragma unroll
-          for (int d = 0; d < DH; ++d) acc = fma2r<DH>(q[p][d], kr, d, acc);
+          for (int d = 1; d < DH; ++d) acc = fma2r<DH>(q[p][d], kr, d, acc);
           s[p][u] = acc;
           x[p] = __builtin_elementwise_max(x[p], acc);
         }
@@ -969,9 +990,7 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R, in
       if (__any(move)) {
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
-          const f2 mo = (f2){m[p].x == -INFINITY ? 0.f : m[p].x, m[p].y == -INFINITY ? 0.f : m[p].y};
-          const f2 mn = (f2){x[p].x == -INFINITY ? 0.f : x[p].x, x[p].y == -INFINITY ? 0.f : x[p].y};
-          const f2 cf = ex2(mo - mn);
+          const f2 cf = ex2(m[p] - x[p]);    // 0 from M_INIT
           m[p] = x[p];
           l[p] *= cf;
 #pragma unroll
@@ -983,7 +1002,7 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R, in
       f2 mu[NP];
 #pragma unroll
       for (int p = 0; p < NP; ++p)
-        mu[p] = (f2){m[p].x == -INFINITY ? 0.f : m[p].x, m[p].y == -INFINITY ? 0.f : m[p].y};
+        mu[p] = m[p];
 #pragma unroll
       for (int u = 0; u < 8; u += 2) {
         f2 p0[NP], p1[NP];
@@ -1006,9 +1025,11 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R, in
               const uint32_t bits = attn_pair_bits_mixed(rk[c][t], kpm);
               klo[t] = (bits & 0xffffu) >= a.thr;
               khi[t] = (bits >> 16) >= a.thr;
+            }
+#pragma unroll
+            for (int t = 0; t < R2; ++t)
               w[c][t] = push_bit(push_bit(w[c][t], __builtin_amdgcn_ballot_w64(klo[t])),
                                  __builtin_amdgcn_ballot_w64(khi[t]));
-            }
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
               const f2 a0 = sel2(klo[2 * p], klo[2 * p + 1], p0[p]);
