@@ -1121,7 +1121,11 @@ void attn_rep_bwd_kernel(AttnArgs a, int R, int QS) {
   __shared__ __attribute__((aligned(16))) float Dos[RC * TQR * DH];
   __shared__ float Ls[TQR], Dsum[TQR], Dc[RC * TQR];
   __shared__ uint32_t Ws[RC * NWB * WST];
+  // keep-mask table: 2-bit keep pattern of a key pair -> {keep0, keep1} as 0/1 floats (one
+  // bit extract and one LDS read per copy and key pair instead of 2 extracts and 2 ANDs)
+  __shared__ __attribute__((aligned(8))) f2 Mk[4];
   __shared__ __attribute__((aligned(16))) float Qw[NWV * TQR * DH];
+  if (threadIdx.x < 4) Mk[threadIdx.x] = (f2){(float)(threadIdx.x & 1), (float)(threadIdx.x >> 1)};
   const int nkb = (a.Lk + KB - 1) / KB;
   const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
   const int kb = wg % nkb;
@@ -1247,10 +1251,7 @@ void attn_rep_bwd_kernel(AttnArgs a, int R, int QS) {
           lrow2<DH>(Dos + (c * TQR + i) * DH, dr);
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
-            // keep bit -> 1.0f / 0.0f (sign-extending bit extract AND the bits of 1.0f)
-            const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)wk[c], sh + 2 * p, 1);
-            const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)wk[c], sh + 2 * p + 1, 1);
-            const f2 mk = (f2){__uint_as_float(m0 & 0x3f800000u), __uint_as_float(m1 & 0x3f800000u)};
+            const f2 mk = Mk[__builtin_amdgcn_ubfe(wk[c], sh + 2 * p, 2)];   // {keep0, keep1}
 #pragma unroll
             for (int d = 0; d < DH; ++d) G[p][d] = fma2ru<DH>(mk, dr, d, G[p][d]);
           }
