@@ -246,6 +246,7 @@ class EncChainFn(torch.autograd.Function):
             5 * w[0].nb + 2 for w in work) + 2)
         _stamps.mark("enc_chain_bwd" + "_".join(str(w[2]) for w in work))
         lib.enc_chain_bwd(G, groups, dfr, s)
+        _stamps.mark("enc_chain_bwd_end")
         grads = []
         for sp, B, Lk, nctx, ctxs, params, dkv, gflat, gviews, wsk, dx0, dy in work:
             nb = sp.nb
@@ -275,6 +276,7 @@ class EncChainFn(torch.autograd.Function):
                          None, dctxs[blk].data_ptr(), E, M, 0) for blk in range(nb)]
                 lib.linear_bwd_data_group(nb, _ops.lin_groups(rows), E, 2 * E, s)
             grads += [dx0] + dctxs + gviews
+            _stamps.mark(f"enc_dctx{Lk}")
         out = [None]
         for i, gr in enumerate(grads):
             out.append(gr if ng[1 + i] else None)

@@ -25,7 +25,7 @@ import ctypes as C
 
 import torch
 
-from . import _config
+from . import _config, _stamps
 from ._lib import lib
 
 
@@ -142,6 +142,7 @@ def flush():
     for s in _S.streams:
         if s != cur:
             cur.wait_stream(s)
+    _stamps.mark("flush")
     lib.colsum_flush(C.byref(_S.clist), cur.cuda_stream)
     for t in _S.keep:
         t.record_stream(cur)

@@ -564,11 +564,13 @@ class SelfAttnFn(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         b, d = qkv.data_ptr(), dqkv.data_ptr()
         ws = _attn_ws(B, H, L, L, dh, 1, qkv.device)
+        _stamps.mark(f"self_bwd_B{B}_L{L}")
         _timed("attn_bwd", B * H * L * L, lambda: lib.attn_bwd(
             b, L * E3, E3, b + 4 * E, L * E3, E3, b + 8 * E, L * E3, E3, ptr(kbias), L,
             o.data_ptr(), L * E, E, lse.data_ptr(), do.data_ptr(), L * E, E,
             d, L * E3, E3, d + 4 * E, L * E3, E3, d + 8 * E, L * E3, E3,
             B, H, L, L, dh, p, ptr(st), cid, ptr(bits), ptr(ws), stream()))
+        _stamps.mark(f"self_bwd_B{B}_L{L}_end")
         return dqkv, None, None, None
 
 
@@ -650,6 +652,7 @@ class SelfAttnRepFn(torch.autograd.Function):
         lib.attn_rep_bwd(qkv.data_ptr(), L * E3, E3, ptr(kbias), L, o.data_ptr(), L * E, E,
                          lse.data_ptr(), do.data_ptr(), dqkv.data_ptr(), Bd, R, H, L, dh, p,
                          ptr(st), cid, ptr(bits), ptr(ws), stream())
+        _stamps.mark(f"rep_bwd{L}_end")
         return dqkv, None, None, None, None
 
 
