@@ -31,8 +31,12 @@ Rank 0 prints ONE JSON line (value = whole-job SN pairs/s).  Beside it:
                  sample (rank 0, N=1 only);
   parity       : on the reference's own golden fixture of THIS configuration
                  (tests/golden/mmvae_cfg5_b16.npz: B=16, K=8, dropout off, injected
-                 noise): elbo_rel_err = |loss_build - loss_ref| / |loss_ref|, and the
-                 max-rel errors of the latent mu / scale.
+                 noise): elbo_rel_err = |loss_build - loss_ref| / |loss_ref|, the
+                 max-rel errors of the latent mu / scale and decoder locs
+                 (BASELINE.md §3), and the backward: grad_rel_err (full gradient
+                 tensors) and grad_norm_rel_err (every parameter's gradient norm).
+                 The cfg 2/3/4 side lines carry the same against their own fixtures
+                 (elbo_spec_cfg2, elbo_photo_cfg3, mmvae_cfg4) and a CPU baseline each.
 """
 import argparse
 import contextlib
@@ -170,14 +174,20 @@ class Step:
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        try:
+            from VAESNe._capture import guarded   # refuses topologies that crash the capture
+        except ImportError:            # an older package under profiles/ab_pkg.sh
+            guarded = contextlib.nullcontext
         if self.world == 1:
             with torch.cuda.graph(g1):
-                self.fwd_bwd()
-                self.update()
+                with guarded():
+                    self.fwd_bwd()
+                    self.update()
             self.graphs = (g1, None)
         else:
             with torch.cuda.graph(g1):
-                self.fwd_bwd()
+                with guarded():
+                    self.fwd_bwd()
             with torch.cuda.graph(g2):
                 self.update()
             self.graphs = (g1, g2)
@@ -505,34 +515,70 @@ def _cpu_model():
     return "unknown"
 
 
-def parity(device):
-    """The benchmarked configuration (B=16, K=8, cfg 5) on the reference's own golden
-    fixture: identical parameters, inputs and Laplace noise, dropout off.  Returns
-    the ELBO (m_iwae) rel-err and the max-rel errors of the latent mu / scale and
-    of the decoder locations."""
+def _rel(a, b):
+    a = a.detach().double().cpu().numpy()
+    return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1e-30))
+
+
+def golden_parity(device, name, forward_detail=False):
+    """One of the reference's own golden fixtures (tests/golden/<name>.npz, written by
+    tests/golden/gen_golden.py from the reference package): identical parameters,
+    inputs and Laplace noise, dropout off.  Forward AND backward on the HIP path, the
+    backward under the training step's deferred gradient sums (training_util.py):
+      elbo_rel_err      |loss - ref| / |ref|  (m_iwae for an MMVAE, losses.py:78-93;
+                        elbo otherwise, losses.py:16-24)
+      grad_rel_err      max over the fixture's full-gradient tensors of
+                        max|g - ref| / max|ref|
+      grad_norm_rel_err max over EVERY trainable parameter of
+                        |‖g‖ - ref| / max(ref, 1e-3)  (tests/test_gpu_parity.py's bound)
+    With forward_detail also the max-rel errors of the latent mu / scale and of the
+    decoder locations."""
     from VAESNe import rng
-    from VAESNe.losses import m_iwae
+    from VAESNe._defer import deferred
+    from VAESNe.losses import elbo, m_iwae
+    from VAESNe.training_util import backward_negated
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from conftest import build_model, golden_us, golden_x, load_golden
-    g = load_golden("mmvae_cfg5_b16")
+    g = load_golden(name)
     c = g["config"]
+    mm = c["kind"] == "mmvae"
     model = build_model(c, device=device)
     model.train()
     x = golden_x(g, device)
-
-    def rel(a, b):
-        a = a.detach().double().cpu().numpy()
-        return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1e-30))
-    with torch.no_grad(), rng.inject_uniform(golden_us(g)):
-        qz, px, _ = model(x, K=c["K"])
-    with torch.no_grad(), rng.inject_uniform(golden_us(g)):
-        loss = -m_iwae(model, x, K=c["K"])
+    out = {}
+    if forward_detail:
+        with torch.no_grad(), rng.inject_uniform(golden_us(g)):
+            qz, px, _ = model(x, K=c["K"])
+        out.update(mu_rel_err=max(_rel(qz[m].loc, g[f"mu{m}"]) for m in range(2)),
+                   scale_rel_err=max(_rel(qz[m].scale, g[f"scale{m}"]) for m in range(2)),
+                   loc_rel_err=max(_rel(px[e][d].loc, g[f"loc{e}{d}"])
+                                   for e in range(2) for d in range(2)))
+        del qz, px
+    for p in model.parameters():
+        p.grad = None
+    with deferred(), rng.inject_uniform(golden_us(g)):
+        value = m_iwae(model, x, K=c["K"]) if mm else elbo(model, x, K=c["K"])
+        loss = backward_negated(value)
     ref = float(g["loss"])
-    return dict(elbo_rel_err=abs(loss.item() - ref) / abs(ref),
-                mu_rel_err=max(rel(qz[m].loc, g[f"mu{m}"]) for m in range(2)),
-                scale_rel_err=max(rel(qz[m].scale, g[f"scale{m}"]) for m in range(2)),
-                loc_rel_err=max(rel(px[e][d].loc, g[f"loc{e}{d}"]) for e in range(2) for d in range(2)),
-                parity_fixture="tests/golden/mmvae_cfg5_b16.npz (B=16, K=8: this workload)")
+    params = dict(model.named_parameters())
+    names = json.loads(str(g["grad_names"]))
+    gn = max(abs(params[k].grad.norm().item() - n) / max(float(n), 1e-3)
+             for k, n in zip(names, g["grad_norms"]))
+    full = [k[5:] for k in g if k.startswith("grad:")]
+    ge = max(_rel(params[k].grad, g["grad:" + k]) for k in full)
+    out.update(elbo_rel_err=abs(loss.item() - ref) / abs(ref), grad_rel_err=ge,
+               grad_norm_rel_err=gn, grad_tensors=len(full), grad_norms=len(names))
+    return out
+
+
+def parity(device):
+    """The benchmarked configuration (B=16, K=8, cfg 5) on the reference's own golden
+    fixture (mmvae_cfg5_b16): forward (loss, mu, scale, decoder locs) and backward
+    (the fixture's 12 full gradient tensors and the gradient norm of every parameter
+    tensor)."""
+    out = golden_parity(device, "mmvae_cfg5_b16", forward_detail=True)
+    out["parity_fixture"] = "tests/golden/mmvae_cfg5_b16.npz (B=16, K=8: this workload)"
+    return out
 
 
 def extras(device, use_graph, reps=10):
@@ -688,8 +734,18 @@ def config_lines(device, use_graph, steps=10, warmup=3):
                                         beta=1.0),
             src="cannon/test_photospectra.py:90-133"),
     }
+    fixtures = {"cfg2_spectra_elbo": "elbo_spec_cfg2", "cfg3_photometry_elbo": "elbo_photo_cfg3",
+                "cfg4_mmvae_K2": "mmvae_cfg4"}
     out = {}
     for name, c in cases.items():
+        # parity first, on the reference's fixture of this config (its own batch of 4)
+        try:
+            par = golden_parity(device, fixtures[name])
+            par["parity_fixture"] = f"tests/golden/{fixtures[name]}.npz"
+        except Exception as e:
+            par = dict(elbo_rel_err=None, parity_error=repr(e))
+            log(f"[bench] {name}: parity failed: {e!r}")
+        torch.cuda.empty_cache()
         torch.manual_seed(0)
         model = c["make"]().to(device)
         nb = 6 if name == "cfg4_mmvae_K2" else 2
@@ -710,19 +766,74 @@ def config_lines(device, use_graph, steps=10, warmup=3):
                          finite_loss=math.isfinite(step.loss.item()), script=c["src"],
                          gflop_per_sample=c["gf"],
                          matmul_tflops=round(v * c["gf"] / 1e3, 3),
-                         frac_fp32_peak=round(v * c["gf"] / 1e3 / FP32_PEAK_TFLOPS, 4))
+                         frac_fp32_peak=round(v * c["gf"] / 1e3 / FP32_PEAK_TFLOPS, 4), **par)
         del step, model, x
         torch.cuda.empty_cache()
     return out
 
 
-def training_step_script(device, batches=4):
+def config_cpu_baselines():
+    """the CPU oracle beside each of cfg 2/3/4 (the configs of
+    config_lines), one training step (train mode, dropout 0.1, AdamW) on a bounded
+    sample after a 1-sample warm-up.  Per-sample cost is linear in B (no cross-sample
+    term in elbo or m_iwae)."""
+    from oracle import vaesne_oracle as O
+    cores, _, _ = _usable_cores()
+    torch.set_num_threads(cores)
+    eps = torch.finfo(torch.float32).eps
+    cases = {
+        "cfg2_spectra_elbo": (O.VaeCfg("spec", beta=1.0), 8, 1, 2, 2.5e-4),
+        "cfg3_photometry_elbo": (O.VaeCfg("photo", num_bands=2, latent_dim=2, beta=0.5), 32, 1, 2, 2.5e-4),
+        "cfg4_mmvae_K2": (O.MMVAECfg(photo=O.VaeCfg("photo", num_bands=6), spec=O.VaeCfg("spec"),
+                                     beta=1.0), 4, 2, 6, 1e-4),
+    }
+    out = {}
+    for name, (cfg, B, K, nb, lr) in cases.items():
+        g = torch.Generator().manual_seed(0)
+        p = O.make_params(cfg, lambda k, shp: (torch.randn(shp, generator=g) / math.sqrt(shp[-1])).numpy()
+                          if "_pz" not in k else None, requires_grad=True)
+        st = O.AdamWState(lr=lr)
+        mm = isinstance(cfg, O.MMVAECfg)
+
+        def one(nb_):
+            x = synthetic_batch(nb_, 99, "cpu", num_bands=nb)
+            for v in p.values():
+                v.grad = None
+            if mm:
+                us = [torch.empty(K, nb_, 4, 4).uniform_(eps - 1, 1) for _ in range(2)]
+                loss = O.m_iwae(p, cfg, x, K, us, p_drop=0.1, training=True)[0]
+            else:
+                u = torch.empty(K, nb_, cfg.latent_len, cfg.latent_dim).uniform_(eps - 1, 1)
+                loss = O.elbo(p, cfg, x[1] if cfg.kind == "spec" else x[0], K, u, p_drop=0.1,
+                              training=True)[0]
+            (-loss).backward()
+            O.adamw_step(p, {k: v.grad for k, v in p.items() if v.requires_grad}, st)
+        one(1)
+        t0 = time.perf_counter()
+        one(B)
+        dt = time.perf_counter() - t0
+        out[name] = dict(value=round(B / dt, 3), unit="samples/s", cores=torch.get_num_threads(),
+                         kind="port", sample=f"1 oracle training step of {B} samples after a "
+                                             f"1-sample warm-up; {dt:.2f}s")
+    return out
+
+
+ALLREDUCE_MS_ASSUMED = 0.06   # 0.88 MB ring all-reduce over 8 GPUs' xGMI: latency-bound
+
+
+def training_step_script(device, batches=8):
     """What the script runs, literally (cannon/ZTF_photospect.py:76,119-128):
     training_step(model, torch.optim.AdamW, DataLoader(multimodalDataset(...), 16),
-    m_iwae K=8, multimodal=True) with HOST-resident batches (H2D copies, the per-batch
-    loss sync, torch's AdamW), one timed epoch of `batches` batches after a warm-up
-    epoch: as shipped (training_step replays its captured forward + backward,
-    VAESNe._stepgraph) and with every batch eager (VAESNE_STEP_GRAPH=0)."""
+    m_iwae K=8, multimodal=True) with HOST-resident batches (H2D copies, the loss read
+    one batch late, torch's AdamW update applied behind the device skip), one timed
+    epoch of `batches` batches after a warm-up epoch: as shipped (training_step
+    replays its captured forward + backward, VAESNe._stepgraph) and with every batch
+    eager (VAESNE_STEP_GRAPH=0).
+    b2: the same loop at 2 pairs per batch, i.e. each rank's share when `torchrun
+    --nproc-per-node 8` splits the script's batch of 16 (training_step shards every
+    batch); with the flat-gradient all-reduce it bounds the unchanged script's 8-GPU
+    strong-scaling speed-up: captured(16) / (b2 + all-reduce), the all-reduce time an
+    assumption (one GPU here)."""
     from torch.utils.data import DataLoader, TensorDataset
     from VAESNe import _config, _stepgraph
     from VAESNe.data_util import multimodalDataset
@@ -731,14 +842,14 @@ def training_step_script(device, batches=4):
     out = {}
     saved = _config.step_graph
     try:
-        for name, graph in (("captured", True), ("eager", False)):
+        for name, graph, bs in (("captured", True, 16), ("eager", False, 16), ("b2", True, 2)):
             _config.step_graph = graph
             torch.manual_seed(0)
             model = make_model(device, CFG["dropout"])
             opt = torch.optim.AdamW(model.parameters(), lr=CFG["lr"])
-            x = synthetic_batch(16 * batches, 2024, "cpu")
+            x = synthetic_batch(bs * batches, 2024, "cpu")
             loader = DataLoader(multimodalDataset(TensorDataset(*x[0]), TensorDataset(*x[1])),
-                                batch_size=16, shuffle=False)
+                                batch_size=bs, shuffle=False)
             fn = lambda m, xx: m_iwae(m, xx, K=CFG["K"])
             training_step(model, opt, loader, loss_fn=fn, multimodal=True)
             torch.cuda.synchronize(device)
@@ -746,16 +857,20 @@ def training_step_script(device, batches=4):
             loss = training_step(model, opt, loader, loss_fn=fn, multimodal=True)
             torch.cuda.synchronize(device)
             dt = (time.perf_counter() - t0) / batches
-            out[name] = dict(value=round(16 / dt, 2), unit="SN pairs/s", ms_per_step=round(dt * 1e3, 3),
-                             finite_loss=math.isfinite(loss))
+            out[name] = dict(value=round(bs / dt, 2), unit="SN pairs/s", ms_per_step=round(dt * 1e3, 3),
+                             batch=bs, finite_loss=math.isfinite(loss))
             _stepgraph.clear(model)
             del model, opt
             torch.cuda.empty_cache()
     finally:
         _config.step_graph = saved
-    out.update(batch=16, batches=batches, optimizer="torch.optim.AdamW",
-               note="host-resident DataLoader batches, per-batch loss sync; the headline times "
-                    "bench's own captured step with FusedAdamW on HBM-resident inputs")
+    b2 = out["b2"]["ms_per_step"]
+    out["b2_ms_per_step"] = b2
+    out["predicted_8gpu_strong_speedup"] = round(
+        out["captured"]["ms_per_step"] / (b2 + ALLREDUCE_MS_ASSUMED), 2)
+    out.update(batches=batches, optimizer="torch.optim.AdamW", allreduce_ms_assumed=ALLREDUCE_MS_ASSUMED,
+               note="host-resident DataLoader batches; the headline times bench's own captured "
+                    "step with FusedAdamW on HBM-resident inputs")
     return out
 
 
@@ -924,6 +1039,15 @@ def main():
             out["extras"] = ex
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
+            cfgs = (out.get("extras") or {}).get("configs")
+            if cfgs:
+                try:
+                    for name, cb in config_cpu_baselines().items():
+                        if name in cfgs:
+                            cfgs[name]["cpu_baseline"] = cb
+                            cfgs[name]["vs_cpu"] = round(cfgs[name]["value"] / cb["value"], 1)
+                except Exception as e:
+                    log(f"[bench] config cpu baselines failed: {e!r}")
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -508,6 +508,18 @@ int vaesne_adamw(float* p, const float* g, float* m, float* v, int64_t n, const 
  * NaN posterior, PhotometricVAE.py:160-161). */
 int vaesne_adamw_steps_advance(float* steps, const uint8_t* active, int P, const int32_t* skip,
                                void* stream);
+/* the user's own torch.optim.AdamW (cannon/ZTF_photospect.py:119 `AdamW(params, lr)`,
+ * stepped by training_util.py:45) applied by training_step behind the device-side skip:
+ * torch's foreach update (torch/optim/adam.py _multi_tensor_adam, decoupled decay) over
+ * `count` separate tensors (params[i], grads[i], exp_avgs[i], exp_avg_sqs[i], ns[i]
+ * elements), op for op, with the per-tensor scalars torch computes on the host:
+ * coefs[sets[i]*8 + 0..6] = {1 - lr*wd, 1 - beta1, beta2, 1 - beta2, sqrt(1 - beta2^step),
+ * eps, -lr / (1 - beta1^step)} (step = the tensor's state['step'] after its increment).
+ * fma: ops of the form a + b*c as one fused multiply-add (torch's kernels as ROCm compiles
+ * them) or two roundings.  skip as vaesne_adamw. */
+int vaesne_adamw_list(float* const* params, const float* const* grads, float* const* exp_avgs,
+                      float* const* exp_avg_sqs, const int64_t* ns, const int32_t* sets,
+                      const float* coefs, int count, const int32_t* skip, int fma, void* stream);
 int vaesne_step_advance(float* step, int64_t* rng_state, void* stream);
 /* measurement utility (no reference counterpart): when the stream reaches this node,
  * buf[slot] = the device's constant 100 MHz wall clock.  tools/stamps.py places such

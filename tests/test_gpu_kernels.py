@@ -322,7 +322,8 @@ def _decoder_blocks(n, seed):
     return blocks
 
 
-@pytest.mark.parametrize("N,L,Lc,nblk", [(6, 982, 5, 2), (5, 60, 4, 2), (3, 37, 1, 1), (2, 130, 8, 3)])
+@pytest.mark.parametrize("N,L,Lc,nblk", [(6, 982, 5, 2), (5, 60, 4, 2), (3, 37, 1, 1), (2, 130, 8, 3),
+                                         (3, 300, 2, 2), (2, 400, 3, 2)])
 def test_fused_decoder_stack_vs_oracle(N, L, Lc, nblk):
     """util_layers.decoder_stack (self-attention kernel + fused tail kernel per
     block) against the oracle's TransformerBlock chain in fp64."""
@@ -399,7 +400,8 @@ def test_fused_decoder_tail_dropout_fwd_bwd_consistent():
     assert (o1 - o2).abs().max().item() > 1e-3
 
 
-@pytest.mark.parametrize("L,Lc,store", [(982, 5, True), (300, 4, False), (57, 8, True)])
+@pytest.mark.parametrize("L,Lc,store", [(982, 5, True), (300, 4, False), (57, 8, True),
+                                        (300, 2, True), (400, 3, False)])
 def test_decoder_tail_fused_backward_matches_two_kernel_path(L, Lc, store):
     """The fused per-sequence tail backward (no per-token scratch) against the
     data-kernel + scratch + weight-gradient-kernel path on the same draws: every

@@ -64,8 +64,8 @@ def test_state_dict_round_trip_between_optimizers(src, dst):
 
 
 def test_flagged_step_changes_nothing():
-    """A set non-finite guard flag (VAESNe.guard: NaN posterior / non-finite loss of
-    this step) makes the update kernels no-ops: parameters, moments and step counts
+    """A set non-finite guard flag handed to the update kernels (training_step passes
+    it as apply_update's skip) makes them no-ops: parameters, moments and step counts
     unchanged, as inside a captured step where nothing on the host can intervene.
     Clearing the flag lets the next step update as usual."""
     from VAESNe import guard
@@ -78,15 +78,34 @@ def test_flagged_step_changes_nothing():
     before = [fl[k].clone() for k in ("flat", "m", "v", "steps")]
     guard.flag(DEV)[1] = 1
     try:
-        opt.step()
+        opt.pack_grads()
+        opt.apply_update(skip=guard.ptr(fl["flat"]))
         torch.cuda.synchronize()
         for k, b in zip(("flat", "m", "v", "steps"), before):
             assert torch.equal(fl[k], b), k
     finally:
         guard.reset(DEV)
-    opt.step()
+    opt.pack_grads()
+    opt.apply_update(skip=guard.ptr(fl["flat"]))
     torch.cuda.synchronize()
     assert not torch.equal(fl["flat"], before[0]) and float(fl["steps"].max()) == 1.0
+
+
+def test_plain_step_ignores_a_stale_flag():
+    """a custom loop (the reference's *2goldstein_* scripts call
+    optimizer.step() themselves) after an eval forward that flagged a NaN: FusedAdamW's
+    plain step() updates, as torch.optim.AdamW would -- no silently dropped steps."""
+    from VAESNe import guard
+    from VAESNe.optim import FusedAdamW
+    ref, _ = _run(torch.optim.AdamW, 3)
+    guard.flag(DEV)[0] = 1           # left behind by an unchecked eval call
+    try:
+        got, opt = _run(FusedAdamW, 3)
+        assert float(opt._flat[0]["steps"].max()) == 3.0
+        for a, b in zip(got, ref):
+            assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), (a - b).abs().max()
+    finally:
+        guard.reset(DEV)
 
 
 def test_load_state_dict_refuses_amsgrad_and_maximize():

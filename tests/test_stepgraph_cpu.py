@@ -59,6 +59,34 @@ def test_module_scalars_and_parameters_key_the_network():
     assert SG._signature(net, _fn(1), x, False, params) != s0
 
 
+def test_numpy_and_tensor_attributes_key_the_network():
+    """values baked into a captured graph as kernel arguments must be in
+    the signature whatever their Python type -- numpy scalars (llik_scaling =
+    1 / np.float64(beta)), numpy globals of the loss function -- and a tensor attribute
+    re-bound to another tensor is a new signature."""
+    import numpy as np
+    net = nn.Sequential(nn.Linear(3, 4))
+    net.llik_scaling = 1.0 / np.float64(0.5)
+    x = [torch.zeros(2, 3)]
+    params = list(net.parameters())
+    s0 = SG._signature(net, _fn(1), x, False, params)
+    net.llik_scaling = 1.0 / np.float64(0.25)       # beta annealing with a numpy beta
+    assert SG._signature(net, _fn(1), x, False, params) != s0
+    net.llik_scaling = 1.0 / np.float64(0.5)
+    assert SG._signature(net, _fn(1), x, False, params) == s0
+    net.scale = torch.ones(())
+    s1 = SG._signature(net, _fn(1), x, False, params)
+    net.scale.mul_(2)                               # in place: the graph reads it live
+    assert SG._signature(net, _fn(1), x, False, params) == s1
+    old = net.scale                                 # (kept alive: a distinct storage)
+    net.scale = torch.ones(())                      # re-bound: a new signature
+    assert SG._signature(net, _fn(1), x, False, params) != s1 and old is not net.scale
+    net._private = np.float64(3.0)                  # private attributes never key
+    assert SG._signature(net, _fn(1), x, False, params) == SG._signature(net, _fn(1), x, False, params)
+    assert SG._fn_key(_fn(np.int64(2))) != SG._fn_key(_fn(np.int64(3)))
+    assert SG._fn_key(_fn(np.int64(2))) == SG._fn_key(_fn(np.int64(2)))
+
+
 def test_walk_matches_module_and_parameter_order():
     """_walk's single traversal gives Module.modules()' scalars and Module.parameters()
     in their orders, shared submodules / parameters once."""
@@ -71,8 +99,8 @@ def test_walk_matches_module_and_parameter_order():
     for net in nets:
         scal, params = SG._walk(net)
         assert [id(p) for p in params] == [id(p) for p in net.parameters()]
-        ref = tuple(v for m in net.modules() for v in m.__dict__.values()
-                    if type(v) in SG._SCALARS)
+        ref = tuple((k, SG._scalar_key(v)) for m in net.modules() for k, v in m.__dict__.items()
+                    if k[0] != "_" and SG._scalar_key(v) is not SG._SKIP)
         assert scal == ref
 
 
@@ -98,3 +126,38 @@ def test_unflat_restores_the_multimodal_structure():
     back = SG._unflat(flat, x, True)
     assert isinstance(back, list) and len(back[0]) == 2 and len(back[1]) == 1
     assert back[1][0] is flat[2]
+
+
+def test_capture_topology_rule():
+    """ADVICE / VERDICT r03: the fork / join shapes that crash hipStreamEndCapture
+    (tools/capture_patterns.py, profiles/r03_v4/capture_patterns.txt) raise
+    CaptureTopologyError before the offending wait; the product's shapes (side streams
+    forked from and joined into the origin) pass."""
+    import pytest
+    from VAESNe._capture import CaptureTopologyError, check_edges
+    O, S, P, Q = 1, 2, 3, 4
+
+    def edges(pattern):
+        # "w X Y": X waits on Y (Y records an event, X waits on it); "k X": ignored
+        out, n = [], 0
+        for op in pattern.split("|"):
+            f = op.split()
+            if f[0] == "w":
+                n += 1
+                out += [("record", n, {"O": O, "S": S, "P": P, "Q": Q}[f[2]]),
+                        ("wait", n, {"O": O, "S": S, "P": P, "Q": Q}[f[1]])]
+        return out
+    ok = ["w S O|k S|w O S", "w S O|w P O|k S|k P|w O S|w O P",
+          "w S O|w P O|w Q O|k S|w O S|k O|w S O|k S|w O S"]
+    crash = {   # each crashed (rc -11) in the r03 probe
+        "nested": "w S O|w P S|k P|w S P|k S|w O S",
+        "sibling_mutual": "w S O|w P O|k S|k P|w S P|k S|w P S|k P|w O S|w O P",
+        "sibling_back": "w S O|w P O|k P|w S P|k S|w P S|k P|w O S|w O P",
+        "child_waits_origin": "w S O|w P S|k P|w S P|k O|w P O|k P|w O P|w O S",
+    }
+    for p in ok:
+        check_edges(O, edges(p))
+    for name, p in crash.items():
+        with pytest.raises(CaptureTopologyError):
+            check_edges(O, edges(p))
+    check_edges(O, [("wait", 99, S)])          # an event recorded before the capture

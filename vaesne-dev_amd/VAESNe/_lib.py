@@ -107,6 +107,8 @@ SIGNATURES = {
     "vaesne_infonce_bwd": (I32, [P, P, P, I32, I32, F32, P, P, P, P]),
     "vaesne_adamw": (I32, [P, P, P, P, I64, P, P, F32, F32, F32, F32, F32, P, P]),
     "vaesne_adamw_steps_advance": (I32, [P, P, I32, P, P]),
+    "vaesne_adamw_list": (I32, [PP, PP, PP, PP, C.POINTER(I64), C.POINTER(I32), C.POINTER(F32),
+                                I32, P, I32, P]),
     "vaesne_step_advance": (I32, [P, P, P]),
     "vaesne_stamp": (I32, [P, I32, P]),
     "vaesne_pack": (I32, [PP, C.POINTER(I64), C.POINTER(I64), I32, P, I32, P]),

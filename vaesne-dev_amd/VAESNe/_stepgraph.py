@@ -27,17 +27,38 @@ what the same batch would draw eagerly (tests/test_gpu_stepgraph.py: bitwise).
 """
 from __future__ import annotations
 
+import numbers
 import sys
 import weakref
 
+import numpy as np
 import torch
 
-from . import _config, _defer, rng, training_util
+from . import _capture, _config, _defer, rng, training_util
 
 WARMUP = 2
 MAX_GRAPHS = 3
 
-_SCALARS = (int, float, bool, str)
+_SKIP = object()
+
+
+def _scalar_key(v, depth=0):
+    """The value key of a number (Python or numpy: an llik_scaling of 1/np.float64(beta)),
+    string, None or a tuple / list of them; a tensor by its storage, shape and dtype (a
+    graph reads the memory it was captured on, so re-binding the attribute to another
+    tensor is a new signature while in-place updates need none); _SKIP otherwise."""
+    if v is None or isinstance(v, (str, bool)):
+        return v
+    if isinstance(v, numbers.Number):
+        if isinstance(v, np.generic):
+            return (type(v).__name__, v.item())
+        return (type(v).__name__, v)
+    if isinstance(v, torch.Tensor):
+        return ("tensor", v.data_ptr(), tuple(v.shape), v.dtype, v.device)
+    if isinstance(v, (tuple, list)) and depth < 2 and len(v) <= 16:
+        ks = tuple(_scalar_key(e, depth + 1) for e in v)
+        return _SKIP if any(k is _SKIP for k in ks) else (type(v).__name__,) + ks
+    return _SKIP
 
 
 class _Entry:
@@ -53,11 +74,10 @@ _warned = set()
 
 
 def _value_key(v):
-    """Scalars by value; anything else (functions, modules, tensors, containers) by
-    identity."""
-    if type(v) in _SCALARS or v is None:
-        return v
-    return ("id", id(v))
+    """Numbers, strings, tensors and tuples of them by value (_scalar_key); anything
+    else (functions, modules, containers) by identity."""
+    k = _scalar_key(v)
+    return ("id", id(v)) if k is _SKIP else k
 
 
 def _fn_key(fn):
@@ -66,10 +86,15 @@ def _fn_key(fn):
         return ("obj", id(fn))
     cells = tuple(_value_key(c.cell_contents) for c in (fn.__closure__ or ()))
     g = getattr(fn, "__globals__", {})
-    names = tuple((n, g[n]) for n in code.co_names if n in g and type(g[n]) in _SCALARS)
+    names = []
+    for n in code.co_names:     # the scalar globals it names (a script's K, beta, ...)
+        if n in g:
+            k = _scalar_key(g[n])
+            if k is not _SKIP:
+                names.append((n, k))
     defaults = tuple(_value_key(d) for d in (fn.__defaults__ or ()))
     kw = tuple(sorted((k, _value_key(v)) for k, v in (fn.__kwdefaults__ or {}).items()))
-    return (code, cells, names, defaults, kw, _value_key(getattr(fn, "__self__", None)))
+    return (code, cells, tuple(names), defaults, kw, _value_key(getattr(fn, "__self__", None)))
 
 
 def _module_scalars(network):
@@ -90,7 +115,13 @@ def _walk(network):
             continue
         seen_m.add(id(m))
         d = m.__dict__
-        scalars.extend(v for v in d.values() if type(v) in _SCALARS)
+        # public attributes only: private ones (`_qz_x_params`, set by every forward;
+        # the module's own registries) are not hyperparameters
+        for name, v in d.items():
+            if name[0] != "_":
+                k = _scalar_key(v)
+                if k is not _SKIP:
+                    scalars.append((name, k))
         for prm in d["_parameters"].values():
             if prm is not None and id(prm) not in seen_p:
                 seen_p.add(id(prm))
@@ -178,7 +209,7 @@ def _capture(ent, network, loss_fn, x, xs, multimodal, params) -> bool:
     try:
         torch.cuda.synchronize()
         with torch.cuda.graph(g):
-            with _defer.deferred():
+            with _capture.guarded(), _defer.deferred():
                 sloss = training_util.backward_negated(loss_fn(network, sx))
     except Exception as e:   # noqa: BLE001 -- any capture failure: this signature stays eager
         ent.failed = True

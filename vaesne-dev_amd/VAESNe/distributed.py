@@ -23,6 +23,7 @@ ROCm; "gloo" is used by the CPU-side tests of the process-group logic.
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import torch
@@ -188,6 +189,88 @@ def allreduce_grads(params, reduction="sum", weight=None):
         n = p.grad.numel()
         p.grad.copy_(flat[o:o + n].view_as(p.grad))
         o += n
+
+
+class FlatExchange:
+    """training_step's data-parallel exchange: ONE all-reduce (SUM) per batch of a
+    persistent buffer [every gradient, in `params` order | loss | 2 guard words].
+
+    * The gradients are gathered into the buffer by one pack launch (zeros for a
+      parameter this rank has no gradient for), weighted by the rank's batch share for
+      a mean objective, and after the all-reduce every `.grad` that should exist IS a
+      view of the buffer: no per-parameter copies back.
+    * The loss (times the same weight) and the guard words ride in the same
+      collective: the reduced words are every rank's verdict, and the update kernels
+      read them as their skip flag (a float word is non-zero iff its bits are), so all
+      ranks skip or apply together without a host round trip.
+    * Which parameters get a gradient (the MAX over ranks of "has a gradient", so an
+      empty shard or an unreached branch still updates like the full batch) is agreed
+      once per key (the step's loss function and batch size: identical on every rank,
+      so every rank decides alike whether to agree again) and cached."""
+
+    def __init__(self, params, device):
+        self.params = list(params)
+        self.device = torch.device(device)
+        self.ns = [p.numel() for p in self.params]
+        self.n = sum(self.ns)
+        self.buf = torch.zeros(self.n + 3, dtype=torch.float32, device=self.device)
+        self.views, o = [], 0
+        self.offs = []
+        for p, k in zip(self.params, self.ns):
+            self.views.append(self.buf[o:o + k].view_as(p))
+            self.offs.append(o)
+            o += k
+        self.patterns = {}
+
+    def grads_flat(self):
+        return self.buf[:self.n]
+
+    def skip_ptr(self):
+        return self.buf[self.n + 1:].data_ptr()
+
+    def agree(self, key):
+        local = tuple(p.grad is not None for p in self.params)
+        mask = self.patterns.get(key)
+        if mask is None:
+            t = torch.tensor(local, dtype=torch.int32, device=self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            mask = self.patterns[key] = tuple(bool(v) for v in t.tolist())
+        elif any(a and not b for a, b in zip(local, mask)):
+            raise RuntimeError("VAESNe data parallel: a parameter got a gradient that the "
+                               "agreed pattern of this step signature does not have")
+        return mask
+
+    def run(self, loss, weight, mean, flag, mask):
+        """Gather, all-reduce, re-bind the gradients; returns the reduced
+        [loss, post_flag, loss_flag] (a device view, no sync)."""
+        n = self.n
+        if self.buf.is_cuda:
+            from . import _lib
+            srcs = [p.grad if p.grad is not None and p.grad.is_contiguous() else None
+                    for p in self.params]
+            _lib.lib.pack(_lib.ptr_array(srcs), (C.c_int64 * len(srcs))(*self.offs),
+                          (C.c_int64 * len(srcs))(*self.ns), len(srcs), self.buf.data_ptr(), 0,
+                          _lib.stream())
+            for p, v, s in zip(self.params, self.views, srcs):
+                if s is None and p.grad is not None:
+                    v.copy_(p.grad)
+        else:
+            for p, v in zip(self.params, self.views):
+                if p.grad is None:
+                    v.zero_()
+                elif p.grad.data_ptr() != v.data_ptr():
+                    v.copy_(p.grad)
+        if mean and weight != 1.0:
+            self.buf[:n].mul_(weight)
+        torch.mul(loss.detach().reshape(1).float(), weight, out=self.buf[n:n + 1])
+        if flag is None:
+            self.buf[n + 1:].zero_()
+        else:
+            self.buf[n + 1:].copy_(flag)
+        dist.all_reduce(self.buf, op=dist.ReduceOp.SUM)
+        for p, v, m in zip(self.params, self.views, mask):
+            p.grad = v if m else None
+        return self.buf[n:]
 
 
 class _GatherRows(torch.autograd.Function):

@@ -13,9 +13,13 @@ flat fp32 parameter buffer on the device.
   "step", "exp_avg", "exp_avg_sq"), so checkpoints move between the two.  Only
   lr / betas / eps / weight_decay are taken from a loaded group; a group saved with
   amsgrad or maximize set is refused (the kernel implements neither).
-* Non-finite guard: the update kernels read the device flag of VAESNe.guard and
-  apply nothing (parameters, moments and step counts unchanged) when the step's
-  forward flagged a NaN posterior or a non-finite loss; training_step raises on it.
+* Non-finite guard: inside training_step the update kernels read the device flag of
+  VAESNe.guard (apply_update's `skip`) and apply nothing (parameters, moments and
+  step counts unchanged) once a batch's forward flagged a NaN posterior or a
+  non-finite loss; training_step raises on it.  A plain `step()` (a custom loop, as
+  the reference's *2goldstein_* scripts write) updates unconditionally, exactly as
+  torch.optim.AdamW would: a flag left by an earlier eval forward never silently
+  drops its updates.
 """
 from __future__ import annotations
 
@@ -23,7 +27,7 @@ import ctypes as C
 
 import torch
 
-from . import _lib, guard
+from . import _lib
 from ._lib import lib, stream
 
 
@@ -68,6 +72,15 @@ class FusedAdamW(torch.optim.Optimizer):
     def flat_grad(self, group=0):
         return self._flat[group]["grad"]
 
+    def flat_params_list(self):
+        """Every parameter of the flat buffers, group after group, in buffer order (the
+        layout of training_step's data-parallel gradient buffer)."""
+        return [p for fl in self._flat if fl is not None for p in fl["params"]]
+
+    def flat_sizes(self):
+        """Elements per group's flat buffer (0 for a group without trainable tensors)."""
+        return [0 if fl is None else fl["flat"].numel() for fl in self._flat]
+
     def pack_grads(self):
         """Gather every p.grad into the flat gradient buffer (one launch per 144 tensors)."""
         for fl in self._flat:
@@ -96,18 +109,25 @@ class FusedAdamW(torch.optim.Optimizer):
         return loss
 
     @torch.no_grad()
-    def apply_update(self):
-        """The AdamW update from the (already packed / reduced) flat gradient."""
-        for group, fl in zip(self.param_groups, self._flat):
+    def apply_update(self, skip=None, grads=None):
+        """The AdamW update from the (already packed / reduced) flat gradient.
+        skip: device address of two int32 words (the guard flag, or the all-reduced
+        guard words of training_step's data-parallel exchange); when either is set the
+        kernels change nothing.  Only training_step passes it: a plain step() updates
+        unconditionally, as torch.optim.AdamW does.  grads: per group, a flat gradient
+        to read instead of the packed one (training_step's all-reduced buffer)."""
+        for gi, (group, fl) in enumerate(zip(self.param_groups, self._flat)):
             if fl is None:
                 continue
             b1, b2 = group["betas"]
-            skip = guard.ptr(fl["flat"])
+            gflat = fl["grad"] if grads is None else grads[gi]
+            if gflat.numel() != fl["flat"].numel() or not gflat.is_contiguous():
+                raise ValueError("FusedAdamW.apply_update: flat gradient of the wrong size")
             lib.adamw_steps_advance(fl["steps"].data_ptr(), self._active(fl), len(fl["params"]),
                                     skip, stream())
             runs = self._runs(fl)
             for o, n in runs:
-                lib.adamw(fl["flat"].data_ptr() + 4 * o, fl["grad"].data_ptr() + 4 * o,
+                lib.adamw(fl["flat"].data_ptr() + 4 * o, gflat.data_ptr() + 4 * o,
                           fl["m"].data_ptr() + 4 * o, fl["v"].data_ptr() + 4 * o, n,
                           fl["steps"].data_ptr(), fl["pidx"].data_ptr() + 4 * o,
                           float(group["lr"]), float(b1), float(b2),

@@ -28,6 +28,7 @@ from . import _lib
 _states: dict = {}
 _seed = None
 _call = 0
+_drawn = False      # a call id was issued since the device counter last advanced
 _queue: list = []
 _mode = "device"
 
@@ -64,9 +65,10 @@ def effective_seed() -> int:
 def manual_seed(seed: int):
     """Reset the device RNG of every device to `seed` (folded with the
     data-parallel rank, see rank_seed), counter 0."""
-    global _seed, _call
+    global _seed, _call, _drawn
     _seed = rank_seed(int(seed) & _MASK63, _rank())
     _call = 0
+    _drawn = False
     for st in _states.values():
         st.copy_(torch.tensor([_seed, 0], dtype=torch.int64))
 
@@ -84,8 +86,9 @@ def state(device) -> torch.Tensor:
 
 
 def next_call_id() -> int:
-    global _call
+    global _call, _drawn
     _call = (_call + 1) & 0xFFFFFFFF
+    _drawn = True
     return _call
 
 
@@ -97,8 +100,18 @@ def reset_call_ids():
 
 def advance(device, step: torch.Tensor | None = None):
     """Bump the device counter (and an optional device step counter)."""
+    global _drawn
     st = state(device)
     _lib.lib.step_advance(_lib.ptr(step), st.data_ptr(), _lib.stream())
+    _drawn = False
+
+
+def begin_training(device):
+    """training_step restarts the call ids at every batch; draws made since the last
+    counter advance (an eval / generate / reconstruct call) used the current counter
+    with call ids 1.., which the first training batch would repeat: advance past them."""
+    if _drawn:
+        advance(device)
 
 
 def capturable() -> bool:

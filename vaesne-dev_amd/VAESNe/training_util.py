@@ -6,13 +6,14 @@ Data parallel.  Under a launcher that describes a world
 first call brings the process group up itself (distributed.init_from_env; the
 scripts never do) and broadcasts the parameters from rank 0 once.  Each rank
 trains on its contiguous slice of every batch (sizes differ by at most one) and
-gradients are all-reduced once per step (VAESNe.distributed): SUM for
+gradients are all-reduced once per step (distributed.FlatExchange): SUM for
 sum-over-batch objectives (m_iwae, the multimodal default) and, for mean
 objectives (elbo, the single-modality default), each rank's gradient weighted by
 its share of the batch before the SUM.  A rank whose slice is empty (B < world)
 joins the all-reduce with zero gradients, and every rank holds a gradient for the
-same parameters (distributed.agree_grad_pattern), so all ranks apply the same update.  Each rank draws its own noise / dropout streams
-(rng.rank_seed).  The returned value is the mean full-batch loss on every rank.
+same parameters (agreed once per loss function and batch size), so all ranks apply
+the same update.  Each rank draws its own noise / dropout streams (rng.rank_seed).
+The returned value is the mean full-batch loss on every rank.
 
 Captured steps (VAESNe._stepgraph): after two eager batches of one signature
 (input shapes, loss function, parameters), the forward + backward is captured
@@ -23,23 +24,27 @@ replayed batch computes exactly what the eager batch would (VAESNE_STEP_GRAPH=0:
 always eager).
 
 Non-finite values (VAESNe.guard): the HIP kernels flag a NaN posterior or a
-NaN / Inf loss on the device.  The flag is cleared before each batch's forward
-and read, with the loss, at ONE sync placed before `optimizer.step()` (the
-reference's `.item()`, training_util.py:46, moves ahead of the update): under data
-parallelism the loss and both flag words travel in one all-reduce, so every rank
-sees the same verdict and all raise RuntimeError together (a rank-local raise
-would leave the others blocked in the next all-reduce).  The update is never
-applied for a flagged batch, as the reference stops before its update
-(PhotometricVAE.py:160-161).  A non-finite loss also raises (stricter than the
-reference, which would train on it)."""
+NaN / Inf loss on the device.  The flag is cleared once when training_step starts
+and stays set from the first flagged batch on; the update is enqueued at once
+behind that device-side skip (VAESNe._update: FusedAdamW, and the scripts' own
+torch.optim.AdamW applied op for op by a HIP kernel on its own state), and the
+host reads each batch's (loss, flags) one batch late, while the next batch runs
+(the reference's `.item()`, training_util.py:46).  A flagged batch raises
+RuntimeError there, its update and any later one never applied (the reference
+stops before its update, PhotometricVAE.py:160-161) and the optimizer's host-side
+step counts rolled back.  Other optimizers step after their batch's verdict.  Under
+data parallelism the gradients, the loss and both flag words travel in ONE
+all-reduce (distributed.FlatExchange), so every rank skips, and raises, together.
+A non-finite loss also raises (stricter than the reference, which would train on
+it)."""
+import collections
 import math
 
 import torch
 
-from . import _defer, _stepgraph, guard, rng
+from . import _defer, _stepgraph, _update, guard, rng
 from . import distributed as D
 from .losses import elbo
-from .optim import FusedAdamW
 
 
 _SEEDS = {}
@@ -68,6 +73,41 @@ def safelog10(x):
     return math.log10(tmp)
 
 
+class _Verdicts:
+    """Each batch's [loss, posterior flag, loss flag], copied to pinned host memory
+    behind the batch's work and read later: the host reads batch i's verdict while
+    batch i+1 runs (one wait per batch, the GPU never idles for it)."""
+
+    def __init__(self, device, slots=4):
+        self.cuda = device.type == "cuda"
+        self.q = collections.deque()
+        self.i = 0
+        if self.cuda:
+            self.host = [torch.empty(3, dtype=torch.float32, pin_memory=True)
+                         for _ in range(slots)]
+            self.ev = [torch.cuda.Event() for _ in range(slots)]
+
+    def push(self, stat, batch):
+        if not self.cuda:
+            self.q.append((batch, stat.tolist()))
+            return
+        k = self.i % len(self.host)
+        self.i += 1
+        self.host[k].copy_(stat, non_blocking=True)
+        self.ev[k].record()
+        self.q.append((batch, k))
+
+    def __len__(self):
+        return len(self.q)
+
+    def pop(self):
+        batch, k = self.q.popleft()
+        if not self.cuda:
+            return batch, k
+        self.ev[k].synchronize()
+        return batch, self.host[k].tolist()
+
+
 def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=False,
                   release_memory=False, grad_reduction=None):
     network.train()
@@ -76,35 +116,59 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
     device = next(network.parameters()).device
     rank, ws = D.init_from_env()
     reduction = grad_reduction or ("sum" if multimodal else "mean")
-    fused = isinstance(optimizer, FusedAdamW)
     if ws > 1:
         D.sync_parameters_once(network)
-        if fused and optimizer.grad_hook is None:
-            optimizer.grad_hook = D.GradAllReduce(reduction)
-    params = [p for p in network.parameters() if p.requires_grad]
+    upd = _update.for_optimizer(optimizer)
+    xchg = _exchange(upd, network, device) if ws > 1 else None
+    cuda = device.type == "cuda"
+    if cuda:
+        guard.reset(device)      # a flag left by an unchecked eval call is not this call's
+        rng.begin_training(device)
+    verdicts = _Verdicts(device)
+    last_update = [-1]           # index of the last batch whose update was enqueued
+
+    def settle(keep):
+        """Read verdicts until `keep` remain pending; raise on a flagged batch."""
+        nonlocal total_loss, num_batches
+        while len(verdicts) > keep:
+            batch, (loss_v, post_bad, loss_bad) = verdicts.pop()
+            if post_bad or loss_bad or not math.isfinite(loss_v):
+                # the sticky flag made the device skip this batch's update and every later
+                # one: undo their host bookkeeping, so the optimizer is as before the batch
+                upd.rollback(max(0, last_update[0] - batch + 1))
+                if cuda:
+                    torch.cuda.synchronize(device)
+                if ws > 1:
+                    # every rank read the same reduced verdict: leave together, so no rank
+                    # tears the group down while another is still in a collective
+                    torch.distributed.barrier()
+                guard.raise_for(device, (post_bad > 0, loss_bad > 0 or not math.isfinite(loss_v)),
+                                "training_step")
+            total_loss += loss_v
+            num_batches += 1.
+
     # the next batch is collated and copied to the device while this one runs (its copy
     # queued behind this batch's work, from pinned memory): the host's DataLoader work
     # leaves the per-batch idle window.  Not in the host-generator parity mode, where
     # the model's draws and a dataset's share torch's CPU generator in the reference's
     # order.
-    ahead = device.type == "cuda" and rng.capturable()
+    ahead = cuda and rng.capturable()
     batches = iter(data_loader)
     nxt = _fetch(batches, device, multimodal, ahead)
+    index = 0
     while nxt is not None:
         x = nxt
         nxt = None
         optimizer.zero_grad()
         w = 1.0
         empty = False
+        B = None
         if ws > 1:
             B = (x[0][0] if multimodal else x[0]).shape[0]
             lo, hi = D.split_bounds(B, rank, ws)
             empty = hi == lo
             w = (hi - lo) / B if reduction == "mean" else 1.0
-            if fused and isinstance(optimizer.grad_hook, D.GradAllReduce):
-                optimizer.grad_hook.weight = w if reduction == "mean" else None
             x = D.shard(x, rank, ws)
-        guard.reset(device)       # a flag left by an unchecked eval call is not this batch's
         rng.reset_call_ids()      # every batch draws under call ids 1.. (eager or replayed)
         loss = None
         if empty:
@@ -118,41 +182,49 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
                 loss = backward_negated(loss_fn(network, x))
         if ahead:
             nxt = _fetch(batches, device, multimodal, True)
+        flag = guard.flag(device) if cuda else None
         if ws > 1:
-            # every rank all-reduces the same set of gradients (an empty slice, or a
-            # parameter the loss does not reach on some rank, gets zeros)
-            D.agree_grad_pattern(params)
-            if fused:
-                optimizer.pack_grads()
-                optimizer.reduce_grads()
-            else:
-                D.allreduce_grads(params, reduction, weight=w)
-        # the one sync per batch, before the update: loss and the guard words
-        stat = torch.cat([(loss.detach().float() * w).reshape(1), guard.words(device)])
-        if ws > 1:
-            torch.distributed.all_reduce(stat)
-        loss_v, post_bad, loss_bad = stat.tolist()
-        if post_bad or loss_bad or not math.isfinite(loss_v):
-            if ws > 1:
-                # every rank reached the same verdict: leave together, so no rank tears the
-                # group down while another still completes the all-reduce above
-                torch.distributed.barrier()
-            guard.raise_for(device, (post_bad > 0, loss_bad > 0 or not math.isfinite(loss_v)),
-                            "training_step")
-        if fused and ws > 1:
-            optimizer.apply_update()       # gradients already packed and all-reduced
+            # ONE collective: gradients, loss and guard words (distributed.FlatExchange)
+            key = (_stepgraph._fn_key(loss_fn), multimodal, B, reduction)
+            stat = xchg.run(loss, w, reduction == "mean", flag, xchg.agree(key))
+            skip, flat = xchg.skip_ptr(), xchg.grads_flat()
         else:
+            stat = torch.cat([(loss.detach().float() * w).reshape(1),
+                              flag.float() if cuda else torch.zeros(2)])
+            skip, flat = (flag.data_ptr() if cuda else None), None
+        if cuda and upd.ready():
+            upd.update(skip, flat)        # applied on the device unless a batch was flagged
+            last_update[0] = index
+            verdicts.push(stat, index)
+            settle(1)                     # the previous batch's verdict, read while this runs
+        else:
+            verdicts.push(stat, index)
+            settle(0)                     # the verdict first, then the optimizer's own step
             optimizer.step()
-        if device.type == "cuda":
+            last_update[0] = index
+        if cuda:
             rng.advance(device)            # the next batch draws fresh noise / dropout
-        total_loss += loss_v
-        num_batches += 1.
+        index += 1
         if release_memory:
             del x
             torch.cuda.empty_cache()
         if not ahead:
             nxt = _fetch(batches, device, multimodal, False)
+    settle(0)
     return total_loss / num_batches
+
+
+def _exchange(upd, network, device):
+    """The data-parallel buffer of (updater, network): the updater's parameters in its
+    order (FusedAdamW: its flat layout) then any other trainable parameter."""
+    order = upd.layout()
+    seen = {id(p) for p in order}
+    order += [p for p in network.parameters() if p.requires_grad and id(p) not in seen]
+    key = tuple(id(p) for p in order)
+    x = getattr(upd, "_exchange", None)
+    if x is None or x[0] != key:
+        x = upd._exchange = (key, D.FlatExchange(order, device))
+    return x[1]
 
 
 def _fetch(batches, device, multimodal, pinned):

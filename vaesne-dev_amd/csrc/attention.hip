@@ -161,6 +161,55 @@ __device__ __forceinline__ f2 fma2_bias(f2 a, f2 b, f2 c) {
         : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
+// Two dh-8 score chains (bias + q . k, the first FMA reading its key bias out of the pair,
+// as fma2_bias) interleaved in ONE asm statement.  Consecutive dependent v_pk_fma_f32 need
+// one wait state on gfx950, and hipcc pads every asm-to-asm dependence it cannot see
+// through (it counts an asm statement as zero wait states): as one statement per FMA the
+// forward's 8-key trip carried 39 `s_nop 0` (4 cycles each).  Interleaved, each chain's
+// next FMA is two instructions after its last, which is the wait state; the statement
+// boundary costs at most one pad.
+#define VAESNE_QK_BIAS0(o, q, k, kb) "v_pk_fma_f32 %" #o ", %" #q ", %" #k ", %" #kb " op_sel_hi:[1,0,0]\n"
+#define VAESNE_QK_BIAS1(o, q, k, kb) \
+  "v_pk_fma_f32 %" #o ", %" #q ", %" #k ", %" #kb " op_sel:[0,0,1] op_sel_hi:[1,0,1]\n"
+#define VAESNE_QK_TAIL                                                 \
+  "v_pk_fma_f32 %0, %3, %18, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"   \
+  "v_pk_fma_f32 %1, %11, %22, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"  \
+  "v_pk_fma_f32 %0, %4, %19, %0 op_sel_hi:[1,0,1]\n"                  \
+  "v_pk_fma_f32 %1, %12, %23, %1 op_sel_hi:[1,0,1]\n"                 \
+  "v_pk_fma_f32 %0, %5, %19, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"   \
+  "v_pk_fma_f32 %1, %13, %23, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"  \
+  "v_pk_fma_f32 %0, %6, %20, %0 op_sel_hi:[1,0,1]\n"                  \
+  "v_pk_fma_f32 %1, %14, %24, %1 op_sel_hi:[1,0,1]\n"                 \
+  "v_pk_fma_f32 %0, %7, %20, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"   \
+  "v_pk_fma_f32 %1, %15, %24, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"  \
+  "v_pk_fma_f32 %0, %8, %21, %0 op_sel_hi:[1,0,1]\n"                  \
+  "v_pk_fma_f32 %1, %16, %25, %1 op_sel_hi:[1,0,1]\n"                 \
+  "v_pk_fma_f32 %0, %9, %21, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"   \
+  "v_pk_fma_f32 %1, %17, %25, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
+#define VAESNE_QK_OPERANDS                                                                    \
+  : "=&v"(sa), "=&v"(sb)                                                                      \
+  : "v"(qa[0]), "v"(qa[1]), "v"(qa[2]), "v"(qa[3]), "v"(qa[4]), "v"(qa[5]), "v"(qa[6]),       \
+    "v"(qa[7]), "v"(qb[0]), "v"(qb[1]), "v"(qb[2]), "v"(qb[3]), "v"(qb[4]), "v"(qb[5]),       \
+    "v"(qb[6]), "v"(qb[7]), "v"(kra[0]), "v"(kra[1]), "v"(kra[2]), "v"(kra[3]),               \
+    "v"(krb[0]), "v"(krb[1]), "v"(krb[2]), "v"(krb[3]), "v"(kba), "v"(kbb)
+template <int HA, int HB>
+__device__ __forceinline__ void qk_chains2(const f2 (&qa)[8], const f2 (&kra)[4], f2 kba,
+                                           const f2 (&qb)[8], const f2 (&krb)[4], f2 kbb,
+                                           f2& sa, f2& sb) {
+  if constexpr (HA == 0 && HB == 0)
+    asm(VAESNE_QK_BIAS0(0, 2, 18, 26) VAESNE_QK_BIAS0(1, 10, 22, 27) VAESNE_QK_TAIL VAESNE_QK_OPERANDS);
+  else if constexpr (HA == 0)
+    asm(VAESNE_QK_BIAS0(0, 2, 18, 26) VAESNE_QK_BIAS1(1, 10, 22, 27) VAESNE_QK_TAIL VAESNE_QK_OPERANDS);
+  else if constexpr (HB == 0)
+    asm(VAESNE_QK_BIAS1(0, 2, 18, 26) VAESNE_QK_BIAS0(1, 10, 22, 27) VAESNE_QK_TAIL VAESNE_QK_OPERANDS);
+  else
+    asm(VAESNE_QK_BIAS1(0, 2, 18, 26) VAESNE_QK_BIAS1(1, 10, 22, 27) VAESNE_QK_TAIL VAESNE_QK_OPERANDS);
+}
+#undef VAESNE_QK_BIAS0
+#undef VAESNE_QK_BIAS1
+#undef VAESNE_QK_TAIL
+#undef VAESNE_QK_OPERANDS
+
 template <int DH>
 __device__ __forceinline__ f2 fma2r(f2 a, const f2 (&r)[DH / 2], int d, f2 c) {
   return (d & 1) ? fma2_hi(a, r[d >> 1], c) : fma2_lo(a, r[d >> 1], c);
@@ -177,6 +226,162 @@ __device__ __forceinline__ void lrow2(const float* s, f2 (&r)[DH / 2]) {
     float4 a = *reinterpret_cast<const float4*>(s + d);
     r[d / 2] = (f2){a.x, a.y};
     r[d / 2 + 1] = (f2){a.z, a.w};
+  }
+}
+
+// The fused backward's two chains of one (query, key pair): s = kbias + k . q (scores,
+// log2 domain) and g = v . dO, interleaved in ONE asm statement (see qk_chains2: as
+// separate statements hipcc padded each step, 30 `s_nop 0` per two-query trip).
+// %0 s, %1 g, %2-%9 k[0..7], %10-%17 v[0..7], %18-%21 q row, %22-%25 dO row, %26 kbias
+__device__ __forceinline__ void sg_chains(const f2 (&k)[8], const f2 (&v)[8], const f2 (&qr)[4],
+                                          const f2 (&dr)[4], f2 kb, f2& s, f2& g) {
+  asm("v_pk_fma_f32 %0, %2, %18, %26 op_sel_hi:[1,0,1]\n"
+      "v_pk_mul_f32 %1, %10, %22 op_sel_hi:[1,0]\n"
+      "v_pk_fma_f32 %0, %3, %18, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %1, %11, %22, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %0, %4, %19, %0 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %1, %12, %23, %1 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %0, %5, %19, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %1, %13, %23, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %0, %6, %20, %0 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %1, %14, %24, %1 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %0, %7, %20, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %1, %15, %24, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %0, %8, %21, %0 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %1, %16, %25, %1 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %0, %9, %21, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %1, %17, %25, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
+      : "=&v"(s), "=&v"(g)
+      : "v"(k[0]), "v"(k[1]), "v"(k[2]), "v"(k[3]), "v"(k[4]), "v"(k[5]), "v"(k[6]), "v"(k[7]),
+        "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
+        "v"(qr[0]), "v"(qr[1]), "v"(qr[2]), "v"(qr[3]), "v"(dr[0]), "v"(dr[1]), "v"(dr[2]),
+        "v"(dr[3]), "v"(kb));
+}
+
+// The fused backward's accumulator updates of one (query, key pair): dV += aP dO and
+// dK += dS q over the 8 features, one statement (no pads between the 16 FMAs).
+// %0-%7 dv, %8-%15 dk, %16 aP, %17 dS, %18-%21 dO row, %22-%25 q row
+__device__ __forceinline__ void dvdk_update(f2 (&dv)[8], f2 (&dk)[8], f2 aP, f2 dS,
+                                            const f2 (&dr)[4], const f2 (&qr)[4]) {
+  asm(
+      "v_pk_fma_f32 %0, %16, %18, %0 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %8, %17, %22, %8 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %1, %16, %18, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %9, %17, %22, %9 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %2, %16, %19, %2 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %10, %17, %23, %10 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %3, %16, %19, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %11, %17, %23, %11 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %4, %16, %20, %4 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %12, %17, %24, %12 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %5, %16, %20, %5 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %13, %17, %24, %13 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %6, %16, %21, %6 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %14, %17, %25, %14 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %7, %16, %21, %7 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %15, %17, %25, %15 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
+      : "+v"(dv[0]), "+v"(dv[1]), "+v"(dv[2]), "+v"(dv[3]), "+v"(dv[4]), "+v"(dv[5]), "+v"(dv[6]),
+        "+v"(dv[7]), "+v"(dk[0]), "+v"(dk[1]), "+v"(dk[2]), "+v"(dk[3]), "+v"(dk[4]), "+v"(dk[5]),
+        "+v"(dk[6]), "+v"(dk[7])
+      : "v"(aP), "v"(dS), "v"(dr[0]), "v"(dr[1]), "v"(dr[2]), "v"(dr[3]), "v"(qr[0]), "v"(qr[1]),
+        "v"(qr[2]), "v"(qr[3]));
+}
+
+// The fused dQ's per-feature key sums of two queries over the lane's two key pairs (NP 2):
+// F[d] = sx0 k0[d].x + sy0 k0[d].y + sx1 k1[d].x + sy1 k1[d].y, as one statement whose four
+// passes over d keep each F[d]'s dependent FMAs eight instructions apart.
+// %0-%7 F, %8 sx0, %9 sy0, %10 sx1, %11 sy1, %12-%19 k0[0..7], %20-%27 k1[0..7]
+#define VAESNE_DQ_PASS(op, mod, s, kb)                                                       \
+  op " %0, %" #s ", %" #kb "0" mod "\n" op " %1, %" #s ", %" #kb "1" mod "\n"                \
+  op " %2, %" #s ", %" #kb "2" mod "\n" op " %3, %" #s ", %" #kb "3" mod "\n"
+__device__ __forceinline__ void dq_sums(f2 sx0, f2 sy0, f2 sx1, f2 sy1, const f2 (&k0)[8],
+                                        const f2 (&k1)[8], f2 (&F)[8]) {
+  asm("v_pk_mul_f32 %0, %8, %12 op_sel_hi:[1,0]\n"
+      "v_pk_mul_f32 %1, %8, %13 op_sel_hi:[1,0]\n"
+      "v_pk_mul_f32 %2, %8, %14 op_sel_hi:[1,0]\n"
+      "v_pk_mul_f32 %3, %8, %15 op_sel_hi:[1,0]\n"
+      "v_pk_mul_f32 %4, %8, %16 op_sel_hi:[1,0]\n"
+      "v_pk_mul_f32 %5, %8, %17 op_sel_hi:[1,0]\n"
+      "v_pk_mul_f32 %6, %8, %18 op_sel_hi:[1,0]\n"
+      "v_pk_mul_f32 %7, %8, %19 op_sel_hi:[1,0]\n"
+      "v_pk_fma_f32 %0, %9, %12, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %1, %9, %13, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %2, %9, %14, %2 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %3, %9, %15, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %4, %9, %16, %4 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %5, %9, %17, %5 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %6, %9, %18, %6 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %7, %9, %19, %7 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %0, %10, %20, %0 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %1, %10, %21, %1 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %2, %10, %22, %2 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %3, %10, %23, %3 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %4, %10, %24, %4 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %5, %10, %25, %5 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %6, %10, %26, %6 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %7, %10, %27, %7 op_sel_hi:[1,0,1]\n"
+      "v_pk_fma_f32 %0, %11, %20, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %1, %11, %21, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %2, %11, %22, %2 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %3, %11, %23, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %4, %11, %24, %4 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %5, %11, %25, %5 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %6, %11, %26, %6 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+      "v_pk_fma_f32 %7, %11, %27, %7 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
+      : "=&v"(F[0]), "=&v"(F[1]), "=&v"(F[2]), "=&v"(F[3]), "=&v"(F[4]), "=&v"(F[5]),
+        "=&v"(F[6]), "=&v"(F[7])
+      : "v"(sx0), "v"(sy0), "v"(sx1), "v"(sy1), "v"(k0[0]), "v"(k0[1]), "v"(k0[2]), "v"(k0[3]),
+        "v"(k0[4]), "v"(k0[5]), "v"(k0[6]), "v"(k0[7]), "v"(k1[0]), "v"(k1[1]), "v"(k1[2]),
+        "v"(k1[3]), "v"(k1[4]), "v"(k1[5]), "v"(k1[6]), "v"(k1[7]));
+}
+#undef VAESNE_DQ_PASS
+
+// s[p][u] = kb[u] + q[p] . k[u] for the 8 keys of a group, x[p] = max(x[p], s[p][.]).
+// dh 8: two chains per asm statement (qk_chains2): the two query pairs of one key (NP 2),
+// or one query pair and two keys (NP 1).
+template <int DH, int NP>
+__device__ __forceinline__ void qk_group(const f2 (&q)[NP][DH], const float* ks, const float* kb,
+                                         f2 (&s)[NP][8], f2 (&x)[NP]) {
+  if constexpr (DH == 8 && NP == 2) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      f2 kr[4];
+      lrow2<8>(ks + u * 8, kr);
+      const f2 kb2 = *reinterpret_cast<const f2*>(kb + (u & ~1));
+      if (u & 1)
+        qk_chains2<1, 1>(q[0], kr, kb2, q[1], kr, kb2, s[0][u], s[1][u]);
+      else
+        qk_chains2<0, 0>(q[0], kr, kb2, q[1], kr, kb2, s[0][u], s[1][u]);
+      x[0] = __builtin_elementwise_max(x[0], s[0][u]);
+      x[1] = __builtin_elementwise_max(x[1], s[1][u]);
+    }
+  } else if constexpr (DH == 8 && NP == 1) {
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      f2 k0[4], k1[4];
+      lrow2<8>(ks + u * 8, k0);
+      lrow2<8>(ks + (u + 1) * 8, k1);
+      const f2 kb2 = *reinterpret_cast<const f2*>(kb + u);
+      qk_chains2<0, 1>(q[0], k0, kb2, q[0], k1, kb2, s[0][u], s[0][u + 1]);
+      x[0] = __builtin_elementwise_max(x[0], s[0][u]);
+      x[0] = __builtin_elementwise_max(x[0], s[0][u + 1]);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      f2 kr[DH / 2];
+      lrow2<DH>(ks + u * DH, kr);
+      const f2 kb2 = *reinterpret_cast<const f2*>(kb + (u & ~1));
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        // acc = kb + q . k, the chain's first FMA reading the bias from its pair
+        f2 acc = (u & 1) ? fma2_bias<1>(q[p][0], kr[0], kb2) : fma2_bias<0>(q[p][0], kr[0], kb2);
+#pragma unroll
+        for (int d = 1; d < DH; ++d) acc = fma2r<DH>(q[p][d], kr, d, acc);
+        s[p][u] = acc;
+        x[p] = __builtin_elementwise_max(x[p], acc);
+      }
+    }
   }
 }
 
@@ -318,21 +523,7 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
       f2 x[NP];
 #pragma unroll
       for (int p = 0; p < NP; ++p) x[p] = m[p];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        f2 kr[DH / 2];
-        lrow2<DH>(Ks + (g0 + u) * DH, kr);
-        const f2 kb2 = *reinterpret_cast<const f2*>(Kb + g0 + (u & ~1));
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-          // acc = kb + q . k, the chain's first FMA reading the bias from its pair
-          f2 acc = (u & 1) ? fma2_bias<1>(q[p][0], kr[0], kb2) : fma2_bias<0>(q[p][0], kr[0], kb2);
-#pragma unroll
-          for (int d = 1; d < DH; ++d) acc = fma2r<DH>(q[p][d], kr, d, acc);
-          s[p][u] = acc;
-          x[p] = __builtin_elementwise_max(x[p], acc);
-        }
-      }
+      qk_group<DH, NP>(q, Ks + g0 * DH, Kb + g0, s, x);
       // Lazy rescaling: m is the exponent origin, moved (and o, l rescaled) only
       // when some row's running max x passes it by more than 8 (p <= 2^8, no
       // overflow) -- a wave-uniform branch taken on the first groups only.
@@ -684,11 +875,17 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
         }
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
-          f2 s = kbias[p], g = mul2_lo(v[p][0], dr[0]);
+          f2 s, g;
+          if constexpr (DH == 8) {
+            sg_chains(k[p], v[p], qr, dr, kbias[p], s, g);
+          } else {
+            s = kbias[p];
+            g = mul2_lo(v[p][0], dr[0]);
 #pragma unroll
-          for (int d = 0; d < DH; ++d) {
-            s = fma2ru<DH>(k[p][d], qr, d, s);
-            if (d > 0) g = fma2ru<DH>(v[p][d], dr, d, g);
+            for (int d = 0; d < DH; ++d) {
+              s = fma2ru<DH>(k[p][d], qr, d, s);
+              if (d > 0) g = fma2ru<DH>(v[p][d], dr, d, g);
+            }
           }
           const f2 pr = ex2(s - li);
           f2 aP = pr, dS;
@@ -700,22 +897,31 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
             dS = pr * (g - Di);
           }
           dSq[i - i0][p] = dS;
+          if constexpr (DH == 8) {
+            dvdk_update(dv[p], dk[p], aP, dS, dr, qr);
+          } else {
 #pragma unroll
-          for (int d = 0; d < DH; ++d) {
-            dv[p][d] = fma2ru<DH>(aP, dr, d, dv[p][d]);
-            dk[p][d] = fma2ru<DH>(dS, qr, d, dk[p][d]);
+            for (int d = 0; d < DH; ++d) {
+              dv[p][d] = fma2ru<DH>(aP, dr, d, dv[p][d]);
+              dk[p][d] = fma2ru<DH>(dS, qr, d, dk[p][d]);
+            }
           }
         }
       }
       if (DQ) {   // F[d] = {dQ_d of query i0, of query i0 + 1} over this lane's keys
         f2 F[DH];
+        if constexpr (NP == 2 && DH == 8) {
+          dq_sums((f2){dSq[0][0].x, dSq[1][0].x}, (f2){dSq[0][0].y, dSq[1][0].y},
+                  (f2){dSq[0][1].x, dSq[1][1].x}, (f2){dSq[0][1].y, dSq[1][1].y}, k[0], k[1], F);
+        } else {
 #pragma unroll
-        for (int p = 0; p < NP; ++p) {
-          const f2 sx = {dSq[0][p].x, dSq[1][p].x}, sy = {dSq[0][p].y, dSq[1][p].y};
+          for (int p = 0; p < NP; ++p) {
+            const f2 sx = {dSq[0][p].x, dSq[1][p].x}, sy = {dSq[0][p].y, dSq[1][p].y};
 #pragma unroll
-          for (int d = 0; d < DH; ++d) {
-            F[d] = p == 0 ? mul2_lo(sx, k[p][d]) : fma2_lo_u(sx, k[p][d], F[d]);
-            F[d] = fma2_hi_u(sy, k[p][d], F[d]);
+            for (int d = 0; d < DH; ++d) {
+              F[d] = p == 0 ? mul2_lo(sx, k[p][d]) : fma2_lo_u(sx, k[p][d], F[d]);
+              F[d] = fma2_hi_u(sy, k[p][d], F[d]);
+            }
           }
         }
         // component order: level-32 pairs (feature 2j, 2j + 1) of one query, so
@@ -968,21 +1174,7 @@ __global__ __launch_bounds__(NTT) void attn_rep_fwd_kernel(AttnArgs a, int R, in
       f2 x[NP];
 #pragma unroll
       for (int p = 0; p < NP; ++p) x[p] = m[p];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        f2 kr[DH / 2];
-        lrow2<DH>(Ks + (g0 + u) * DH, kr);
-        const f2 kb2 = *reinterpret_cast<const f2*>(Kb + g0 + (u & ~1));
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-          // acc = kb + q . k, the chain's first FMA reading the bias from its pair
-          f2 acc = (u & 1) ? fma2_bias<1>(q[p][0], kr[0], kb2) : fma2_bias<0>(q[p][0], kr[0], kb2);
-#pragma unroll
-          for (int d = 1; d < DH; ++d) acc = fma2r<DH>(q[p][d], kr, d, acc);
-          s[p][u] = acc;
-          x[p] = __builtin_elementwise_max(x[p], acc);
-        }
-      }
+      qk_group<DH, NP>(q, Ks + g0 * DH, Kb + g0, s, x);
       // lazy rescaling, as attn_fwd_kernel (wave-uniform, first groups only)
       bool move = false;
 #pragma unroll

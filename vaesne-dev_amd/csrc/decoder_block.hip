@@ -1583,7 +1583,7 @@ int dispatch_fused(const Tail& a, int grid, hipStream_t s) {
   return launch_fused<LCV, false, false>(a, grid, s);
   // LC: the compile-time context-token bound (4: photometry decoder, latent_len tokens;
   // 5: spectra decoder, latent_len + the phase token; 8: anything else up to LCMAX)
-  if (a.Lc == 4) { VAESNE_FUSED_CASE(4) }
+  if (a.Lc <= 4) { VAESNE_FUSED_CASE(4) }
   if (a.Lc == 5) { VAESNE_FUSED_CASE(5) }
   VAESNE_FUSED_CASE(8)
 #undef VAESNE_FUSED_CASE
@@ -1610,7 +1610,7 @@ int dispatch(const Tail& a, int grid, float* scr, hipStream_t s) {
   if (next) return FWD ? launch_fwd<LCV, true, false>(a, grid, scr, s) : launch_bwd<LCV, true, false>(a, grid, scr, s);       \
   if (drop) return FWD ? launch_fwd<LCV, false, true>(a, grid, scr, s) : launch_bwd<LCV, false, true>(a, grid, scr, s);       \
   return FWD ? launch_fwd<LCV, false, false>(a, grid, scr, s) : launch_bwd<LCV, false, false>(a, grid, scr, s);
-  if (a.Lc == 4) { VAESNE_TAIL_CASE(4) }
+  if (a.Lc <= 4) { VAESNE_TAIL_CASE(4) }
   if (a.Lc == 5) { VAESNE_TAIL_CASE(5) }
   VAESNE_TAIL_CASE(8)
 #undef VAESNE_TAIL_CASE

@@ -339,6 +339,63 @@ __global__ void pack_kernel(PackArgs a, float* __restrict__ dst, int unpack) {
   }
 }
 
+// torch.optim.AdamW as the cannon scripts construct it (AdamW(params, lr): foreach,
+// capturable=False; torch/optim/adam.py _multi_tensor_adam with decoupled decay) over a
+// LIST of tensors, for training_step's update behind the device-side skip.  Each line
+// below is one of torch's _foreach ops, in its order, with each op's own rounding, and
+// the scalars are the ones torch computes on the host in double precision and hands its
+// kernels (cast to fp32): per scalar set, {1 - lr*wd, 1 - beta1, beta2, 1 - beta2,
+// sqrt(1 - beta2^step), eps, -lr / (1 - beta1^step)}.  FMA: whether an op of the form
+// a + b*c is one fused multiply-add (as ROCm's compiler contracts torch's foreach
+// kernels) or two roundings.
+constexpr int ADAMW_LIST_MAX = 96;     // 96 x 37 B + 8 sets x 32 B of kernel arguments (< 4 KB)
+constexpr int ADAMW_LIST_SETS = 8;
+struct AdamwListArgs {
+  float* p[ADAMW_LIST_MAX];
+  const float* g[ADAMW_LIST_MAX];
+  float* m[ADAMW_LIST_MAX];
+  float* v[ADAMW_LIST_MAX];
+  int32_t n[ADAMW_LIST_MAX];
+  uint8_t set[ADAMW_LIST_MAX];
+  float coef[ADAMW_LIST_SETS][8];
+  int count;
+};
+
+template <bool FMA>
+__device__ __forceinline__ float madd(float a, float b, float c) {
+  return FMA ? __builtin_fmaf(a, b, c) : __fadd_rn(__fmul_rn(a, b), c);
+}
+
+template <bool FMA>
+__global__ void adamw_list_kernel(AdamwListArgs a, const int32_t* __restrict__ skip) {
+  if (skip && (skip[0] | skip[1])) return;
+  const int i = blockIdx.y;
+  if (i >= a.count) return;
+  const float* c = a.coef[a.set[i]];
+  const float decay = c[0], wl = c[1], b2 = c[2], vb2 = c[3], bc2s = c[4], eps = c[5],
+              step = c[6];
+  float* __restrict__ p = a.p[i];
+  const float* __restrict__ g = a.g[i];
+  float* __restrict__ m = a.m[i];
+  float* __restrict__ v = a.v[i];
+  const int n = a.n[i];
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const float gg = g[t];
+    const float w = __fmul_rn(p[t], decay);                        // _foreach_mul_(params, 1-lr*wd)
+    float mm = m[t];
+    const float d = __fsub_rn(gg, mm);                            // _foreach_lerp_(m, g, 1-beta1)
+    mm = fabsf(wl) < 0.5f ? madd<FMA>(wl, d, mm) : madd<FMA>(-d, __fsub_rn(1.f, wl), gg);
+    float vv = __fmul_rn(v[t], b2);                               // _foreach_mul_(v, beta2)
+    vv = madd<FMA>(vb2, __fmul_rn(gg, gg), vv);                   // _foreach_addcmul_(v, g, g, 1-beta2)
+    float den = __fsqrt_rn(vv);                                   // _foreach_sqrt
+    den = __fdiv_rn(den, bc2s);                                   // _foreach_div_(., sqrt(bc2))
+    den = __fadd_rn(den, eps);                                    // _foreach_add_(., eps)
+    p[t] = madd<FMA>(step, __fdiv_rn(mm, den), w);                // _foreach_addcdiv_(p, m, ., -lr/bc1)
+    m[t] = mm;
+    v[t] = vv;
+  }
+}
+
 }  // namespace
 
 VAESNE_API int vaesne_sincos(const float* x, int64_t period, int64_t rows, const float* div, int nf,
@@ -516,6 +573,51 @@ VAESNE_API int vaesne_adamw(float* p, const float* g, float* m, float* v, int64_
   hipLaunchKernelGGL(adamw_kernel, dim3(blocks_for(n, NT, 4096)), dim3(NT), 0,
                      (hipStream_t)stream, p, g, m, v, n, step, pidx, lr, b1, b2, eps, wd, skip);
   VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_adamw_list(float* const* params, const float* const* grads,
+                                 float* const* exp_avgs, float* const* exp_avg_sqs,
+                                 const int64_t* ns, const int32_t* sets, const float* coefs,
+                                 int count, const int32_t* skip, int fma, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int base = 0;
+  while (base < count) {
+    // one launch per run of <= ADAMW_LIST_MAX tensors using <= ADAMW_LIST_SETS scalar sets
+    AdamwListArgs a{};
+    int used[ADAMW_LIST_SETS];
+    int nsets = 0, c = 0;
+    int64_t maxn = 1;
+    for (; base + c < count && c < ADAMW_LIST_MAX; ++c) {
+      const int i = base + c;
+      if (ns[i] < 0 || ns[i] > INT32_MAX || sets[i] < 0) return (int)hipErrorInvalidValue;
+      if (ns[i] > 0 && !(params[i] && grads[i] && exp_avgs[i] && exp_avg_sqs[i]))
+        return (int)hipErrorInvalidValue;
+      int k = 0;
+      while (k < nsets && used[k] != sets[i]) ++k;
+      if (k == nsets) {
+        if (nsets == ADAMW_LIST_SETS) break;
+        used[nsets] = sets[i];
+        for (int j = 0; j < 8; ++j) a.coef[nsets][j] = coefs[(int64_t)sets[i] * 8 + j];
+        ++nsets;
+      }
+      a.p[c] = params[i];
+      a.g[c] = grads[i];
+      a.m[c] = exp_avgs[i];
+      a.v[c] = exp_avg_sqs[i];
+      a.n[c] = (int32_t)ns[i];
+      a.set[c] = (uint8_t)k;
+      if (ns[i] > maxn) maxn = ns[i];
+    }
+    a.count = c;
+    const unsigned gx = blocks_for(maxn, NT, 64);
+    if (fma)
+      hipLaunchKernelGGL(adamw_list_kernel<true>, dim3(gx, c), dim3(NT), 0, s, a, skip);
+    else
+      hipLaunchKernelGGL(adamw_list_kernel<false>, dim3(gx, c), dim3(NT), 0, s, a, skip);
+    VAESNE_CHECK_LAUNCH();
+    base += c;
+  }
   return 0;
 }
 
