@@ -191,3 +191,62 @@ def test_nonfinite_loss_on_one_rank_raises_on_every_rank():
         assert raised, f"rank {rank} did not raise"
         assert "non-finite" in msg, msg
         assert unchanged, f"rank {rank}: parameters changed by a rejected step"
+
+
+def _count_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(ws), LOCAL_RANK=str(rank))
+    try:
+        from VAESNe.losses import elbo
+        from VAESNe.training_util import training_step
+        torch.set_num_threads(1)
+        torch.manual_seed(0)
+        model = _ToyVAE()
+        batches = [_data(4)[0] for _ in range(3)]
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+        training_step(model, opt, batches, loss_fn=elbo)        # first epoch: agrees the pattern
+        counts = {"all_reduce": 0, "tolist": 0, "item": 0}
+        real_ar, real_tl, real_it = dist.all_reduce, torch.Tensor.tolist, torch.Tensor.item
+
+        def ar(*a, **k):
+            counts["all_reduce"] += 1
+            return real_ar(*a, **k)
+
+        def tl(self):
+            counts["tolist"] += 1
+            return real_tl(self)
+
+        steps = {id(st["step"]) for st in opt.state.values()}   # torch's host step counts
+
+        def it(self):
+            if id(self) not in steps:
+                counts["item"] += 1
+            return real_it(self)
+        dist.all_reduce, torch.Tensor.tolist, torch.Tensor.item = ar, tl, it
+        try:
+            training_step(model, opt, batches, loss_fn=elbo)    # steady state
+        finally:
+            dist.all_reduce, torch.Tensor.tolist, torch.Tensor.item = real_ar, real_tl, real_it
+        q.put((rank, counts, len(batches)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_dp_step_has_one_collective_and_one_host_read_per_batch():
+    """in steady state a data-parallel training_step batch runs
+    exactly ONE all-reduce (gradients, loss and guard words in one buffer: the
+    gradient pattern is agreed once per loss function and batch size) and ONE host
+    read (the batch's verdict), no per-parameter copies and no pattern all-reduce."""
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_count_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(300)
+        assert pr.exitcode == 0, f"rank exit code {pr.exitcode}"
+    for rank, counts, nb in sorted(q.get() for _ in range(ws)):
+        assert counts == {"all_reduce": nb, "tolist": nb, "item": 0}, (rank, counts)
