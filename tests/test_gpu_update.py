@@ -60,31 +60,32 @@ def _adamw_run(steps, device_update, fma=None, monkeypatch=None):
     return [p.detach().clone() for p in ps], opt
 
 
-@pytest.mark.parametrize("fma", [1, 0])
-def test_adamw_list_against_torch_adamw(fma, monkeypatch):
-    """The shipped variant (_update.TORCH_FMA) is bitwise torch; the other is within
-    fp32 rounding (the test names which one matched)."""
+def test_adamw_list_against_torch_adamw(monkeypatch):
+    """Both contraction variants of vaesne_adamw_list against torch.optim.AdamW: each
+    within fp32 rounding, and the shipped one (_update.TORCH_FMA) bitwise -- moments and
+    state_dict included."""
     from VAESNe import _update
     shipped = _update.TORCH_FMA
     ref, ropt = _adamw_run(6, False)
-    got, gopt = _adamw_run(6, True, fma=fma, monkeypatch=monkeypatch)
-    bitwise = all(torch.equal(a, b) for a, b in zip(got, ref))
-    for a, b in zip(got, ref):
-        assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), (a - b).abs().max()
-    rs, gs = ropt.state_dict(), gopt.state_dict()
-    assert rs["param_groups"] == gs["param_groups"]
-    assert set(rs["state"]) == set(gs["state"])
-    for k in rs["state"]:
-        assert float(rs["state"][k]["step"]) == float(gs["state"][k]["step"]), k
-        assert not gs["state"][k]["step"].is_cuda
-        for name in ("exp_avg", "exp_avg_sq"):
-            a, b = rs["state"][k][name], gs["state"][k][name]
-            assert torch.allclose(a, b, rtol=1e-6, atol=1e-12), (k, name)
-            if fma == shipped:
-                assert torch.equal(a, b), (k, name)
-    if fma == shipped:
-        assert bitwise, f"TORCH_FMA={shipped} is not bitwise torch.optim.AdamW"
-    print(f"[adamw_list] fma={fma}: bitwise={bitwise}")
+    res = {}
+    for fma in (1, 0):
+        got, gopt = _adamw_run(6, True, fma=fma, monkeypatch=monkeypatch)
+        for a, b in zip(got, ref):
+            assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), (fma, (a - b).abs().max())
+        rs, gs = ropt.state_dict(), gopt.state_dict()
+        assert rs["param_groups"] == gs["param_groups"]
+        assert set(rs["state"]) == set(gs["state"])
+        same = all(torch.equal(a, b) for a, b in zip(got, ref))
+        for k in rs["state"]:
+            assert float(rs["state"][k]["step"]) == float(gs["state"][k]["step"]), k
+            assert not gs["state"][k]["step"].is_cuda
+            for name in ("exp_avg", "exp_avg_sq"):
+                a, b = rs["state"][k][name], gs["state"][k][name]
+                assert torch.allclose(a, b, rtol=1e-6, atol=1e-12), (fma, k, name)
+                same = same and torch.equal(a, b)
+        res[fma] = same
+    monkeypatch.setattr(_update, "TORCH_FMA", shipped)
+    assert res[shipped], f"bitwise equal to torch.optim.AdamW by variant (fma: bitwise): {res}"
 
 
 def _script_run(device_update, monkeypatch, epochs=2, n=12, B=4, opt_kind="torch",

@@ -34,7 +34,8 @@ import weakref
 import numpy as np
 import torch
 
-from . import _capture, _config, _defer, rng, training_util
+from . import _config, _defer, rng, training_util
+from ._capture import guarded as _guarded
 
 WARMUP = 2
 MAX_GRAPHS = 3
@@ -209,7 +210,7 @@ def _capture(ent, network, loss_fn, x, xs, multimodal, params) -> bool:
     try:
         torch.cuda.synchronize()
         with torch.cuda.graph(g):
-            with _capture.guarded(), _defer.deferred():
+            with _guarded(), _defer.deferred():
                 sloss = training_util.backward_negated(loss_fn(network, sx))
     except Exception as e:   # noqa: BLE001 -- any capture failure: this signature stays eager
         ent.failed = True

@@ -208,12 +208,18 @@ class FlatExchange:
       once per key (the step's loss function and batch size: identical on every rank,
       so every rank decides alike whether to agree again) and cached."""
 
-    def __init__(self, params, device):
+    def __init__(self, params, device, buf=None):
         self.params = list(params)
         self.device = torch.device(device)
         self.ns = [p.numel() for p in self.params]
         self.n = sum(self.ns)
-        self.buf = torch.zeros(self.n + 3, dtype=torch.float32, device=self.device)
+        # buf: storage to exchange in (FusedAdamW's own gradient buffer, so its flat
+        # gradient IS the reduced one); at least n + 3 floats
+        if buf is not None and (buf.numel() < self.n + 3 or buf.dtype != torch.float32
+                                or buf.device != self.device):
+            raise ValueError("FlatExchange: buffer too small or of the wrong dtype / device")
+        self.buf = buf[:self.n + 3] if buf is not None else \
+            torch.zeros(self.n + 3, dtype=torch.float32, device=self.device)
         self.views, o = [], 0
         self.offs = []
         for p, k in zip(self.params, self.ns):

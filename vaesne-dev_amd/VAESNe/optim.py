@@ -60,8 +60,11 @@ class FusedAdamW(torch.optim.Optimizer):
                     o += p.numel()
             pidx = torch.repeat_interleave(torch.arange(len(ps), dtype=torch.int32),
                                            torch.tensor(ns, dtype=torch.int64)).to(dev)
+            # the gradient buffer carries 4 spare words: training_step's data-parallel
+            # exchange all-reduces [gradient | loss | guard words] in place (distributed.FlatExchange)
+            gstore = torch.zeros(n + 4, dtype=torch.float32, device=dev)
             self._flat.append(dict(
-                params=ps, flat=flat, grad=torch.zeros_like(flat), m=torch.zeros_like(flat),
+                params=ps, flat=flat, grad=gstore[:n], gstore=gstore, m=torch.zeros_like(flat),
                 v=torch.zeros_like(flat),
                 steps=torch.zeros(len(ps), dtype=torch.float32, device=dev), pidx=pidx,
                 active={}, offs=(C.c_int64 * len(ps))(*offs), ns=(C.c_int64 * len(ps))(*ns)))
@@ -76,6 +79,11 @@ class FusedAdamW(torch.optim.Optimizer):
         """Every parameter of the flat buffers, group after group, in buffer order (the
         layout of training_step's data-parallel gradient buffer)."""
         return [p for fl in self._flat if fl is not None for p in fl["params"]]
+
+    def exchange_buffer(self):
+        """The one group's gradient storage with its spare words (None with several groups)."""
+        fls = [fl for fl in self._flat if fl is not None]
+        return fls[0]["gstore"] if len(fls) == 1 else None
 
     def flat_sizes(self):
         """Elements per group's flat buffer (0 for a group without trainable tensors)."""

@@ -223,7 +223,10 @@ def _exchange(upd, network, device):
     key = tuple(id(p) for p in order)
     x = getattr(upd, "_exchange", None)
     if x is None or x[0] != key:
-        x = upd._exchange = (key, D.FlatExchange(order, device))
+        buf = None
+        if isinstance(upd, _update.FusedUpdater) and len(order) == len(upd.layout()):
+            buf = upd.opt.exchange_buffer()       # FusedAdamW's flat gradient, reduced in place
+        x = upd._exchange = (key, D.FlatExchange(order, device, buf))
     return x[1]
 
 

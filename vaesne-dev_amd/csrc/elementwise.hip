@@ -387,7 +387,7 @@ __global__ void adamw_list_kernel(AdamwListArgs a, const int32_t* __restrict__ s
     mm = fabsf(wl) < 0.5f ? madd<FMA>(wl, d, mm) : madd<FMA>(-d, __fsub_rn(1.f, wl), gg);
     float vv = __fmul_rn(v[t], b2);                               // _foreach_mul_(v, beta2)
     vv = madd<FMA>(vb2, __fmul_rn(gg, gg), vv);                   // _foreach_addcmul_(v, g, g, 1-beta2)
-    float den = __fsqrt_rn(vv);                                   // _foreach_sqrt
+    float den = sqrtf(vv);   // _foreach_sqrt (sqrtf: correctly rounded; __fsqrt_rn is a bare v_sqrt_f32)
     den = __fdiv_rn(den, bc2s);                                   // _foreach_div_(., sqrt(bc2))
     den = __fadd_rn(den, eps);                                    // _foreach_add_(., eps)
     p[t] = madd<FMA>(step, __fdiv_rn(mm, den), w);                // _foreach_addcdiv_(p, m, ., -lr/bc1)
