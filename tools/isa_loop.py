@@ -26,6 +26,10 @@ def blocks(path, name):
     for l in lines[start + 1:]:
         if l.startswith(".Lfunc_end"):
             break
+        if l.startswith("; %bb."):          # a fall-through block (no .LBB label)
+            cur = l[2:].split(":")[0]
+            out[cur] = []
+            continue
         s = l.split(";")[0].strip()
         if not s:
             continue

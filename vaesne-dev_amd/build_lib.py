@@ -25,6 +25,11 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-fvisibility=
           "-I" + os.path.join(ROOT, "include"), "-Wall", "-Wno-unused-function"]
 
 
+# per-source flags: the attention kernels' MFMA results feed VALU code directly (VGPR form:
+# no v_accvgpr_read copies out of the accumulation registers)
+FILE_FLAGS = {"attention.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
 
@@ -42,7 +47,7 @@ def _compile(src, extra=(), obj=None):
     if not extra and os.path.exists(obj) and \
             os.path.getmtime(obj) >= max(os.path.getmtime(p) for p in [src] + hdrs):
         return obj          # object newer than its source and every header
-    cmd = [HIPCC, "-c", *CFLAGS, *extra, "-o", obj, src]
+    cmd = [HIPCC, "-c", *CFLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra, "-o", obj, src]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

@@ -650,6 +650,286 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+// ======================= forward, scores on the matrix cores ==================
+// head_dim 8.  S = Q K^T runs on v_mfma_f32_16x16x4_f32 -- bit for bit the VALU kernel's
+// fmaf chain kbias + q0 k0 + ... + q7 k7 (the accumulator starts at the key bias, the two
+// 4-deep k-steps chain) -- so the matrix cores take the score FMAs off the VALU, which
+// keeps the softmax, the dropout hash and decisions and P V (VALU issue is the binding
+// limit of the attention kernels).
+// Wave: 64 queries, four 16-query column tiles; lane l owns queries 16n + (l & 15) and,
+// of every 64-key tile, the 16 keys 16g .. 16g + 15 (g = l >> 4): the A operand's rows
+// are permuted (row 4G + I of m-tile mt = key 16G + 4mt + I) so each accumulator's four
+// registers are four consecutive keys of the lane's query.  Each lane keeps its own
+// online-softmax state (m, l, o) over its keys; the four lanes of a query combine at the
+// end.  The keep bitmap keeps its layout: a lane assembles its 16 decisions of a tile
+// and one v_permlane16_swap joins the two halves of each 32-key word.
+// max3 as one instruction: fmaxf on an MFMA result makes hipcc canonicalise it first
+// (a v_max_f32 x, x per operand)
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// o[n][j] += p * v[j] for the four queries n of a lane and the 8 dims of one key, the key's
+// probability the lo (H = 0) or hi (H = 1) half of pn[n]: one statement (no pads)
+#define VAESNE_PV_ROW(H, n)                                                                   \
+  "v_pk_fma_f32 %" #n "0, %16, %" #n "P, %" #n "0 " H "\n"
+template <int H>
+__device__ __forceinline__ void pv_key(f2 (&o)[4][4], const f2 (&vr)[4], const f2 (&pn)[4]) {
+  if constexpr (H == 0)
+    asm("v_pk_fma_f32 %0, %16, %20, %0 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %4, %16, %21, %4 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %8, %16, %22, %8 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %12, %16, %23, %12 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %1, %17, %20, %1 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %5, %17, %21, %5 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %9, %17, %22, %9 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %13, %17, %23, %13 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %2, %18, %20, %2 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %6, %18, %21, %6 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %10, %18, %22, %10 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %14, %18, %23, %14 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %3, %19, %20, %3 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %7, %19, %21, %7 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %11, %19, %22, %11 op_sel_hi:[1,0,1]\n"
+        "v_pk_fma_f32 %15, %19, %23, %15 op_sel_hi:[1,0,1]"
+        : "+v"(o[0][0]), "+v"(o[0][1]), "+v"(o[0][2]), "+v"(o[0][3]), "+v"(o[1][0]),
+          "+v"(o[1][1]), "+v"(o[1][2]), "+v"(o[1][3]), "+v"(o[2][0]), "+v"(o[2][1]),
+          "+v"(o[2][2]), "+v"(o[2][3]), "+v"(o[3][0]), "+v"(o[3][1]), "+v"(o[3][2]), "+v"(o[3][3])
+        : "v"(vr[0]), "v"(vr[1]), "v"(vr[2]), "v"(vr[3]), "v"(pn[0]), "v"(pn[1]), "v"(pn[2]),
+          "v"(pn[3]));
+  else
+    asm("v_pk_fma_f32 %0, %16, %20, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %4, %16, %21, %4 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %8, %16, %22, %8 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %12, %16, %23, %12 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %1, %17, %20, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %5, %17, %21, %5 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %9, %17, %22, %9 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %13, %17, %23, %13 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %2, %18, %20, %2 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %6, %18, %21, %6 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %10, %18, %22, %10 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %14, %18, %23, %14 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %3, %19, %20, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %7, %19, %21, %7 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %11, %19, %22, %11 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
+        "v_pk_fma_f32 %15, %19, %23, %15 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
+        : "+v"(o[0][0]), "+v"(o[0][1]), "+v"(o[0][2]), "+v"(o[0][3]), "+v"(o[1][0]),
+          "+v"(o[1][1]), "+v"(o[1][2]), "+v"(o[1][3]), "+v"(o[2][0]), "+v"(o[2][1]),
+          "+v"(o[2][2]), "+v"(o[2][3]), "+v"(o[3][0]), "+v"(o[3][1]), "+v"(o[3][2]), "+v"(o[3][3])
+        : "v"(vr[0]), "v"(vr[1]), "v"(vr[2]), "v"(vr[3]), "v"(pn[0]), "v"(pn[1]), "v"(pn[2]),
+          "v"(pn[3]));
+}
+#undef VAESNE_PV_ROW
+typedef float f4v __attribute__((ext_vector_type(4)));
+// NWV waves per workgroup (64 queries each) share each staged key tile
+template <bool DROP, int NWV>
+__global__ __launch_bounds__(64 * NWV) void attn_fwd_mfma_kernel(AttnArgs a) {
+  constexpr int FM_NT = 64 * NWV, FM_QB = 64 * NWV;
+  __shared__ __attribute__((aligned(16))) float Ka[TK * 8];   // A-operand image of the K tile
+  __shared__ __attribute__((aligned(16))) float Vs[TK * 8];
+  __shared__ __attribute__((aligned(16))) float Kb[TK];
+  __shared__ uint32_t Kp[TK / 2];                            // the tile's key-pair hash mixes
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int nqb = (a.Lq + FM_QB - 1) / FM_QB;
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int qb = wg % nqb, bh = wg / nqb;
+  const int b = bh / a.H, h = bh - b * a.H;
+  int qrow[4];
+  float qop[4][2];            // B operands: Q[query][4c + g] * scale_log2
+  f2 o[4][4];                 // o[n][dims 2j, 2j + 1]
+  float m[4];
+  f2 l[4];                    // l[n]: two partial sums (even / odd keys), added at the end
+  uint32_t rk[4], w[4];
+  uint32_t skey = 0u;
+  if (DROP) skey = key_of(a.rng_state, a.call_id);
+  {
+    const float* qbase = a.q + (int64_t)b * a.q_bs + h * 8 + g;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      qrow[n] = qb * FM_QB + wave * 64 + 16 * n + col;
+      const int qc = min(qrow[n], a.Lq - 1);
+      qop[n][0] = qbase[(int64_t)qc * a.q_ls] * a.scale_log2;
+      qop[n][1] = qbase[(int64_t)qc * a.q_ls + 4] * a.scale_log2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[n][j] = bc(0.f);
+      m[n] = M_INIT;
+      l[n] = bc(0.f);
+      w[n] = 0u;
+      if (DROP) rk[n] = attn_row_key(skey, (uint32_t)((int64_t)bh * a.Lq + qc));
+    }
+  }
+  const float* kg = a.k + (int64_t)b * a.k_bs + h * 8;
+  const float* vg = a.v + (int64_t)b * a.v_bs + h * 8;
+  const float* kbg = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
+  uint32_t* bitp = DROP ? a.bits + (int64_t)bh * a.nw * a.Lq : nullptr;
+  const int kbeg = blockIdx.y * a.kchunk, klim = min(a.Lk, kbeg + a.kchunk);
+  // issue-early / write-late staging of the next tile (as attn_fwd_kernel's ASYNC path):
+  // thread t < 128 holds K float4 (row t/2, half t%2), t >= 128 the V float4 of row (t-128)/2,
+  // t < 64 the key bias of row t
+  float4 rKV = make_float4(0.f, 0.f, 0.f, 0.f);
+  float rB = -INFINITY;
+  const int st = threadIdx.x, shalf = st & 1, srow = (st & 127) >> 1;
+  auto issue = [&](int kt) {
+    if (st >= 256) return;
+    const bool ok = kt + srow < klim;
+    const int64_t kc = min(kt + srow, klim - 1);
+    const float* src = st < 128 ? kg + kc * a.k_ls : vg + kc * a.v_ls;
+    rKV = ok ? *reinterpret_cast<const float4*>(src + 4 * shalf) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (st < TK) rB = kt + st < klim ? (kbg ? kbg[kt + st] : 0.f) : -INFINITY;
+  };
+  if (kbeg < klim) issue(kbeg);
+  for (int kt = kbeg; kt < klim; kt += TK) {
+    __syncthreads();
+    if (st < 128) {
+      // key srow, dims 4 shalf + k -> A operand (m-tile mt, k-step c = shalf) of lane
+      // rho + 16 k, rho = 4 (srow >> 4) + (srow & 3), mt = (srow >> 2) & 3
+      const int rho = 4 * (srow >> 4) + (srow & 3), mt = (srow >> 2) & 3;
+      float* dst = Ka + (mt * 64 + rho) * 2 + shalf;
+      dst[0] = rKV.x; dst[32] = rKV.y; dst[64] = rKV.z; dst[96] = rKV.w;
+    } else if (st < 256) {
+      *reinterpret_cast<float4*>(Vs + srow * 8 + 4 * shalf) = rKV;
+    }
+    if (st < TK) Kb[st] = rB;
+    if (DROP && st < TK / 2) Kp[st] = attn_keypair_mix(skey, (uint32_t)((kt >> 1) + st));
+    __syncthreads();
+    if (kt + TK < klim) issue(kt + TK);   // next tile's loads fly under this compute
+    // the next m-tile's scores are issued before this one's VALU work (their matrix-core
+    // latency hides under it)
+    auto scores = [&](int mt, f4v (&s)[4]) {
+      const f2 ka = *reinterpret_cast<const f2*>(Ka + (mt * 64 + lane) * 2);
+      const float4 kb4 = *reinterpret_cast<const float4*>(Kb + 16 * g + 4 * mt);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        f4v acc = {kb4.x, kb4.y, kb4.z, kb4.w};
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ka.x, qop[n][0], acc, 0, 0, 0);
+        s[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(ka.y, qop[n][1], acc, 0, 0, 0);
+      }
+    };
+    f4v sn[4];
+    scores(0, sn);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      f4v s[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) s[n] = sn[n];
+      if (mt < 3) scores(mt + 1, sn);
+      // lazy rescaling (attn_fwd_kernel): the origin moves when a score passes it by 8
+      bool move = false;
+      float x[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        x[n] = vmax3(vmax3(m[n], s[n].x, s[n].y), s[n].z, s[n].w);
+        move |= x[n] > m[n] + 8.f;
+      }
+      if (__any(move)) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const float c = ex2(m[n] - x[n]);
+          m[n] = x[n];
+          l[n] *= bc(c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[n][j] *= c;
+        }
+      }
+      f2 p[4][2];   // p[n][pair]: keys (2 pair, 2 pair + 1) of this m-tile
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        p[n][0] = ex2((f2){s[n].x, s[n].y} - bc(m[n]));
+        p[n][1] = ex2((f2){s[n].z, s[n].w} - bc(m[n]));
+        l[n] += p[n][0] + p[n][1];
+      }
+      if (DROP) {
+        const uint2 kpm = *reinterpret_cast<const uint2*>(Kp + 8 * g + 2 * mt);
+        bool klo[4][2], khi[4][2];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const uint32_t bits = attn_pair_bits_mixed(rk[n], j ? kpm.y : kpm.x);
+            klo[n][j] = (bits & 0xffffu) >= a.thr;
+            khi[n][j] = (bits >> 16) >= a.thr;
+          }
+        }
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            w[n] = push_bit(push_bit(w[n], __builtin_amdgcn_ballot_w64(klo[n][j])),
+                            __builtin_amdgcn_ballot_w64(khi[n][j]));
+            p[n][j] = sel2(klo[n][j], khi[n][j], p[n][j]);
+          }
+        }
+      }
+      // o[n] += p[n][key] * v[key] over the lane's four keys of this m-tile
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f2 vr[4];
+        lrow2<8>(Vs + (16 * g + 4 * mt + i) * 8, vr);
+        const f2 pn[4] = {p[0][i >> 1], p[1][i >> 1], p[2][i >> 1], p[3][i >> 1]};
+        if (i & 1)
+          pv_key<1>(o, vr, pn);
+        else
+          pv_key<0>(o, vr, pn);
+      }
+    }
+    if (DROP) {
+      // this lane's 16 decisions (key 16g + b at bit b), the two halves of each 32-key word
+      // joined across lane rows (g, g ^ 1); the bits the VALU kernel would not write (keys
+      // past the last 8-key group it visits) cleared
+      const int kend = min(TK, klim - kt);
+      const int word = (kt >> 5) + (g >> 1);
+      const int nvalid = min(32, max(0, ((kend + 7) & ~7) - 32 * (g >> 1)));
+      const uint32_t vmask = nvalid >= 32 ? 0xffffffffu : ((1u << nvalid) - 1u);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const uint32_t f = __builtin_bitreverse32(w[n] << 16);
+        const auto r = __builtin_amdgcn_permlane16_swap(f, f, false, false);
+        const uint32_t wd = (r[0] | (r[1] << 16)) & vmask;
+        if ((g & 1) == 0 && nvalid > 0 && qrow[n] < a.Lq) bitp[(int64_t)word * a.Lq + qrow[n]] = wd;
+        w[n] = 0u;
+      }
+    }
+  }
+  // the four lanes of a query (l, l ^ 16, l ^ 32, l ^ 48) combine their states
+  const float ik = DROP ? a.inv_keep : 1.f;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    float M = fmaxf(m[n], __shfl_xor(m[n], 16));
+    M = fmaxf(M, __shfl_xor(M, 32));
+    const float c = ex2(m[n] - M);
+    float L = (l[n].x + l[n].y) * c;
+    L += __shfl_xor(L, 16);
+    L += __shfl_xor(L, 32);
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float u0 = o[n][j].x * c, u1 = o[n][j].y * c;
+      u0 += __shfl_xor(u0, 16);
+      u1 += __shfl_xor(u1, 16);
+      u0 += __shfl_xor(u0, 32);
+      u1 += __shfl_xor(u1, 32);
+      r[2 * j] = u0;
+      r[2 * j + 1] = u1;
+    }
+    const int q = qrow[n];
+    if (g != 0 || q >= a.Lq) continue;
+    if (a.ml) {   // split launch: un-normalised partial o and (m, l) of this key chunk
+      str<8>(a.o_out + blockIdx.y * a.o_ss + (int64_t)b * a.o_bs + (int64_t)q * a.o_ls + h * 8, r);
+      *reinterpret_cast<float2*>(a.ml + ((int64_t)blockIdx.y * a.B * a.H + bh) * a.Lq * 2 + 2 * q) =
+          make_float2(M, L);
+    } else {
+      const float inv = ik / L;    // L == 0 (every key masked) -> NaN, as the reference
+#pragma unroll
+      for (int d = 0; d < 8; ++d) r[d] *= inv;
+      str<8>(a.o_out + (int64_t)b * a.o_bs + (int64_t)q * a.o_ls + h * 8, r);
+      a.lse[(int64_t)bh * a.Lq + q] = M + __log2f(L);
+    }
+  }
+}
+
 // sum of v[0..15] over the 64 lanes of a wave; lane l returns the total of
 // component l >> 2.  Transposing butterfly: each exchange level sends half of
 // the live components to the partner lane group and keeps the other half, so
@@ -1841,6 +2121,18 @@ Geo pick_geo(int64_t bh, int L) {
   return best;
 }
 
+// the dh-8 forward's score products on the matrix cores (attn_fwd_mfma_kernel);
+// VAESNE_ATTN_MFMA_FWD=0 (or a forced geometry) selects the packed-VALU kernel
+// VAESNE_ATTN_MFMA_FWD = 0 / 4 / 8: off / waves per workgroup (default 4)
+int mfma_fwd_waves() {
+  static const int w = [] {
+    const char* e = getenv("VAESNE_ATTN_MFMA_FWD");
+    const int v = e ? atoi(e) : 4;
+    return v == 0 ? 0 : (v == 8 ? 8 : 4);
+  }();
+  return w;
+}
+
 // tuning / A/B hook: VAESNE_ATTN_FUSED_DQ=0 keeps dQ in its own kernel
 bool fused_dq_enabled() {
   static const bool on = [] {
@@ -2025,6 +2317,21 @@ int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s, bool b
   } else {
     sp = {1, a.Lk};
   }
+  if (DHV == 8 && !bits_in && mfma_fwd_waves() && g_forced.nt == 0) {
+    const int nwv = mfma_fwd_waves(), qb = 64 * nwv;
+    dim3 grid((unsigned)((int64_t)a.B * a.H * ((a.Lq + qb - 1) / qb)), (unsigned)sp.n);
+    if (nwv == 8) {
+      if (p_drop > 0.f)
+        hipLaunchKernelGGL((attn_fwd_mfma_kernel<true, 8>), grid, dim3(512), 0, s, c);
+      else
+        hipLaunchKernelGGL((attn_fwd_mfma_kernel<false, 8>), grid, dim3(512), 0, s, c);
+    } else {
+      if (p_drop > 0.f)
+        hipLaunchKernelGGL((attn_fwd_mfma_kernel<true, 4>), grid, dim3(256), 0, s, c);
+      else
+        hipLaunchKernelGGL((attn_fwd_mfma_kernel<false, 4>), grid, dim3(256), 0, s, c);
+    }
+  } else {
   const Geo g = pick_geo((int64_t)a.B * a.H, a.Lq);
   VAESNE_GEO_SWITCH(g, {
     const int nqb = (a.Lq + 2 * NP * NTT - 1) / (2 * NP * NTT);
@@ -2036,6 +2343,7 @@ int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s, bool b
     else
       hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, c);
   })
+  }
   VAESNE_CHECK_LAUNCH();
   if (sp.n > 1) {
     const int64_t n = (int64_t)a.B * a.H * a.Lq;
