@@ -312,6 +312,8 @@ def roofline(device, B, in_step=None):
     lib = _lib.lib
     bits = torch.empty(lib.attn_keep_bits_size(N, H, L, L), dtype=torch.uint8, device=device)
     b, d, s3 = qkv.data_ptr(), dqkv.data_ptr(), L * 3 * E
+    # the fused backward's dQ partials (several key blocks per sequence), as _ops passes it
+    wsb = torch.empty(max(1, lib.attn_workspace(N, H, L, L, dh, 1) // 4), device=device)
 
     def fwd():
         lib.attn_fwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E,
@@ -324,13 +326,17 @@ def roofline(device, B, in_step=None):
                           kbias.data_ptr(), L, o.data_ptr(), L * E, E, lse.data_ptr(),
                           do.data_ptr(), L * E, E, d, s3, 3 * E, d + 4 * E, s3, 3 * E, d + 8 * E,
                           s3, 3 * E, N, H, L, L, dh, pd, st.data_ptr(), 7, bits.data_ptr(),
-                          None, _lib.stream())
+                          wsb.data_ptr(), _lib.stream())
 
     fwd()
     scores = N * H * L * L
     res = {}
-    for name, kern, fn, fl in [("fwd", "attn_fwd_kernel", fwd, 4 * dh),
-                               ("bwd", "attn_bwd_kv_kernel", bwd(lib.attn_bwd), 8 * dh)]:
+    mf = os.environ.get("VAESNE_ATTN_MFMA_FWD", "4") != "0"
+    mb = os.environ.get("VAESNE_ATTN_MFMA_BWD", "0") != "0"
+    for name, kern, fn, fl in [("fwd", "attn_fwd_mfma_kernel" if mf else "attn_fwd_kernel", fwd,
+                                4 * dh),
+                               ("bwd", "attn_bwd_mfma_kernel" if mb else "attn_bwd_kv_kernel",
+                                bwd(lib.attn_bwd), 8 * dh)]:
         t = time_kernel(fn, 20, device)
         res[name] = dict(kernel=kern, ms=t * 1e3, tflops=scores * fl / t / 1e12,
                          flops_per_launch=scores * fl)

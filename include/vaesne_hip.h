@@ -221,6 +221,14 @@ int vaesne_attn_rep_config(int fnt, int frc, int bnt, int bnp, int brc, int bwgs
  * the automatic choice.  Process-wide; not for use while launches are in flight. */
 int vaesne_attn_force_geometry(int nt, int np);
 
+/* Test / tuning hook: the head_dim-8 matrix-core attention kernels (S = Q K^T and, in the
+ * fused backward, dP and dQ on v_mfma_f32_16x16x4_f32).  fwd_waves / bwd_waves: 0 = the
+ * packed-VALU kernel, 4 or 8 waves per workgroup; fwd_unpacked: P V as unpacked FMAs;
+ * bwd_variant: code-shape variant (0-4, 8, 12).  A negative argument keeps its setting
+ * (initially VAESNE_ATTN_MFMA_FWD / _FWD_UNPK / _BWD / _BWD_V); fwd_waves = -2 restores
+ * those load-time settings.  Process-wide; not while launches are in flight. */
+int vaesne_attn_mfma_config(int fwd_waves, int fwd_unpacked, int bwd_waves, int bwd_variant);
+
 /* ---- fused decoder-block tail --------------------------------------------------
  * Everything of a decoder TransformerBlock after its masked self-attention core
  * (util_layers.py:292-307 as called by SpectraLayers.py:61-62 and

@@ -650,7 +650,8 @@ def test_keep_bits_generator_matches_forward_and_bits_in_forward(geo, B, H, Lq, 
                                            (2, 4, 300, 77, 0.2, 0.1), (5, 2, 33, 40, 0.0, 0.1),
                                            (16, 4, 983, 983, 0.05, 0.1), (2, 4, 257, 1100, 0.5, 0.0),
                                            (2, 4, 500, 64, 0.0, 0.1)])
-def test_mfma_forward_matches_valu_forward(B, H, Lq, Lk, pm, p):
+@pytest.mark.parametrize("unpk", [0, 1])
+def test_mfma_forward_matches_valu_forward(B, H, Lq, Lk, pm, p, unpk):
     """The matrix-core forward (attn_fwd_mfma_kernel: scores on v_mfma_f32_16x16x4_f32,
     the auto path for head_dim 8) against the packed-VALU forward (a forced geometry):
     the same keep bitmap word for word, o and lse to fp32 summation order.  Includes
@@ -668,6 +669,7 @@ def test_mfma_forward_matches_valu_forward(B, H, Lq, Lk, pm, p):
     n = lib.attn_keep_bits_size(B, H, Lq, Lk) // 4
     ws = torch.empty(max(1, lib.attn_workspace(B, H, Lq, Lk, 8, 1) // 4), device=DEV)
     out = []
+    assert lib.attn_mfma_config(4, unpk, -1, -1) == 0
     for geo in ((0, 0), (256, 2)):
         assert lib.attn_force_geometry(*geo) == 0
         try:
@@ -682,6 +684,7 @@ def test_mfma_forward_matches_valu_forward(B, H, Lq, Lk, pm, p):
             out.append((o, lse, bits))
         finally:
             lib.attn_force_geometry(0, 0)
+            lib.attn_mfma_config(-2, -1, -1, -1)
     (o0, l0, b0), (o1, l1, b1) = out
     if p > 0:
         assert torch.equal(b0, b1)
@@ -691,6 +694,67 @@ def test_mfma_forward_matches_valu_forward(B, H, Lq, Lk, pm, p):
     assert _rel(o0[fin], o1[fin]) < 1e-5
     lf = torch.isfinite(l1)
     assert _rel(l0[lf], l1[lf]) < 1e-6
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,pm,p", [(3, 4, 982, 982, 0.05, 0.1), (2, 4, 983, 983, 0.0, 0.0),
+                                           (2, 4, 300, 77, 0.2, 0.1), (5, 2, 33, 40, 0.0, 0.1),
+                                           (16, 4, 983, 983, 0.05, 0.1), (2, 4, 257, 1100, 0.5, 0.0),
+                                           (2, 4, 500, 64, 0.0, 0.1), (4, 4, 130, 700, 0.1, 0.1)])
+@pytest.mark.parametrize("variant", [0, 8, 12])
+def test_mfma_backward_matches_valu_backward(B, H, Lq, Lk, pm, p, variant):
+    """The matrix-core backward (attn_bwd_mfma_kernel: S^T, dP^T and dQ on
+    v_mfma_f32_16x16x4_f32, the auto path for head_dim 8) against the packed-VALU fused
+    backward (a forced geometry) on the same forward: dQ, dK, dV to fp32 summation order
+    (the two sum keys and queries in different orders), NaN pattern equal.  Includes split
+    launches (query chunks summed after), several key blocks (dQ partials summed after),
+    ragged key blocks past Lk, key padding masks with fully masked rows."""
+    from VAESNe import _lib, rng
+    lib = _lib.lib
+    E, cid = H * 8, 555
+    g = torch.Generator(device=DEV).manual_seed(Lq + 5 * Lk)
+    q, k, v, do = (torch.randn(B, n, E, device=DEV, generator=g) for n in (Lq, Lk, Lk, Lq))
+    kbias = torch.where(torch.rand(B, Lk, device=DEV, generator=g) < pm, float("-inf"), 0.0)
+    if pm >= 0.5:
+        kbias[0] = float("-inf")
+    st = rng.state(DEV)
+    n = lib.attn_keep_bits_size(B, H, Lq, Lk) // 4
+    nws = 1
+    assert lib.attn_mfma_config(-1, -1, 4, variant) == 0
+    for geo in ((0, 0), (256, 2)):
+        assert lib.attn_force_geometry(*geo) == 0
+        nws = max(nws, lib.attn_workspace(B, H, Lq, Lk, 8, 1) // 4,
+                  lib.attn_workspace(B, H, Lq, Lk, 8, 0) // 4)
+    lib.attn_force_geometry(0, 0)
+    ws = torch.empty(nws, device=DEV)
+    bits = torch.zeros((n,), dtype=torch.int32, device=DEV)
+    o = torch.empty(B, Lq, E, device=DEV)
+    lse = torch.empty(B, H, Lq, device=DEV)
+    assert lib.attn_fwd(q.data_ptr(), Lq * E, E, k.data_ptr(), Lk * E, E, v.data_ptr(), Lk * E, E,
+                        kbias.data_ptr(), Lk, o.data_ptr(), Lq * E, E, lse.data_ptr(), B, H, Lq, Lk,
+                        8, p, st.data_ptr(), cid, bits.data_ptr(), 0, ws.data_ptr(),
+                        _lib.stream()) == 0
+    out = []
+    for geo in ((0, 0), (256, 2)):
+        assert lib.attn_force_geometry(*geo) == 0
+        try:
+            dq = torch.full((B, Lq, E), 7.0, device=DEV)
+            dk = torch.full((B, Lk, E), 7.0, device=DEV)
+            dv = torch.full((B, Lk, E), 7.0, device=DEV)
+            assert lib.attn_bwd(q.data_ptr(), Lq * E, E, k.data_ptr(), Lk * E, E, v.data_ptr(),
+                                Lk * E, E, kbias.data_ptr(), Lk, o.data_ptr(), Lq * E, E,
+                                lse.data_ptr(), do.data_ptr(), Lq * E, E, dq.data_ptr(), Lq * E, E,
+                                dk.data_ptr(), Lk * E, E, dv.data_ptr(), Lk * E, E, B, H, Lq, Lk, 8,
+                                p, st.data_ptr(), cid, bits.data_ptr(), ws.data_ptr(),
+                                _lib.stream()) == 0
+            torch.cuda.synchronize()
+            out.append((dq, dk, dv))
+        finally:
+            lib.attn_force_geometry(0, 0)
+    lib.attn_mfma_config(-2, -1, -1, -1)
+    for name, a, b in zip(("dq", "dk", "dv"), out[0], out[1]):
+        assert torch.equal(torch.isnan(a), torch.isnan(b)), name
+        fin = ~torch.isnan(b)
+        assert _rel(a[fin], b[fin]) < 2e-5, (name, _rel(a[fin], b[fin]))
 
 
 @pytest.mark.parametrize("M,with_h,defer", [(982 * 3, True, False), (251392, True, True),

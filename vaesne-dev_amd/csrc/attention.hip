@@ -665,6 +665,11 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
 // and one v_permlane16_swap joins the two halves of each 32-key word.
 // max3 as one instruction: fmaxf on an MFMA result makes hipcc canonicalise it first
 // (a v_max_f32 x, x per operand)
+// one unpacked FMA c + a b
+__device__ __forceinline__ float fma1(float a, float b, float c) {
+  asm("v_fma_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+  return c;
+}
 __device__ __forceinline__ float vmax3(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -724,7 +729,8 @@ __device__ __forceinline__ void pv_key(f2 (&o)[4][4], const f2 (&vr)[4], const f
 #undef VAESNE_PV_ROW
 typedef float f4v __attribute__((ext_vector_type(4)));
 // NWV waves per workgroup (64 queries each) share each staged key tile
-template <bool DROP, int NWV>
+// UNPK: P V as unpacked v_fma_f32 (packed fp32 stalls beside the matrix cores' work)
+template <bool DROP, int NWV, bool UNPK = false>
 __global__ __launch_bounds__(64 * NWV) void attn_fwd_mfma_kernel(AttnArgs a) {
   constexpr int FM_NT = 64 * NWV, FM_QB = 64 * NWV;
   __shared__ __attribute__((aligned(16))) float Ka[TK * 8];   // A-operand image of the K tile
@@ -869,10 +875,21 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_mfma_kernel(AttnArgs a) {
         f2 vr[4];
         lrow2<8>(Vs + (16 * g + 4 * mt + i) * 8, vr);
         const f2 pn[4] = {p[0][i >> 1], p[1][i >> 1], p[2][i >> 1], p[3][i >> 1]};
-        if (i & 1)
+        if constexpr (UNPK) {
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+            const float pk = (i & 1) ? pn[n].y : pn[n].x;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+              o[n][jj].x = fma1(vr[jj].x, pk, o[n][jj].x);
+              o[n][jj].y = fma1(vr[jj].y, pk, o[n][jj].y);
+            }
+          }
+        } else if (i & 1) {
           pv_key<1>(o, vr, pn);
-        else
+        } else {
           pv_key<0>(o, vr, pn);
+        }
       }
     }
     if (DROP) {
@@ -1252,6 +1269,371 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
     for (int d = 0; d < DH; ++d) { r0[d] = dv[p][d].x; r1[d] = dv[p][d].y; }
     if (j0 < a.Lk) str<DH>(dvb + (int64_t)j0 * a.dv_ls, r0);
     if (j1 < a.Lk) str<DH>(dvb + (int64_t)j1 * a.dv_ls, r1);
+  }
+}
+
+// ============== dK, dV, dQ with the score products on the matrix cores ================
+// head_dim 8, fused dQ.  Wave wv of the workgroup owns the 64 keys kb*KB + 64 wv .. + 63 as
+// four 16-key m-tiles; queries stream through the staged 64-query tiles in 16-query
+// sub-tiles.  Per (m-tile, sub-tile), v_mfma_f32_16x16x4_f32 gives S^T = K Q^T (starting at
+// the key bias: bit for bit the forward's score chain) and dP^T = V dO^T, lane l holding
+// query l & 15 and keys 16m + 4r + (l >> 4), r = 0..3 (the A rows are permuted so that
+// register r of dS is the B operand of dQ's key chunk r).  P and dS on the VALU (the
+// keep bits of a lane's four keys gathered from the bitmap word by one multiply);
+// dQ^T += K^T dS^T on the matrix cores; aP and dS are transposed through LDS so that dV and
+// dK accumulate on the packed VALU with lane = key 16m + (l & 15) over queries 4 (l >> 4) + i;
+// the four lanes of a key are summed once at the end.
+// Of the ~27 VALU instructions per score pair of attn_bwd_kv_kernel (score and dP chains,
+// dQ sums) about half remain: the exponentials, the dS algebra and the dV / dK updates.
+__device__ __forceinline__ uint32_t keep_nib(uint32_t w, int sh) {
+  // bits sh, sh + 4, sh + 8, sh + 12 of w -> bits 0..3 (0x1248 moves bit 4r to 12 + r; the
+  // other partial products land on distinct bits, so nothing carries into 12..15)
+  return (((w >> sh) & 0x1111u) * 0x1248u) >> 12 & 15u;
+}
+// V (tuning variants, VAESNE_ATTN_MFMA_BWD_V): bit 0 dV / dK updates as plain vector code
+// (the compiler may unpack them beside MFMAs) instead of op_sel asm; bit 1 interleave the
+// matrix-core products into the VALU stream (sched_group_barrier); bit 2 no prefetch of
+// the next sub-tile's S^T / dP^T
+template <bool DROP, int NWV, int V>
+__global__ __launch_bounds__(64 * NWV) void attn_bwd_mfma_kernel(AttnArgs a) {
+  constexpr bool PLAIN = V & 1, SGB = V & 2, PREF = !(V & 4), UNPK = V & 8;
+  constexpr int DH = 8, NTT = 64 * NWV, KB = 64 * NWV;
+  constexpr int NWB = KB / 32, NWBP = NWB + 1;
+  constexpr int TS = 20;                          // transpose row stride (16-byte rows)
+  __shared__ __attribute__((aligned(16))) float Qs[TK * DH];
+  __shared__ __attribute__((aligned(16))) float Ds_[TK * DH];   // dO tile * 1/(1-p)
+  __shared__ float Ls[TK], Dd[TK];
+  __shared__ uint32_t Ws[TK * NWBP];
+  constexpr int QWS = 16;                         // per-wave dQ row stride (rows d 0..15)
+  __shared__ __attribute__((aligned(16))) float Qw[NWV * TK * QWS];         // per-wave dQ
+  __shared__ __attribute__((aligned(16))) float Tr[NWV * 4 * 2 * 16 * TS];  // aP / dS transposes
+  __shared__ float4 Mt[16];
+  if (DROP && threadIdx.x < 16)
+    Mt[threadIdx.x] = make_float4((float)(threadIdx.x & 1), (float)((threadIdx.x >> 1) & 1),
+                                  (float)((threadIdx.x >> 2) & 1), (float)((threadIdx.x >> 3) & 1));
+  const int nkb = (a.Lk + KB - 1) / KB;
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int kb = wg % nkb, bh = wg / nkb;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int t = threadIdx.x, wv = t >> 6, l = t & 63, c16 = l & 15, g = l >> 4;
+  const int kw0 = kb * KB + 64 * wv;
+  // constant operands: S / dP A rows (row c16 of m-tile m = key 4 (c16 & 3) + (c16 >> 2)),
+  // dQ's A = K^T (row d = c16 < 8, key chunk cc: key 4 cc + g), the key biases of the
+  // accumulator rows (register r = key 4r + g; -inf past Lk)
+  float kA[4][2], vA[4][2], kT[4][4];
+  f4v kb4[4];
+  f2 dv[4][4], dk[4][4];
+  {
+    const float* kbase = a.k + (int64_t)b * a.k_bs + h * DH;
+    const float* vbase = a.v + (int64_t)b * a.v_bs + h * DH;
+    const float* kbp = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int64_t ja = min(kw0 + 16 * m + 4 * (c16 & 3) + (c16 >> 2), a.Lk - 1);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        kA[m][c] = kbase[ja * a.k_ls + 4 * c + g];
+        vA[m][c] = vbase[ja * a.v_ls + 4 * c + g];
+      }
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const int64_t jt = min(kw0 + 16 * m + 4 * cc + g, a.Lk - 1);
+        kT[m][cc] = c16 < DH ? kbase[jt * a.k_ls + c16] : 0.f;
+      }
+      float bb[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = kw0 + 16 * m + 4 * r + g;
+        bb[r] = j < a.Lk ? (kbp ? kbp[j] : 0.f) : -INFINITY;
+      }
+      kb4[m] = (f4v){bb[0], bb[1], bb[2], bb[3]};
+#pragma unroll
+      for (int p = 0; p < 4; ++p) { dv[m][p] = bc(0.f); dk[m][p] = bc(0.f); }
+    }
+  }
+  const float* qg = a.q + (int64_t)b * a.q_bs + h * DH;
+  const float* dg = a.dout + (int64_t)b * a.do_bs + h * DH;
+  const float* og = a.o + (int64_t)b * a.o_bs + h * DH;
+  const float* lg = a.lse + (int64_t)bh * a.Lq;
+  const uint32_t* bitp = DROP ? a.bits + (int64_t)bh * a.nw * a.Lq : nullptr;
+  const int wfirst = (kb * KB) >> 5;
+  const int qbeg = blockIdx.y * a.qchunk, qlim = min(a.Lq, qbeg + a.qchunk);
+  // issue-early / write-late staging (attn_bwd_kv_kernel's ASYNC path): t < 128 dO and O
+  // float4 (row t/2, half t%2), 128 <= t < 256 the Q float4 of row (t-128)/2, t < 64 the
+  // lse of row t, every thread NWS keep words
+  constexpr int NWS = DROP ? (TK * NWB) / NTT : 1;
+  static_assert((TK * NWB) % NTT == 0, "keep words per thread");
+  float4 rA = make_float4(0.f, 0.f, 0.f, 0.f), rO = rA;
+  float rL = INFINITY;
+  uint32_t rW[NWS];
+  auto issue = [&](int qt) {
+    const int half = t & 1, row = (t & 127) >> 1, qi = qt + row;
+    const bool ok = qi < qlim;
+    const int64_t qc = min(qi, qlim - 1);
+    if (t < 128) {
+      rA = ok ? *reinterpret_cast<const float4*>(dg + qc * a.do_ls + 4 * half) : make_float4(0.f, 0.f, 0.f, 0.f);
+      rO = ok ? *reinterpret_cast<const float4*>(og + qc * a.o_ls + 4 * half) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if (t < 256) {
+      rA = ok ? *reinterpret_cast<const float4*>(qg + qc * a.q_ls + 4 * half) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (t < TK) rL = qt + t < qlim ? lg[qt + t] : INFINITY;
+    if (DROP) {
+#pragma unroll
+      for (int j = 0; j < NWS; ++j) {
+        const int idx = j * NTT + t, i = idx % TK, w = idx / TK;
+        const int word = wfirst + w;
+        rW[j] = (qt + i < qlim && word < a.nw) ? bitp[(int64_t)word * a.Lq + qt + i] : 0u;
+      }
+    }
+  };
+  auto commit = [&]() {
+    const int half = t & 1, row = (t & 127) >> 1;
+    if (t < 128) {
+      // D = rowsum(dO * O) in the fmaf order over d = 0..7 (attn_bwd_kv_kernel)
+      float pd = fmaf(rA.x, rO.x, 0.f);
+      pd = fmaf(rA.y, rO.y, pd);
+      pd = fmaf(rA.z, rO.z, pd);
+      pd = fmaf(rA.w, rO.w, pd);
+      const float p0 = __shfl_xor(pd, 1);
+      if (half) {
+        float Di = fmaf(rA.x, rO.x, p0);
+        Di = fmaf(rA.y, rO.y, Di);
+        Di = fmaf(rA.z, rO.z, Di);
+        Di = fmaf(rA.w, rO.w, Di);
+        Dd[row] = Di;
+      }
+      const float m = a.inv_keep;
+      *reinterpret_cast<float4*>(Ds_ + row * DH + 4 * half) =
+          make_float4(rA.x * m, rA.y * m, rA.z * m, rA.w * m);
+    } else if (t < 256) {
+      const float m = a.scale_log2;
+      *reinterpret_cast<float4*>(Qs + row * DH + 4 * half) =
+          make_float4(rA.x * m, rA.y * m, rA.z * m, rA.w * m);
+    }
+    if (t < TK) Ls[t] = rL;      // +inf for padding rows -> p = 0
+    if (DROP) {
+#pragma unroll
+      for (int j = 0; j < NWS; ++j) {
+        const int idx = j * NTT + t, i = idx % TK, w = idx / TK;
+        Ws[i * NWBP + w] = rW[j];
+      }
+    }
+  };
+  float* trw = Tr + wv * (4 * 2 * 16 * TS);
+  if (qbeg < qlim) issue(qbeg);
+  for (int qt = qbeg; qt < qlim; qt += TK) {
+    __syncthreads();
+    commit();
+    __syncthreads();
+    if (qt + TK < qlim) issue(qt + TK);   // next tile's loads fly under this compute
+    const int qend = min(TK, qlim - qt);
+    // S^T / dP^T of sub-tile j (the matrix-core half of its work); each sub-tile's products
+    // are issued one sub-tile ahead, so the matrix cores run them under the previous
+    // sub-tile's VALU work (dS algebra, dV / dK updates) instead of in front of it
+    auto scores = [&](int j, f4v (&S)[4], f4v (&G)[4]) {
+      const int qq = 16 * j + c16;
+      const float qB0 = Qs[qq * DH + g], qB1 = Qs[qq * DH + 4 + g];
+      const float dB0 = Ds_[qq * DH + g], dB1 = Ds_[qq * DH + 4 + g];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        S[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(kA[m][0], qB0, kb4[m], 0, 0, 0);
+        S[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(kA[m][1], qB1, S[m], 0, 0, 0);
+        G[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(vA[m][0], dB0, (f4v){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        G[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(vA[m][1], dB1, G[m], 0, 0, 0);
+      }
+    };
+    f4v S[4], G[4];
+    if (PREF) scores(0, S, G);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (16 * j < qend) {
+        if (!PREF) scores(j, S, G);
+        const int qq = 16 * j + c16;
+        const f2 li = bc(Ls[qq]), Di = bc(Dd[qq]);
+        uint32_t wd0 = 0u, wd1 = 0u;
+        if (DROP) { wd0 = Ws[qq * NWBP + 2 * wv]; wd1 = Ws[qq * NWBP + 2 * wv + 1]; }
+        f4v dq0 = {0.f, 0.f, 0.f, 0.f}, dq1 = dq0;
+        // (the transposes through Tr need no barrier: LDS runs a wave's accesses in order,
+        // and the compiler cannot reorder these writes and reads, whose addresses may alias)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const f2 p0 = ex2((f2){S[m].x, S[m].y} - li), p1 = ex2((f2){S[m].z, S[m].w} - li);
+          const f2 g0 = {G[m].x, G[m].y}, g1 = {G[m].z, G[m].w};
+          f2 aP0 = p0, aP1 = p1, d0, d1;
+          if (DROP) {
+            // dS = pr * (keep * g - Di) = aP * g - pr * Di (attn_bwd_kv_kernel's order)
+            const float4 km = Mt[keep_nib(m < 2 ? wd0 : wd1, 16 * (m & 1) + g)];
+            aP0 = p0 * (f2){km.x, km.y};
+            aP1 = p1 * (f2){km.z, km.w};
+            d0 = fma2(aP0, g0, -(p0 * Di));
+            d1 = fma2(aP1, g1, -(p1 * Di));
+          } else {
+            d0 = p0 * (g0 - Di);
+            d1 = p1 * (g1 - Di);
+          }
+          f4v& acc = (m & 1) ? dq1 : dq0;
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kT[m][0], d0.x, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kT[m][1], d0.y, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kT[m][2], d1.x, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kT[m][3], d1.y, acc, 0, 0, 0);
+          // T[key 4r + g][query c16]
+          float* tp = trw + m * (2 * 16 * TS) + g * TS + c16;
+          tp[0] = aP0.x; tp[4 * TS] = aP0.y; tp[8 * TS] = aP1.x; tp[12 * TS] = aP1.y;
+          tp += 16 * TS;
+          tp[0] = d0.x; tp[4 * TS] = d0.y; tp[8 * TS] = d1.x; tp[12 * TS] = d1.y;
+        }
+        // the next sub-tile's products (its rows are staged: padding rows are zeros)
+        if (PREF && j < 3) scores(j + 1, S, G);
+        // dV[key] += aP[q, key] dO[q]  over this lane's queries 16j + 4g + i
+        {
+          f2 dr[4][4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) lrow2<8>(Ds_ + (16 * j + 4 * g + i) * DH, dr[i]);
+          if constexpr (UNPK) {
+            // unpacked v_fma_f32 (packed fp32 cannot issue beside the matrix cores' work:
+            // MI355X_MICROARCH.md); query i outermost, so dependent FMAs are 32 apart
+            float4 tv[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+              tv[m] = *reinterpret_cast<const float4*>(trw + m * (2 * 16 * TS) + c16 * TS + 4 * g);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int m = 0; m < 4; ++m) {
+                const float w = i == 0 ? tv[m].x : i == 1 ? tv[m].y : i == 2 ? tv[m].z : tv[m].w;
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                  dv[m][p].x = fma1(dr[i][p].x, w, dv[m][p].x);
+                  dv[m][p].y = fma1(dr[i][p].y, w, dv[m][p].y);
+                }
+              }
+          } else {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const float4 ap = *reinterpret_cast<const float4*>(trw + m * (2 * 16 * TS) + c16 * TS + 4 * g);
+            const f2 a01 = {ap.x, ap.y}, a23 = {ap.z, ap.w};
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+              if constexpr (PLAIN) {
+                dv[m][p] = fma2(dr[0][p], bc(a01.x), dv[m][p]);
+                dv[m][p] = fma2(dr[1][p], bc(a01.y), dv[m][p]);
+                dv[m][p] = fma2(dr[2][p], bc(a23.x), dv[m][p]);
+                dv[m][p] = fma2(dr[3][p], bc(a23.y), dv[m][p]);
+              } else {
+                dv[m][p] = fma2_lo(dr[0][p], a01, dv[m][p]);
+                dv[m][p] = fma2_hi(dr[1][p], a01, dv[m][p]);
+                dv[m][p] = fma2_lo(dr[2][p], a23, dv[m][p]);
+                dv[m][p] = fma2_hi(dr[3][p], a23, dv[m][p]);
+              }
+            }
+          }
+          }
+        }
+        // dK[key] += dS[q, key] Qs[q]
+        {
+          f2 qr[4][4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) lrow2<8>(Qs + (16 * j + 4 * g + i) * DH, qr[i]);
+          if constexpr (UNPK) {
+            // unpacked v_fma_f32 (packed fp32 cannot issue beside the matrix cores' work:
+            // MI355X_MICROARCH.md); query i outermost, so dependent FMAs are 32 apart
+            float4 tv[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+              tv[m] = *reinterpret_cast<const float4*>(trw + m * (2 * 16 * TS) + 16 * TS + c16 * TS + 4 * g);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int m = 0; m < 4; ++m) {
+                const float w = i == 0 ? tv[m].x : i == 1 ? tv[m].y : i == 2 ? tv[m].z : tv[m].w;
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                  dk[m][p].x = fma1(qr[i][p].x, w, dk[m][p].x);
+                  dk[m][p].y = fma1(qr[i][p].y, w, dk[m][p].y);
+                }
+              }
+          } else {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const float4 ds = *reinterpret_cast<const float4*>(trw + m * (2 * 16 * TS) + 16 * TS +
+                                                               c16 * TS + 4 * g);
+            const f2 s01 = {ds.x, ds.y}, s23 = {ds.z, ds.w};
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+              if constexpr (PLAIN) {
+                dk[m][p] = fma2(qr[0][p], bc(s01.x), dk[m][p]);
+                dk[m][p] = fma2(qr[1][p], bc(s01.y), dk[m][p]);
+                dk[m][p] = fma2(qr[2][p], bc(s23.x), dk[m][p]);
+                dk[m][p] = fma2(qr[3][p], bc(s23.y), dk[m][p]);
+              } else {
+                dk[m][p] = fma2_lo(qr[0][p], s01, dk[m][p]);
+                dk[m][p] = fma2_hi(qr[1][p], s01, dk[m][p]);
+                dk[m][p] = fma2_lo(qr[2][p], s23, dk[m][p]);
+                dk[m][p] = fma2_hi(qr[3][p], s23, dk[m][p]);
+              }
+            }
+          }
+          }
+        }
+        // dQ^T rows d = 4g + r of this sub-tile -> the wave's slot (rows 8..15 are zero:
+        // stored anyway, so no branch splits this block)
+        *reinterpret_cast<f4v*>(Qw + (wv * TK + qq) * QWS + 4 * g) = dq0 + dq1;
+        if constexpr (SGB) {
+          // spread the 32 matrix-core products over the VALU stream (one per 8 vector
+          // instructions) so one wave keeps both pipes fed
+#pragma unroll
+          for (int i = 0; i < 32; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+          }
+        }
+      }
+    }
+    // dQ rows of this tile: the waves' key ranges summed (fixed order); key block kb's
+    // share (nkb > 1: a partial slot, summed after the launch)
+    __syncthreads();
+    float* dqb = a.dq + kb * a.dq_ss + (int64_t)b * a.dq_bs + h * DH;
+    for (int idx = t; idx < qend * (DH / 4); idx += NTT) {
+      const int i = idx / (DH / 4), c = (idx - i * (DH / 4)) * 4;
+      float4 acc = *reinterpret_cast<const float4*>(Qw + i * QWS + c);
+#pragma unroll
+      for (int w = 1; w < NWV; ++w) {
+        const float4 u = *reinterpret_cast<const float4*>(Qw + (w * TK + i) * QWS + c);
+        acc.x += u.x; acc.y += u.y; acc.z += u.z; acc.w += u.w;
+      }
+      acc.x *= a.scale; acc.y *= a.scale; acc.z *= a.scale; acc.w *= a.scale;
+      *reinterpret_cast<float4*>(dqb + (int64_t)(qt + i) * a.dq_ls + c) = acc;
+    }
+  }
+  // the four lanes of a key (g = 0..3) hold partial dV / dK over their queries: a
+  // transposing butterfly (permlane32, then permlane16 swaps) leaves lane g with the totals
+  // of m-tile g -- component e = 16m + x: x < 8 dV dim x, x >= 8 dK dim x - 8
+  auto comp = [&](int e) -> float {
+    const int m = e >> 4, x = e & 15;
+    const f2 v = x < 8 ? dv[m][x >> 1] : dk[m][(x - 8) >> 1];
+    return (x & 1) ? v.y : v.x;
+  };
+  float u[32], s[16];
+#pragma unroll
+  for (int e = 0; e < 32; ++e) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(comp(e)),
+                                                    __float_as_uint(comp(e + 32)), false, false);
+    u[e] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(u[e]),
+                                                    __float_as_uint(u[e + 16]), false, false);
+    s[e] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  const int key = kw0 + 16 * g + c16;
+  if (key < a.Lk) {
+    const float kf = a.scale / a.scale_log2;
+    float rv[DH], rk[DH];
+#pragma unroll
+    for (int d = 0; d < DH; ++d) { rv[d] = s[d]; rk[d] = s[8 + d] * kf; }
+    str<DH>(a.dv + blockIdx.y * a.dk_ss + (int64_t)b * a.dv_bs + (int64_t)key * a.dv_ls + h * DH, rv);
+    str<DH>(a.dk + blockIdx.y * a.dk_ss + (int64_t)b * a.dk_bs + (int64_t)key * a.dk_ls + h * DH, rk);
   }
 }
 
@@ -2121,17 +2503,30 @@ Geo pick_geo(int64_t bh, int L) {
   return best;
 }
 
-// the dh-8 forward's score products on the matrix cores (attn_fwd_mfma_kernel);
-// VAESNE_ATTN_MFMA_FWD=0 (or a forced geometry) selects the packed-VALU kernel
-// VAESNE_ATTN_MFMA_FWD = 0 / 4 / 8: off / waves per workgroup (default 4)
-int mfma_fwd_waves() {
-  static const int w = [] {
-    const char* e = getenv("VAESNE_ATTN_MFMA_FWD");
-    const int v = e ? atoi(e) : 4;
-    return v == 0 ? 0 : (v == 8 ? 8 : 4);
-  }();
-  return w;
+// matrix-core attention kernels (head_dim 8): forward waves per workgroup (0 = the packed-
+// VALU kernel, 4, 8), its P V unpacked; fused backward waves (0 = packed VALU, 4, 8) and
+// code-shape variant.  From VAESNE_ATTN_MFMA_FWD / _FWD_UNPK / _BWD / _BWD_V at load, or
+// vaesne_attn_mfma_config().  A forced geometry selects the packed-VALU kernels.
+struct MfmaCfg { int fwd, fwd_unpk, bwd, bwd_v; };
+constexpr int kMfmaBwdV = 0;
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
 }
+int waves_or_off(int v) { return v == 0 ? 0 : (v == 8 ? 8 : 4); }
+bool bwd_variant_ok(int v) { return (v >= 0 && v <= 4) || v == 8 || v == 12; }
+MfmaCfg mfma_cfg_from_env() {
+  MfmaCfg c;
+  c.fwd = waves_or_off(env_int("VAESNE_ATTN_MFMA_FWD", 4));
+  c.fwd_unpk = env_int("VAESNE_ATTN_MFMA_FWD_UNPK", 0) == 1;
+  c.bwd = waves_or_off(env_int("VAESNE_ATTN_MFMA_BWD", 0));
+  c.bwd_v = env_int("VAESNE_ATTN_MFMA_BWD_V", kMfmaBwdV);
+  if (!bwd_variant_ok(c.bwd_v)) c.bwd_v = kMfmaBwdV;
+  return c;
+}
+MfmaCfg g_mfma = mfma_cfg_from_env();
+int mfma_fwd_waves() { return g_mfma.fwd; }
+bool mfma_fwd_unpacked() { return g_mfma.fwd_unpk != 0; }
 
 // tuning / A/B hook: VAESNE_ATTN_FUSED_DQ=0 keeps dQ in its own kernel
 bool fused_dq_enabled() {
@@ -2140,6 +2535,12 @@ bool fused_dq_enabled() {
     return !(e && e[0] == '0');
   }();
   return on;
+}
+
+int mfma_bwd_waves() { return g_mfma.bwd; }
+int mfma_bwd_variant() { return g_mfma.bwd_v; }
+bool mfma_bwd_on(int dh) {
+  return dh == 8 && mfma_bwd_waves() > 0 && g_forced.nt == 0 && fused_dq_enabled();
 }
 
 // Split launches for grids too small to fill the chip (the encoder's 983-token
@@ -2255,7 +2656,11 @@ int64_t fwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sp) {
   return (int64_t)sp.n * B * Lq * H * dh + (int64_t)sp.n * B * H * Lq * 2;
 }
 // key blocks of the dK/dV launch (the fused dQ's partial count)
-int kv_blocks(int64_t bh, int Lk) {
+int kv_blocks(int64_t bh, int Lk, int dh) {
+  if (mfma_bwd_on(dh)) {
+    const int kb = 64 * mfma_bwd_waves();
+    return (Lk + kb - 1) / kb;
+  }
   const Geo g = pick_geo(bh, Lk);
   return (Lk + 2 * g.np * g.nt - 1) / (2 * g.np * g.nt);
 }
@@ -2264,7 +2669,7 @@ int kv_blocks(int64_t bh, int Lk) {
 // several; the larger of the two so either path fits
 int64_t bwd_dq_floats(int B, int H, int Lq, int Lk, int dh, const Split& sq) {
   const int64_t unfused = (int64_t)(sq.n > 1 ? sq.n : 0) * B * Lq * H * dh;
-  const int nkb = kv_blocks((int64_t)B * H, Lk);
+  const int nkb = kv_blocks((int64_t)B * H, Lk, dh);
   const int64_t fused = dh == 8 && nkb > 1 ? (int64_t)nkb * B * Lq * H * dh : 0;
   return std::max(unfused, fused);
 }
@@ -2273,7 +2678,10 @@ int64_t bwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sq, Split& sk
   sk = {1, Lq};   // dK/dV: query chunks
   if (Lq <= 2 * SQ) return 0;
   sq = pick_split(waves_of((int64_t)B * H, Lq), Lk);
-  sk = pick_split(waves_of((int64_t)B * H, Lk), Lq);
+  const int64_t kv_waves = mfma_bwd_on(dh) ? (int64_t)B * H * kv_blocks((int64_t)B * H, Lk, dh) *
+                                                  mfma_bwd_waves()
+                                            : waves_of((int64_t)B * H, Lk);
+  sk = pick_split(kv_waves, Lq);
   return bwd_dq_floats(B, H, Lq, Lk, dh, sq) +
          (int64_t)(sk.n > 1 ? sk.n : 0) * B * Lk * H * dh * 2;
 }
@@ -2325,6 +2733,11 @@ int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s, bool b
         hipLaunchKernelGGL((attn_fwd_mfma_kernel<true, 8>), grid, dim3(512), 0, s, c);
       else
         hipLaunchKernelGGL((attn_fwd_mfma_kernel<false, 8>), grid, dim3(512), 0, s, c);
+    } else if (mfma_fwd_unpacked()) {
+      if (p_drop > 0.f)
+        hipLaunchKernelGGL((attn_fwd_mfma_kernel<true, 4, true>), grid, dim3(256), 0, s, c);
+      else
+        hipLaunchKernelGGL((attn_fwd_mfma_kernel<false, 4, true>), grid, dim3(256), 0, s, c);
     } else {
       if (p_drop > 0.f)
         hipLaunchKernelGGL((attn_fwd_mfma_kernel<true, 4>), grid, dim3(256), 0, s, c);
@@ -2376,7 +2789,7 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
   float* ws_dkv = ws && wsf > 0 ? ws + bwd_dq_floats(a.B, a.H, a.Lq, a.Lk, DHV, sq) : nullptr;
   // fused dK/dV/dQ (head_dim 8): one key block covers the whole key axis (dQ
   // written directly), or several write dQ partials into the workspace
-  const int nkb = kv_blocks((int64_t)a.B * a.H, a.Lk);
+  const int nkb = kv_blocks((int64_t)a.B * a.H, a.Lk, DHV);
   const bool fuse = DHV == 8 && part == 3 && fused_dq_enabled() &&
                     (nkb == 1 || (ws && wsf > 0));
   if (part & 1) {
@@ -2391,6 +2804,28 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
       c.dq = ws_dq; c.dq_bs = (int64_t)a.Lq * E; c.dq_ls = E;
       c.dq_ss = (int64_t)a.B * a.Lq * E;
     }
+    if (fuse && mfma_bwd_on(DHV)) {
+      dim3 grid((unsigned)((int64_t)a.B * a.H * nkb), (unsigned)sk.n);
+      if (mfma_bwd_waves() == 8) {
+        if (p_drop > 0.f)
+          hipLaunchKernelGGL((attn_bwd_mfma_kernel<true, 8, kMfmaBwdV>), grid, dim3(512), 0, s, c);
+        else
+          hipLaunchKernelGGL((attn_bwd_mfma_kernel<false, 8, kMfmaBwdV>), grid, dim3(512), 0, s, c);
+      } else {
+        switch (mfma_bwd_variant()) {
+#define VAESNE_BWD_V(VV)                                                                       \
+  case VV:                                                                                     \
+    if (p_drop > 0.f)                                                                          \
+      hipLaunchKernelGGL((attn_bwd_mfma_kernel<true, 4, VV>), grid, dim3(256), 0, s, c);       \
+    else                                                                                       \
+      hipLaunchKernelGGL((attn_bwd_mfma_kernel<false, 4, VV>), grid, dim3(256), 0, s, c);      \
+    break;
+          VAESNE_BWD_V(0) VAESNE_BWD_V(1) VAESNE_BWD_V(2) VAESNE_BWD_V(3)
+          VAESNE_BWD_V(4) VAESNE_BWD_V(8) VAESNE_BWD_V(12)
+#undef VAESNE_BWD_V
+        }
+      }
+    } else {
     const Geo gk = pick_geo((int64_t)a.B * a.H, a.Lk);
     VAESNE_GEO_SWITCH(gk, {
       const int nkb = (a.Lk + 2 * NP * NTT - 1) / (2 * NP * NTT);
@@ -2408,6 +2843,7 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
         hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, c);
       }
     })
+    }
     VAESNE_CHECK_LAUNCH();
     if (sk.n > 1) {
       launch_sum_chunks(c.dk, c.dk_ss, sk.n, a.B, a.Lk, E, a.dk, a.dk_bs, a.dk_ls, s);
@@ -2672,6 +3108,20 @@ VAESNE_API int vaesne_attn_force_geometry(int nt, int np) {
   if (nt == 0) { g_forced = {0, 0}; return 0; }
   if ((nt != 64 && nt != 128 && nt != 256) || (np != 1 && np != 2)) return (int)hipErrorInvalidValue;
   g_forced = {nt, np};
+  return 0;
+}
+
+VAESNE_API int vaesne_attn_mfma_config(int fwd_waves, int fwd_unpacked, int bwd_waves,
+                                       int bwd_variant) {
+  if (fwd_waves == -2) { g_mfma = mfma_cfg_from_env(); return 0; }
+  if ((fwd_waves >= 0 && fwd_waves != 0 && fwd_waves != 4 && fwd_waves != 8) ||
+      (bwd_waves >= 0 && bwd_waves != 0 && bwd_waves != 4 && bwd_waves != 8) ||
+      (bwd_variant >= 0 && !bwd_variant_ok(bwd_variant)) || fwd_unpacked > 1)
+    return (int)hipErrorInvalidValue;
+  if (fwd_waves >= 0) g_mfma.fwd = fwd_waves;
+  if (fwd_unpacked >= 0) g_mfma.fwd_unpk = fwd_unpacked;
+  if (bwd_waves >= 0) g_mfma.bwd = bwd_waves;
+  if (bwd_variant >= 0) g_mfma.bwd_v = bwd_variant;
   return 0;
 }
 
