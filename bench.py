@@ -135,16 +135,16 @@ class Step:
         try:
             from VAESNe.training_util import backward_negated
         except ImportError:
-            def backward_negated(v):
+            def backward_negated(v, out=None):
                 loss = -v
                 loss.backward()
-                return loss
+                return loss if out is None else out.copy_(loss.detach())
         self.opt.zero_grad(set_to_none=True)
         _mark("step")
         with deferred():   # parameter-gradient sums: one batched launch at the end of backward
             value = self.loss_fn(self.model, self.x)
             _mark("loss")
-            loss = backward_negated(value)   # = (-f).backward()
+            backward_negated(value, out=self.loss)   # = (-f).backward(); self.loss = -f
         _mark("backward")
         # the VAEs keep their last posterior parameters (the reference's `_qz_x_params`),
         # which would keep this step's autograd graph -- and its AccumulateGrad nodes,
@@ -153,7 +153,6 @@ class Step:
             if getattr(m, "_qz_x_params", None) is not None:
                 m._qz_x_params = None
         self.opt.pack_grads()
-        self.loss.copy_(loss.detach())
 
     def update(self):
         self.opt.apply_update()

@@ -534,6 +534,13 @@ int vaesne_step_advance(float* step, int64_t* rng_state, void* stream);
  * nodes at phase boundaries of the captured training step (VAESNE_STAMPS=1) to time
  * them without a tracer's per-dispatch cost. */
 int vaesne_stamp(uint64_t* buf, int slot, void* stream);
+/* a training batch's verdict words in one launch (training_util.training_step, the
+ * reference's loss.item() + its NaN checks, training_util.py:46 / PhotometricVAE.py:160):
+ * out[0] = value[0] * scale (scale = -w: the negated objective, weighted by the rank's
+ * batch share), out[1..2] = the guard flag int32[2] as floats (0 when flag is null).
+ * The data-parallel exchange writes them after the flat gradient (distributed.FlatExchange). */
+int vaesne_loss_stat(const float* value, float scale, const int32_t* flag, float* out,
+                     void* stream);
 /* gather (unpack=0) / scatter (unpack=1) `count` tensors to/from a flat buffer */
 int vaesne_pack(const float* const* srcs, const int64_t* offs, const int64_t* ns, int count,
                 float* dst, int unpack, void* stream);

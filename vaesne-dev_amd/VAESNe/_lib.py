@@ -112,6 +112,7 @@ SIGNATURES = {
                                 I32, P, I32, P]),
     "vaesne_step_advance": (I32, [P, P, P]),
     "vaesne_stamp": (I32, [P, I32, P]),
+    "vaesne_loss_stat": (I32, [P, F32, P, P, P]),
     "vaesne_pack": (I32, [PP, C.POINTER(I64), C.POINTER(I64), I32, P, I32, P]),
 }
 

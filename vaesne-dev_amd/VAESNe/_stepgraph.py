@@ -158,9 +158,10 @@ def _signature(network, loss_fn, xs, multimodal, params, scalars=None):
 
 
 def step(network, loss_fn, x, multimodal):
-    """The batch's loss (a device scalar) with every parameter gradient set, from a
-    replay of the captured step; None when this batch must run eagerly (warm-up,
-    an uncapturable signature)."""
+    """The batch's objective value (a device scalar: the loss is its negation, as
+    training_util.backward_negated(..., negate=False) returns it) with every parameter
+    gradient set, from a replay of the captured step; None when this batch must run
+    eagerly (warm-up, an uncapturable signature)."""
     xs = _flat(x, multimodal)
     if not all(t.is_cuda for t in xs):
         return None
@@ -211,7 +212,7 @@ def _capture(ent, network, loss_fn, x, xs, multimodal, params) -> bool:
         torch.cuda.synchronize()
         with torch.cuda.graph(g):
             with _guarded(), _defer.deferred():
-                sloss = training_util.backward_negated(loss_fn(network, sx))
+                sloss = training_util.backward_negated(loss_fn(network, sx), negate=False)
     except Exception as e:   # noqa: BLE001 -- any capture failure: this signature stays eager
         ent.failed = True
         for p in params:

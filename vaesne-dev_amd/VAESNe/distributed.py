@@ -246,9 +246,10 @@ class FlatExchange:
                                "agreed pattern of this step signature does not have")
         return mask
 
-    def run(self, loss, weight, mean, flag, mask):
+    def run(self, val, scale, mean, flag, mask):
         """Gather, all-reduce, re-bind the gradients; returns the reduced
-        [loss, post_flag, loss_flag] (a device view, no sync)."""
+        [val * scale, post_flag, loss_flag] (a device view, no sync).  The gradient is
+        multiplied by |scale| (the rank's batch share) for a mean objective."""
         n = self.n
         if self.buf.is_cuda:
             from . import _lib
@@ -266,13 +267,21 @@ class FlatExchange:
                     v.zero_()
                 elif p.grad.data_ptr() != v.data_ptr():
                     v.copy_(p.grad)
+        weight = abs(scale)
         if mean and weight != 1.0:
             self.buf[:n].mul_(weight)
-        torch.mul(loss.detach().reshape(1).float(), weight, out=self.buf[n:n + 1])
-        if flag is None:
-            self.buf[n + 1:].zero_()
+        if self.buf.is_cuda:
+            v = val.detach()
+            if v.dtype != torch.float32 or not v.is_contiguous():
+                v = v.float().contiguous()
+            _lib.lib.loss_stat(v.data_ptr(), float(scale), None if flag is None else flag.data_ptr(),
+                               self.buf.data_ptr() + 4 * n, _lib.stream())
         else:
-            self.buf[n + 1:].copy_(flag)
+            torch.mul(val.detach().reshape(1).float(), scale, out=self.buf[n:n + 1])
+            if flag is None:
+                self.buf[n + 1:].zero_()
+            else:
+                self.buf[n + 1:].copy_(flag)
         dist.all_reduce(self.buf, op=dist.ReduceOp.SUM)
         for p, v, m in zip(self.params, self.views, mask):
             p.grad = v if m else None

@@ -50,22 +50,28 @@ from .losses import elbo
 _SEEDS = {}
 
 
-def backward_negated(value):
+def backward_negated(value, out=None, negate=True):
     """`loss = -value; loss.backward()` (training_util.py:42-44) with the gradient seed
     -1 handed to `value` directly: the same gradients bit for bit (NegBackward
     multiplies the seed 1 by -1 exactly), without the fill and negation launches that
     sit between the forward and the backward of every step.  Returns -value
-    (detached), negated after the backward was issued."""
+    (detached), negated after the backward was issued -- into `out` when given (one
+    launch for the negation and the copy) -- or, with negate=False, `value` itself
+    (detached: training_step folds the sign into its verdict words, no launch)."""
     key = (value.device, value.dtype, tuple(value.shape))
     seed = _SEEDS.get(key)
     if seed is None:
         if value.is_cuda and torch.cuda.is_current_stream_capturing():
             loss = -value          # no persistent seed yet: never allocate one in a capture
             loss.backward()
-            return loss.detach()
+            if not negate:
+                return value.detach()
+            return loss.detach() if out is None else out.copy_(loss.detach())
         seed = _SEEDS[key] = torch.full(key[2], -1.0, dtype=value.dtype, device=value.device)
     value.backward(seed)
-    return -value.detach()
+    if not negate:
+        return value.detach()
+    return -value.detach() if out is None else torch.neg(value.detach(), out=out)
 
 
 def safelog10(x):
@@ -85,7 +91,22 @@ class _Verdicts:
         if self.cuda:
             self.host = [torch.empty(3, dtype=torch.float32, pin_memory=True)
                          for _ in range(slots)]
+            self.dev = torch.empty(slots, 3, dtype=torch.float32, device=device)
             self.ev = [torch.cuda.Event() for _ in range(slots)]
+
+    def words(self, val, scale, flag):
+        """[val * scale, flag words] for the next push: on the device in one launch
+        (vaesne_loss_stat, into the slot's own buffer), or on the host."""
+        if not self.cuda:
+            return torch.cat([(val.detach().float() * scale).reshape(1), torch.zeros(2)])
+        from . import _lib
+        out = self.dev[self.i % len(self.host)]
+        v = val.detach()
+        if v.dtype != torch.float32 or not v.is_contiguous():
+            v = v.float().contiguous()
+        _lib.lib.loss_stat(v.data_ptr(), float(scale), flag.data_ptr(), out.data_ptr(),
+                           _lib.stream())
+        return out
 
     def push(self, stat, batch):
         if not self.cuda:
@@ -170,27 +191,27 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
             w = (hi - lo) / B if reduction == "mean" else 1.0
             x = D.shard(x, rank, ws)
         rng.reset_call_ids()      # every batch draws under call ids 1.. (eager or replayed)
-        loss = None
+        # `val`: the objective (the loss is -val; the sign goes into the verdict words)
+        val = None
         if empty:
-            loss = torch.zeros((), dtype=torch.float32, device=device)
+            val = torch.zeros((), dtype=torch.float32, device=device)
         elif _stepgraph.eligible(device):
             # replay of the captured forward + backward of this batch signature
-            loss = _stepgraph.step(network, loss_fn, x, multimodal)
-        if loss is None:
+            val = _stepgraph.step(network, loss_fn, x, multimodal)
+        if val is None:
             # parameter-gradient sums batched into one launch at the end of backward
             with _defer.deferred():
-                loss = backward_negated(loss_fn(network, x))
+                val = backward_negated(loss_fn(network, x), negate=False)
         if ahead:
             nxt = _fetch(batches, device, multimodal, True)
         flag = guard.flag(device) if cuda else None
         if ws > 1:
             # ONE collective: gradients, loss and guard words (distributed.FlatExchange)
             key = (_stepgraph._fn_key(loss_fn), multimodal, B, reduction)
-            stat = xchg.run(loss, w, reduction == "mean", flag, xchg.agree(key))
+            stat = xchg.run(val, -w, reduction == "mean", flag, xchg.agree(key))
             skip, flat = xchg.skip_ptr(), xchg.grads_flat()
         else:
-            stat = torch.cat([(loss.detach().float() * w).reshape(1),
-                              flag.float() if cuda else torch.zeros(2)])
+            stat = verdicts.words(val, -w, flag)     # [loss * w, flags]: one launch
             skip, flat = (flag.data_ptr() if cuda else None), None
         if cuda and upd.ready():
             upd.update(skip, flat)        # applied on the device unless a batch was flagged

@@ -643,6 +643,23 @@ VAESNE_API int vaesne_step_advance(float* step, int64_t* rng_state, void* stream
   return 0;
 }
 
+// out[0] = value[0] * scale; out[1], out[2] = flag[0], flag[1] as floats (0 without a flag)
+__global__ void loss_stat_kernel(const float* __restrict__ value, float scale,
+                                 const int32_t* __restrict__ flag, float* __restrict__ out) {
+  const int t = threadIdx.x;
+  if (t == 0) out[0] = value[0] * scale;
+  else if (t < 3) out[t] = flag ? (float)flag[t - 1] : 0.f;
+}
+
+VAESNE_API int vaesne_loss_stat(const float* value, float scale, const int32_t* flag, float* out,
+                                void* stream) {
+  if (!value || !out) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(loss_stat_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, value, scale,
+                     flag, out);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
 // Pack (unpack=0: dst <- srcs) or unpack (unpack=1: srcs <- dst) up to
 // `count` tensors at a time; host passes parallel arrays.
 VAESNE_API int vaesne_pack(const float* const* srcs, const int64_t* offs, const int64_t* ns,
