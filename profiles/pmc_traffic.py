@@ -11,7 +11,7 @@ import os
 import re
 import sys
 
-KERNELS = ("attn_fwd_kernel", "attn_bwd_kv_kernel")
+KERNELS = ("attn_fwd_kernel", "attn_bwd_kv_kernel", "attn_fwd_mfma_kernel", "attn_bwd_mfma_kernel")
 
 
 def per_kernel(path, counter):
@@ -21,7 +21,7 @@ def per_kernel(path, counter):
             continue
         name = re.sub(r"^void ", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))
         name = name.split("(")[0]
-        if name.startswith(KERNELS) and "<8, 256, 2, true" in name:
+        if name.startswith(KERNELS) and ("<8, 256, 2, true" in name or "_mfma_kernel<true" in name):
             vals[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 

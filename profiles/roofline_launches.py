@@ -10,9 +10,14 @@ import json
 import sys
 
 N, H = 256, 4          # 2*K*B sequences x heads at cfg 5
+# kernel -> (instantiation, grid threads in x at the decoder launch): the packed-VALU
+# kernels run one 256-thread block per (sequence, head); the matrix-core forward one per
+# 256 queries of it (ceil(982 / 256) = 4)
 KERNELS = {
-    "attn_bwd_kv_kernel": "attn_bwd_kv_kernel<8, 256, 2, true, true>",
-    "attn_fwd_kernel": "attn_fwd_kernel<8, 256, 2, true, false>",
+    "attn_bwd_kv_kernel": ("attn_bwd_kv_kernel<8, 256, 2, true, true>", N * H * 256),
+    "attn_fwd_kernel": ("attn_fwd_kernel<8, 256, 2, true, false>", N * H * 256),
+    "attn_fwd_mfma_kernel": ("attn_fwd_mfma_kernel<true, 4, false>", N * H * 4 * 256),
+    "attn_bwd_mfma_kernel": ("attn_bwd_mfma_kernel<true, 4, 0>", N * H * 4 * 256),
 }
 
 
@@ -37,12 +42,12 @@ def replayed_step_rows(rows):
 def main(path, out):
     res = {}
     rows = replayed_step_rows(list(csv.DictReader(open(path))))
-    for key, inst in KERNELS.items():
+    for key, (inst, gx) in KERNELS.items():
         durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in rows
-                if inst in r["Kernel_Name"] and int(r["Grid_Size_X"]) == N * H * 256
+                if inst in r["Kernel_Name"] and int(r["Grid_Size_X"]) == gx
                 and int(r.get("Grid_Size_Y", 1) or 1) == 1]
         if durs:
-            res[key] = {"instance": inst, "grid": f"{N * H * 256}x1", "launches": len(durs),
+            res[key] = {"instance": inst, "grid": f"{gx}x1", "launches": len(durs),
                         "avg_ms": round(sum(durs) / len(durs), 4)}
     json.dump({"source": path, "kernels": res}, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))

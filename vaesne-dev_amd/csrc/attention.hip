@@ -2517,7 +2517,7 @@ int waves_or_off(int v) { return v == 0 ? 0 : (v == 8 ? 8 : 4); }
 bool bwd_variant_ok(int v) { return (v >= 0 && v <= 4) || v == 8 || v == 12; }
 MfmaCfg mfma_cfg_from_env() {
   MfmaCfg c;
-  c.fwd = waves_or_off(env_int("VAESNE_ATTN_MFMA_FWD", 4));
+  c.fwd = waves_or_off(env_int("VAESNE_ATTN_MFMA_FWD", 0));
   c.fwd_unpk = env_int("VAESNE_ATTN_MFMA_FWD_UNPK", 0) == 1;
   c.bwd = waves_or_off(env_int("VAESNE_ATTN_MFMA_BWD", 0));
   c.bwd_v = env_int("VAESNE_ATTN_MFMA_BWD_V", kMfmaBwdV);
