@@ -1192,11 +1192,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       km = mw.w;
     }
     {
-      float v[16], t[16], c[16], p[H][LC];
+      float v[16], t[16], c[16], p[H][LC], xr[16];
       load_row(a.O, row, h, t);
+      load_row(a.x, row, h, xr);   // in flight with O's row (one HBM round trip)
       put_fl(tO, t, lane);    // read back at the tile's end (the dW_o1 operand): LDS, not HBM
       mv(S.Wo1, S.bo1, t, v, lane);
-      load_row(a.x, row, h, t);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t[r] = xr[r];
       if (DROP && have) {
         const uint32_t kk = opaque(k0);
 #pragma unroll
@@ -1271,12 +1273,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       f16v acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = d[r];
+      // the three q | k | v gradient rows in flight together (one HBM round trip, not three)
+      float4 gq[3][4];
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+          gq[cc][g4] = *reinterpret_cast<const float4*>(a.dqkv + row * 3 * E + cc * E + 8 * g4 + 4 * h);
 #pragma unroll
       for (int cc = 0; cc < 3; ++cc) {
         float g3[16];
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          float4 t = *reinterpret_cast<const float4*>(a.dqkv + row * 3 * E + cc * E + 8 * g4 + 4 * h);
+          const float4 t = gq[cc][g4];
           g3[4 * g4] = t.x; g3[4 * g4 + 1] = t.y; g3[4 * g4 + 2] = t.z; g3[4 * g4 + 3] = t.w;
         }
 #pragma unroll
