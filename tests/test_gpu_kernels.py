@@ -650,8 +650,8 @@ def test_keep_bits_generator_matches_forward_and_bits_in_forward(geo, B, H, Lq, 
                                            (2, 4, 300, 77, 0.2, 0.1), (5, 2, 33, 40, 0.0, 0.1),
                                            (16, 4, 983, 983, 0.05, 0.1), (2, 4, 257, 1100, 0.5, 0.0),
                                            (2, 4, 500, 64, 0.0, 0.1)])
-@pytest.mark.parametrize("unpk", [0, 1])
-def test_mfma_forward_matches_valu_forward(B, H, Lq, Lk, pm, p, unpk):
+@pytest.mark.parametrize("waves", [4, 8])
+def test_mfma_forward_matches_valu_forward(B, H, Lq, Lk, pm, p, waves):
     """The matrix-core forward (attn_fwd_mfma_kernel: scores on v_mfma_f32_16x16x4_f32,
     the auto path for head_dim 8) against the packed-VALU forward (a forced geometry):
     the same keep bitmap word for word, o and lse to fp32 summation order.  Includes
@@ -669,7 +669,7 @@ def test_mfma_forward_matches_valu_forward(B, H, Lq, Lk, pm, p, unpk):
     n = lib.attn_keep_bits_size(B, H, Lq, Lk) // 4
     ws = torch.empty(max(1, lib.attn_workspace(B, H, Lq, Lk, 8, 1) // 4), device=DEV)
     out = []
-    assert lib.attn_mfma_config(4, unpk, -1, -1) == 0
+    assert lib.attn_mfma_config(waves, -1, -1) == 0
     for geo in ((0, 0), (256, 2)):
         assert lib.attn_force_geometry(*geo) == 0
         try:
@@ -684,7 +684,7 @@ def test_mfma_forward_matches_valu_forward(B, H, Lq, Lk, pm, p, unpk):
             out.append((o, lse, bits))
         finally:
             lib.attn_force_geometry(0, 0)
-            lib.attn_mfma_config(-2, -1, -1, -1)
+            lib.attn_mfma_config(-2, -1, -1)
     (o0, l0, b0), (o1, l1, b1) = out
     if p > 0:
         assert torch.equal(b0, b1)
@@ -700,8 +700,8 @@ def test_mfma_forward_matches_valu_forward(B, H, Lq, Lk, pm, p, unpk):
                                            (2, 4, 300, 77, 0.2, 0.1), (5, 2, 33, 40, 0.0, 0.1),
                                            (16, 4, 983, 983, 0.05, 0.1), (2, 4, 257, 1100, 0.5, 0.0),
                                            (2, 4, 500, 64, 0.0, 0.1), (4, 4, 130, 700, 0.1, 0.1)])
-@pytest.mark.parametrize("variant", [0, 8, 12])
-def test_mfma_backward_matches_valu_backward(B, H, Lq, Lk, pm, p, variant):
+@pytest.mark.parametrize("waves,ahead", [(4, 0), (4, 1), (8, 0)])
+def test_mfma_backward_matches_valu_backward(B, H, Lq, Lk, pm, p, waves, ahead):
     """The matrix-core backward (attn_bwd_mfma_kernel: S^T, dP^T and dQ on
     v_mfma_f32_16x16x4_f32, the auto path for head_dim 8) against the packed-VALU fused
     backward (a forced geometry) on the same forward: dQ, dK, dV to fp32 summation order
@@ -719,7 +719,7 @@ def test_mfma_backward_matches_valu_backward(B, H, Lq, Lk, pm, p, variant):
     st = rng.state(DEV)
     n = lib.attn_keep_bits_size(B, H, Lq, Lk) // 4
     nws = 1
-    assert lib.attn_mfma_config(-1, -1, 4, variant) == 0
+    assert lib.attn_mfma_config(-1, waves, ahead) == 0
     for geo in ((0, 0), (256, 2)):
         assert lib.attn_force_geometry(*geo) == 0
         nws = max(nws, lib.attn_workspace(B, H, Lq, Lk, 8, 1) // 4,
@@ -750,7 +750,7 @@ def test_mfma_backward_matches_valu_backward(B, H, Lq, Lk, pm, p, variant):
             out.append((dq, dk, dv))
         finally:
             lib.attn_force_geometry(0, 0)
-    lib.attn_mfma_config(-2, -1, -1, -1)
+    lib.attn_mfma_config(-2, -1, -1)
     for name, a, b in zip(("dq", "dk", "dv"), out[0], out[1]):
         assert torch.equal(torch.isnan(a), torch.isnan(b)), name
         fin = ~torch.isnan(b)

@@ -665,11 +665,6 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
 // and one v_permlane16_swap joins the two halves of each 32-key word.
 // max3 as one instruction: fmaxf on an MFMA result makes hipcc canonicalise it first
 // (a v_max_f32 x, x per operand)
-// one unpacked FMA c + a b
-__device__ __forceinline__ float fma1(float a, float b, float c) {
-  asm("v_fma_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
-  return c;
-}
 __device__ __forceinline__ float vmax3(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -729,8 +724,7 @@ __device__ __forceinline__ void pv_key(f2 (&o)[4][4], const f2 (&vr)[4], const f
 #undef VAESNE_PV_ROW
 typedef float f4v __attribute__((ext_vector_type(4)));
 // NWV waves per workgroup (64 queries each) share each staged key tile
-// UNPK: P V as unpacked v_fma_f32 (packed fp32 stalls beside the matrix cores' work)
-template <bool DROP, int NWV, bool UNPK = false>
+template <bool DROP, int NWV>
 __global__ __launch_bounds__(64 * NWV) void attn_fwd_mfma_kernel(AttnArgs a) {
   constexpr int FM_NT = 64 * NWV, FM_QB = 64 * NWV;
   __shared__ __attribute__((aligned(16))) float Ka[TK * 8];   // A-operand image of the K tile
@@ -875,21 +869,10 @@ __global__ __launch_bounds__(64 * NWV) void attn_fwd_mfma_kernel(AttnArgs a) {
         f2 vr[4];
         lrow2<8>(Vs + (16 * g + 4 * mt + i) * 8, vr);
         const f2 pn[4] = {p[0][i >> 1], p[1][i >> 1], p[2][i >> 1], p[3][i >> 1]};
-        if constexpr (UNPK) {
-#pragma unroll
-          for (int n = 0; n < 4; ++n) {
-            const float pk = (i & 1) ? pn[n].y : pn[n].x;
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-              o[n][jj].x = fma1(vr[jj].x, pk, o[n][jj].x);
-              o[n][jj].y = fma1(vr[jj].y, pk, o[n][jj].y);
-            }
-          }
-        } else if (i & 1) {
+        if (i & 1)
           pv_key<1>(o, vr, pn);
-        } else {
+        else
           pv_key<0>(o, vr, pn);
-        }
       }
     }
     if (DROP) {
@@ -1290,13 +1273,12 @@ __device__ __forceinline__ uint32_t keep_nib(uint32_t w, int sh) {
   // other partial products land on distinct bits, so nothing carries into 12..15)
   return (((w >> sh) & 0x1111u) * 0x1248u) >> 12 & 15u;
 }
-// V (tuning variants, VAESNE_ATTN_MFMA_BWD_V): bit 0 dV / dK updates as plain vector code
-// (the compiler may unpack them beside MFMAs) instead of op_sel asm; bit 1 interleave the
-// matrix-core products into the VALU stream (sched_group_barrier); bit 2 no prefetch of
-// the next sub-tile's S^T / dP^T
-template <bool DROP, int NWV, int V>
+// AHEAD: each sub-tile's S^T / dP^T products issued one sub-tile ahead (under the previous
+// sub-tile's VALU work) instead of at its start.  Measured variants (interleaving via
+// sched_group_barrier, unpacked dV / dK FMAs, plain vector code): profiles/r04_mfma_bwd.
+template <bool DROP, int NWV, bool AHEAD>
 __global__ __launch_bounds__(64 * NWV) void attn_bwd_mfma_kernel(AttnArgs a) {
-  constexpr bool PLAIN = V & 1, SGB = V & 2, PREF = !(V & 4), UNPK = V & 8;
+  constexpr bool PREF = AHEAD;
   constexpr int DH = 8, NTT = 64 * NWV, KB = 64 * NWV;
   constexpr int NWB = KB / 32, NWBP = NWB + 1;
   constexpr int TS = 20;                          // transpose row stride (16-byte rows)
@@ -1489,44 +1471,17 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_mfma_kernel(AttnArgs a) {
           f2 dr[4][4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) lrow2<8>(Ds_ + (16 * j + 4 * g + i) * DH, dr[i]);
-          if constexpr (UNPK) {
-            // unpacked v_fma_f32 (packed fp32 cannot issue beside the matrix cores' work:
-            // MI355X_MICROARCH.md); query i outermost, so dependent FMAs are 32 apart
-            float4 tv[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-              tv[m] = *reinterpret_cast<const float4*>(trw + m * (2 * 16 * TS) + c16 * TS + 4 * g);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int m = 0; m < 4; ++m) {
-                const float w = i == 0 ? tv[m].x : i == 1 ? tv[m].y : i == 2 ? tv[m].z : tv[m].w;
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                  dv[m][p].x = fma1(dr[i][p].x, w, dv[m][p].x);
-                  dv[m][p].y = fma1(dr[i][p].y, w, dv[m][p].y);
-                }
-              }
-          } else {
 #pragma unroll
           for (int m = 0; m < 4; ++m) {
             const float4 ap = *reinterpret_cast<const float4*>(trw + m * (2 * 16 * TS) + c16 * TS + 4 * g);
             const f2 a01 = {ap.x, ap.y}, a23 = {ap.z, ap.w};
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
-              if constexpr (PLAIN) {
-                dv[m][p] = fma2(dr[0][p], bc(a01.x), dv[m][p]);
-                dv[m][p] = fma2(dr[1][p], bc(a01.y), dv[m][p]);
-                dv[m][p] = fma2(dr[2][p], bc(a23.x), dv[m][p]);
-                dv[m][p] = fma2(dr[3][p], bc(a23.y), dv[m][p]);
-              } else {
-                dv[m][p] = fma2_lo(dr[0][p], a01, dv[m][p]);
-                dv[m][p] = fma2_hi(dr[1][p], a01, dv[m][p]);
-                dv[m][p] = fma2_lo(dr[2][p], a23, dv[m][p]);
-                dv[m][p] = fma2_hi(dr[3][p], a23, dv[m][p]);
-              }
+              dv[m][p] = fma2_lo(dr[0][p], a01, dv[m][p]);
+              dv[m][p] = fma2_hi(dr[1][p], a01, dv[m][p]);
+              dv[m][p] = fma2_lo(dr[2][p], a23, dv[m][p]);
+              dv[m][p] = fma2_hi(dr[3][p], a23, dv[m][p]);
             }
-          }
           }
         }
         // dK[key] += dS[q, key] Qs[q]
@@ -1534,25 +1489,6 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_mfma_kernel(AttnArgs a) {
           f2 qr[4][4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) lrow2<8>(Qs + (16 * j + 4 * g + i) * DH, qr[i]);
-          if constexpr (UNPK) {
-            // unpacked v_fma_f32 (packed fp32 cannot issue beside the matrix cores' work:
-            // MI355X_MICROARCH.md); query i outermost, so dependent FMAs are 32 apart
-            float4 tv[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-              tv[m] = *reinterpret_cast<const float4*>(trw + m * (2 * 16 * TS) + 16 * TS + c16 * TS + 4 * g);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int m = 0; m < 4; ++m) {
-                const float w = i == 0 ? tv[m].x : i == 1 ? tv[m].y : i == 2 ? tv[m].z : tv[m].w;
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                  dk[m][p].x = fma1(qr[i][p].x, w, dk[m][p].x);
-                  dk[m][p].y = fma1(qr[i][p].y, w, dk[m][p].y);
-                }
-              }
-          } else {
 #pragma unroll
           for (int m = 0; m < 4; ++m) {
             const float4 ds = *reinterpret_cast<const float4*>(trw + m * (2 * 16 * TS) + 16 * TS +
@@ -1560,33 +1496,16 @@ __global__ __launch_bounds__(64 * NWV) void attn_bwd_mfma_kernel(AttnArgs a) {
             const f2 s01 = {ds.x, ds.y}, s23 = {ds.z, ds.w};
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
-              if constexpr (PLAIN) {
-                dk[m][p] = fma2(qr[0][p], bc(s01.x), dk[m][p]);
-                dk[m][p] = fma2(qr[1][p], bc(s01.y), dk[m][p]);
-                dk[m][p] = fma2(qr[2][p], bc(s23.x), dk[m][p]);
-                dk[m][p] = fma2(qr[3][p], bc(s23.y), dk[m][p]);
-              } else {
-                dk[m][p] = fma2_lo(qr[0][p], s01, dk[m][p]);
-                dk[m][p] = fma2_hi(qr[1][p], s01, dk[m][p]);
-                dk[m][p] = fma2_lo(qr[2][p], s23, dk[m][p]);
-                dk[m][p] = fma2_hi(qr[3][p], s23, dk[m][p]);
-              }
+              dk[m][p] = fma2_lo(qr[0][p], s01, dk[m][p]);
+              dk[m][p] = fma2_hi(qr[1][p], s01, dk[m][p]);
+              dk[m][p] = fma2_lo(qr[2][p], s23, dk[m][p]);
+              dk[m][p] = fma2_hi(qr[3][p], s23, dk[m][p]);
             }
-          }
           }
         }
         // dQ^T rows d = 4g + r of this sub-tile -> the wave's slot (rows 8..15 are zero:
         // stored anyway, so no branch splits this block)
         *reinterpret_cast<f4v*>(Qw + (wv * TK + qq) * QWS + 4 * g) = dq0 + dq1;
-        if constexpr (SGB) {
-          // spread the 32 matrix-core products over the VALU stream (one per 8 vector
-          // instructions) so one wave keeps both pipes fed
-#pragma unroll
-          for (int i = 0; i < 32; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
-          }
-        }
       }
     }
     // dQ rows of this tile: the waves' key ranges summed (fixed order); key block kb's
@@ -2504,29 +2423,24 @@ Geo pick_geo(int64_t bh, int L) {
 }
 
 // matrix-core attention kernels (head_dim 8): forward waves per workgroup (0 = the packed-
-// VALU kernel, 4, 8), its P V unpacked; fused backward waves (0 = packed VALU, 4, 8) and
-// code-shape variant.  From VAESNE_ATTN_MFMA_FWD / _FWD_UNPK / _BWD / _BWD_V at load, or
-// vaesne_attn_mfma_config().  A forced geometry selects the packed-VALU kernels.
-struct MfmaCfg { int fwd, fwd_unpk, bwd, bwd_v; };
-constexpr int kMfmaBwdV = 0;
+// VALU kernel, 4, 8); fused backward waves (0 = packed VALU, 4, 8) and whether it issues
+// each sub-tile's products ahead.  From VAESNE_ATTN_MFMA_FWD / _BWD / _BWD_AHEAD at load,
+// or vaesne_attn_mfma_config().  A forced geometry selects the packed-VALU kernels.
+struct MfmaCfg { int fwd, bwd, bwd_ahead; };
 int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
 int waves_or_off(int v) { return v == 0 ? 0 : (v == 8 ? 8 : 4); }
-bool bwd_variant_ok(int v) { return (v >= 0 && v <= 4) || v == 8 || v == 12; }
 MfmaCfg mfma_cfg_from_env() {
   MfmaCfg c;
   c.fwd = waves_or_off(env_int("VAESNE_ATTN_MFMA_FWD", 0));
-  c.fwd_unpk = env_int("VAESNE_ATTN_MFMA_FWD_UNPK", 0) == 1;
   c.bwd = waves_or_off(env_int("VAESNE_ATTN_MFMA_BWD", 0));
-  c.bwd_v = env_int("VAESNE_ATTN_MFMA_BWD_V", kMfmaBwdV);
-  if (!bwd_variant_ok(c.bwd_v)) c.bwd_v = kMfmaBwdV;
+  c.bwd_ahead = env_int("VAESNE_ATTN_MFMA_BWD_AHEAD", 0) != 0;
   return c;
 }
 MfmaCfg g_mfma = mfma_cfg_from_env();
 int mfma_fwd_waves() { return g_mfma.fwd; }
-bool mfma_fwd_unpacked() { return g_mfma.fwd_unpk != 0; }
 
 // tuning / A/B hook: VAESNE_ATTN_FUSED_DQ=0 keeps dQ in its own kernel
 bool fused_dq_enabled() {
@@ -2538,7 +2452,6 @@ bool fused_dq_enabled() {
 }
 
 int mfma_bwd_waves() { return g_mfma.bwd; }
-int mfma_bwd_variant() { return g_mfma.bwd_v; }
 bool mfma_bwd_on(int dh) {
   return dh == 8 && mfma_bwd_waves() > 0 && g_forced.nt == 0 && fused_dq_enabled();
 }
@@ -2733,11 +2646,6 @@ int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s, bool b
         hipLaunchKernelGGL((attn_fwd_mfma_kernel<true, 8>), grid, dim3(512), 0, s, c);
       else
         hipLaunchKernelGGL((attn_fwd_mfma_kernel<false, 8>), grid, dim3(512), 0, s, c);
-    } else if (mfma_fwd_unpacked()) {
-      if (p_drop > 0.f)
-        hipLaunchKernelGGL((attn_fwd_mfma_kernel<true, 4, true>), grid, dim3(256), 0, s, c);
-      else
-        hipLaunchKernelGGL((attn_fwd_mfma_kernel<false, 4, true>), grid, dim3(256), 0, s, c);
     } else {
       if (p_drop > 0.f)
         hipLaunchKernelGGL((attn_fwd_mfma_kernel<true, 4>), grid, dim3(256), 0, s, c);
@@ -2806,25 +2714,19 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
     }
     if (fuse && mfma_bwd_on(DHV)) {
       dim3 grid((unsigned)((int64_t)a.B * a.H * nkb), (unsigned)sk.n);
+#define VAESNE_BWD_MFMA(NW, AH)                                                            \
+  if (p_drop > 0.f)                                                                          \
+    hipLaunchKernelGGL((attn_bwd_mfma_kernel<true, NW, AH>), grid, dim3(64 * NW), 0, s, c);  \
+  else                                                                                       \
+    hipLaunchKernelGGL((attn_bwd_mfma_kernel<false, NW, AH>), grid, dim3(64 * NW), 0, s, c);
       if (mfma_bwd_waves() == 8) {
-        if (p_drop > 0.f)
-          hipLaunchKernelGGL((attn_bwd_mfma_kernel<true, 8, kMfmaBwdV>), grid, dim3(512), 0, s, c);
-        else
-          hipLaunchKernelGGL((attn_bwd_mfma_kernel<false, 8, kMfmaBwdV>), grid, dim3(512), 0, s, c);
+        VAESNE_BWD_MFMA(8, false)
+      } else if (g_mfma.bwd_ahead) {
+        VAESNE_BWD_MFMA(4, true)
       } else {
-        switch (mfma_bwd_variant()) {
-#define VAESNE_BWD_V(VV)                                                                       \
-  case VV:                                                                                     \
-    if (p_drop > 0.f)                                                                          \
-      hipLaunchKernelGGL((attn_bwd_mfma_kernel<true, 4, VV>), grid, dim3(256), 0, s, c);       \
-    else                                                                                       \
-      hipLaunchKernelGGL((attn_bwd_mfma_kernel<false, 4, VV>), grid, dim3(256), 0, s, c);      \
-    break;
-          VAESNE_BWD_V(0) VAESNE_BWD_V(1) VAESNE_BWD_V(2) VAESNE_BWD_V(3)
-          VAESNE_BWD_V(4) VAESNE_BWD_V(8) VAESNE_BWD_V(12)
-#undef VAESNE_BWD_V
-        }
+        VAESNE_BWD_MFMA(4, false)
       }
+#undef VAESNE_BWD_MFMA
     } else {
     const Geo gk = pick_geo((int64_t)a.B * a.H, a.Lk);
     VAESNE_GEO_SWITCH(gk, {
@@ -3111,17 +3013,14 @@ VAESNE_API int vaesne_attn_force_geometry(int nt, int np) {
   return 0;
 }
 
-VAESNE_API int vaesne_attn_mfma_config(int fwd_waves, int fwd_unpacked, int bwd_waves,
-                                       int bwd_variant) {
+VAESNE_API int vaesne_attn_mfma_config(int fwd_waves, int bwd_waves, int bwd_ahead) {
   if (fwd_waves == -2) { g_mfma = mfma_cfg_from_env(); return 0; }
   if ((fwd_waves >= 0 && fwd_waves != 0 && fwd_waves != 4 && fwd_waves != 8) ||
-      (bwd_waves >= 0 && bwd_waves != 0 && bwd_waves != 4 && bwd_waves != 8) ||
-      (bwd_variant >= 0 && !bwd_variant_ok(bwd_variant)) || fwd_unpacked > 1)
+      (bwd_waves >= 0 && bwd_waves != 0 && bwd_waves != 4 && bwd_waves != 8) || bwd_ahead > 1)
     return (int)hipErrorInvalidValue;
   if (fwd_waves >= 0) g_mfma.fwd = fwd_waves;
-  if (fwd_unpacked >= 0) g_mfma.fwd_unpk = fwd_unpacked;
   if (bwd_waves >= 0) g_mfma.bwd = bwd_waves;
-  if (bwd_variant >= 0) g_mfma.bwd_v = bwd_variant;
+  if (bwd_ahead >= 0) g_mfma.bwd_ahead = bwd_ahead;
   return 0;
 }
 
