@@ -176,3 +176,19 @@ def test_nonfinite_batch_mid_epoch_rolls_back(opt_kind, monkeypatch):
         for k in ("flat", "m", "v", "steps"):
             assert torch.equal(fa[k], fb[k]), k
     assert np.isfinite(ref[1][0])
+
+
+def test_loss_stat_words():
+    """vaesne_loss_stat: a batch's verdict words [value * scale, flag0, flag1] in one launch
+    (training_step's stat, the data-parallel exchange's tail words)."""
+    from VAESNe import _lib
+    v = torch.tensor([3.5], device=DEV)
+    flag = torch.tensor([0, 7], dtype=torch.int32, device=DEV)
+    out = torch.full((3,), 9.0, device=DEV)
+    assert _lib.lib.loss_stat(v.data_ptr(), -0.25, flag.data_ptr(), out.data_ptr(), _lib.stream()) == 0
+    torch.cuda.synchronize()
+    assert out.tolist() == [-0.875, 0.0, 7.0]
+    out.fill_(9.0)
+    assert _lib.lib.loss_stat(v.data_ptr(), 1.0, None, out.data_ptr(), _lib.stream()) == 0
+    torch.cuda.synchronize()
+    assert out.tolist() == [3.5, 0.0, 0.0]
