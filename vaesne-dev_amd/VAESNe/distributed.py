@@ -251,8 +251,9 @@ class FlatExchange:
         [val * scale, post_flag, loss_flag] (a device view, no sync).  The gradient is
         multiplied by |scale| (the rank's batch share) for a mean objective."""
         n = self.n
+        _lib = None
         if self.buf.is_cuda:
-            from . import _lib
+            from . import _lib      # the HIP library (the host path runs without it)
             srcs = [p.grad if p.grad is not None and p.grad.is_contiguous() else None
                     for p in self.params]
             _lib.lib.pack(_lib.ptr_array(srcs), (C.c_int64 * len(srcs))(*self.offs),
@@ -270,7 +271,7 @@ class FlatExchange:
         weight = abs(scale)
         if mean and weight != 1.0:
             self.buf[:n].mul_(weight)
-        if self.buf.is_cuda:
+        if _lib is not None:
             v = val.detach()
             if v.dtype != torch.float32 or not v.is_contiguous():
                 v = v.float().contiguous()

@@ -42,7 +42,7 @@ import math
 
 import torch
 
-from . import _defer, _stepgraph, _update, guard, rng
+from . import _defer, _lib, _stepgraph, _update, guard, rng
 from . import distributed as D
 from .losses import elbo
 
@@ -99,7 +99,6 @@ class _Verdicts:
         (vaesne_loss_stat, into the slot's own buffer), or on the host."""
         if not self.cuda:
             return torch.cat([(val.detach().float() * scale).reshape(1), torch.zeros(2)])
-        from . import _lib
         out = self.dev[self.i % len(self.host)]
         v = val.detach()
         if v.dtype != torch.float32 or not v.is_contiguous():
