@@ -330,8 +330,8 @@ def roofline(device, B, in_step=None):
     fwd()
     scores = N * H * L * L
     res = {}
-    mf = os.environ.get("VAESNE_ATTN_MFMA_FWD", "0") != "0"
-    mb = os.environ.get("VAESNE_ATTN_MFMA_BWD", "0") != "0"
+    mf = os.environ.get("VAESNE_ATTN_MFMA_FWD", "0") not in ("0", "1")   # auto: VALU at this grid
+    mb = os.environ.get("VAESNE_ATTN_MFMA_BWD", "0") not in ("0", "1")
     for name, kern, fn, fl in [("fwd", "attn_fwd_mfma_kernel" if mf else "attn_fwd_kernel", fwd,
                                 4 * dh),
                                ("bwd", "attn_bwd_mfma_kernel" if mb else "attn_bwd_kv_kernel",

@@ -222,12 +222,14 @@ int vaesne_attn_rep_config(int fnt, int frc, int bnt, int bnp, int brc, int bwgs
 int vaesne_attn_force_geometry(int nt, int np);
 
 /* Test / tuning hook: the head_dim-8 matrix-core attention kernels (S = Q K^T and, in the
- * fused backward, dP and dQ on v_mfma_f32_16x16x4_f32; measured slower in the step than the
- * packed-VALU kernels, so off by default: DESIGN.md).  fwd_waves / bwd_waves: 0 = the
- * packed-VALU kernel, 4 or 8 waves per workgroup; bwd_ahead: 1 = issue each sub-tile's
- * products one sub-tile ahead.  A negative argument keeps its setting (initially
- * VAESNE_ATTN_MFMA_FWD / _BWD / _BWD_AHEAD); fwd_waves = -2 restores those load-time
- * settings.  Process-wide; not while launches are in flight. */
+ * fused backward, dP and dQ on v_mfma_f32_16x16x4_f32).  fwd_waves / bwd_waves: 0 = the
+ * packed-VALU kernel, 4 or 8 = the matrix-core kernel with that many waves per workgroup,
+ * 1 = auto (the matrix-core kernel only where the packed-VALU launch would be split --
+ * grids too small to fill the chip -- and the axis spans >= 256 rows).  Default 0: every
+ * matrix-core setting is slower in the training step;
+ * bwd_ahead: 1 = issue each sub-tile's products one sub-tile ahead.  A negative argument
+ * keeps its setting (initially VAESNE_ATTN_MFMA_FWD / _BWD / _BWD_AHEAD); fwd_waves = -2
+ * restores those load-time settings.  Process-wide; not while launches are in flight. */
 int vaesne_attn_mfma_config(int fwd_waves, int bwd_waves, int bwd_ahead);
 
 /* ---- fused decoder-block tail --------------------------------------------------

@@ -95,6 +95,19 @@ def test_mha_forward_backward_vs_oracle(B, Lq, Lk, self_attn, pm):
     assert bgot[E_:2 * E_].abs().max().item() < 1e-4 * bref.abs().max().item() + 1e-6
 
 
+@pytest.mark.parametrize("B,Lq,Lk,self_attn,pm", [(2, 983, 983, True, 0.05), (3, 982, 982, True, 0.05),
+                                                 (2, 300, 257, False, 0.9)])
+def test_mha_vs_oracle_matrix_core_auto(B, Lq, Lk, self_attn, pm):
+    """The module path with the matrix-core kernels in auto mode (vaesne_attn_mfma_config 1:
+    the split launches of small grids on the matrix cores) against the fp64 oracle."""
+    from VAESNe._lib import lib
+    assert lib.attn_mfma_config(1, 1, -1) == 0
+    try:
+        test_mha_forward_backward_vs_oracle(B, Lq, Lk, self_attn, pm)
+    finally:
+        lib.attn_mfma_config(-2, -1, -1)
+
+
 def test_fully_masked_row_gives_nan_like_reference():
     """A key padding mask with no observed key makes softmax NaN in the
     reference (-inf everywhere); the kernel propagates the same NaN."""

@@ -2422,25 +2422,30 @@ Geo pick_geo(int64_t bh, int L) {
   return best;
 }
 
-// matrix-core attention kernels (head_dim 8): forward waves per workgroup (0 = the packed-
-// VALU kernel, 4, 8); fused backward waves (0 = packed VALU, 4, 8) and whether it issues
-// each sub-tile's products ahead.  From VAESNE_ATTN_MFMA_FWD / _BWD / _BWD_AHEAD at load,
-// or vaesne_attn_mfma_config().  A forced geometry selects the packed-VALU kernels.
+// matrix-core attention kernels (head_dim 8).  Forward / fused backward: 0 = the packed-
+// VALU kernels (default), 4 or 8 = the matrix-core kernel with that many waves per
+// workgroup, 1 = auto: the matrix-core kernel (4 waves) only for grids too small to fill
+// the chip (the split launches: the encoders' 983-token context self-attention, B*H = 64),
+// where it is faster alone (fwd 0.065 vs 0.088 ms, bwd 0.10 vs 0.13 ms).  In the step every
+// matrix-core setting is slower (auto 9.09 vs 8.85 ms): its MFMAs stall the packed-VALU
+// attention kernels running beside it on the other stream (profiles/r04_ab).
+// bwd_ahead: issue each sub-tile's products one sub-tile ahead.  From VAESNE_ATTN_MFMA_FWD /
+// _BWD / _BWD_AHEAD at load, or vaesne_attn_mfma_config().  A forced geometry selects the
+// packed-VALU kernels.
 struct MfmaCfg { int fwd, bwd, bwd_ahead; };
 int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
-int waves_or_off(int v) { return v == 0 ? 0 : (v == 8 ? 8 : 4); }
+int mfma_mode(int v) { return v == 0 ? 0 : (v == 1 ? 1 : (v == 8 ? 8 : 4)); }
 MfmaCfg mfma_cfg_from_env() {
   MfmaCfg c;
-  c.fwd = waves_or_off(env_int("VAESNE_ATTN_MFMA_FWD", 0));
-  c.bwd = waves_or_off(env_int("VAESNE_ATTN_MFMA_BWD", 0));
+  c.fwd = mfma_mode(env_int("VAESNE_ATTN_MFMA_FWD", 0));
+  c.bwd = mfma_mode(env_int("VAESNE_ATTN_MFMA_BWD", 0));
   c.bwd_ahead = env_int("VAESNE_ATTN_MFMA_BWD_AHEAD", 0) != 0;
   return c;
 }
 MfmaCfg g_mfma = mfma_cfg_from_env();
-int mfma_fwd_waves() { return g_mfma.fwd; }
 
 // tuning / A/B hook: VAESNE_ATTN_FUSED_DQ=0 keeps dQ in its own kernel
 bool fused_dq_enabled() {
@@ -2451,9 +2456,23 @@ bool fused_dq_enabled() {
   return on;
 }
 
-int mfma_bwd_waves() { return g_mfma.bwd; }
-bool mfma_bwd_on(int dh) {
-  return dh == 8 && mfma_bwd_waves() > 0 && g_forced.nt == 0 && fused_dq_enabled();
+int64_t waves_of(int64_t bh, int L);
+// waves per workgroup of the matrix-core forward / fused backward for this launch (0: the
+// packed-VALU kernel); auto picks it where the packed-VALU launch would be split
+int mfma_pick(int mode, int64_t bh, int L) {
+  if (g_forced.nt != 0 || mode == 0) return 0;
+  if (mode == 1) return waves_of(bh, L) < 2048 ? 4 : 0;
+  return mode;
+}
+int mfma_fwd_for(int dh, int64_t bh, int Lq) {
+  if (dh != 8) return 0;
+  const int w = mfma_pick(g_mfma.fwd, bh, Lq);
+  return g_mfma.fwd == 1 && Lq < 256 ? 0 : w;   // auto: full 256-query blocks only
+}
+int mfma_bwd_for(int dh, int64_t bh, int Lk) {
+  if (dh != 8 || !fused_dq_enabled()) return 0;
+  const int w = mfma_pick(g_mfma.bwd, bh, Lk);
+  return g_mfma.bwd == 1 && Lk < 256 ? 0 : w;   // auto: full 256-key blocks only
 }
 
 // Split launches for grids too small to fill the chip (the encoder's 983-token
@@ -2570,8 +2589,8 @@ int64_t fwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sp) {
 }
 // key blocks of the dK/dV launch (the fused dQ's partial count)
 int kv_blocks(int64_t bh, int Lk, int dh) {
-  if (mfma_bwd_on(dh)) {
-    const int kb = 64 * mfma_bwd_waves();
+  if (const int nw = mfma_bwd_for(dh, bh, Lk)) {
+    const int kb = 64 * nw;
     return (Lk + kb - 1) / kb;
   }
   const Geo g = pick_geo(bh, Lk);
@@ -2591,9 +2610,9 @@ int64_t bwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sq, Split& sk
   sk = {1, Lq};   // dK/dV: query chunks
   if (Lq <= 2 * SQ) return 0;
   sq = pick_split(waves_of((int64_t)B * H, Lq), Lk);
-  const int64_t kv_waves = mfma_bwd_on(dh) ? (int64_t)B * H * kv_blocks((int64_t)B * H, Lk, dh) *
-                                                  mfma_bwd_waves()
-                                            : waves_of((int64_t)B * H, Lk);
+  const int mw = mfma_bwd_for(dh, (int64_t)B * H, Lk);
+  const int64_t kv_waves = mw ? (int64_t)B * H * kv_blocks((int64_t)B * H, Lk, dh) * mw
+                              : waves_of((int64_t)B * H, Lk);
   sk = pick_split(kv_waves, Lq);
   return bwd_dq_floats(B, H, Lq, Lk, dh, sq) +
          (int64_t)(sk.n > 1 ? sk.n : 0) * B * Lk * H * dh * 2;
@@ -2638,8 +2657,9 @@ int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s, bool b
   } else {
     sp = {1, a.Lk};
   }
-  if (DHV == 8 && !bits_in && mfma_fwd_waves() && g_forced.nt == 0) {
-    const int nwv = mfma_fwd_waves(), qb = 64 * nwv;
+  const int nwv = bits_in ? 0 : mfma_fwd_for(DHV, (int64_t)a.B * a.H, a.Lq);
+  if (nwv) {
+    const int qb = 64 * nwv;
     dim3 grid((unsigned)((int64_t)a.B * a.H * ((a.Lq + qb - 1) / qb)), (unsigned)sp.n);
     if (nwv == 8) {
       if (p_drop > 0.f)
@@ -2712,14 +2732,15 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
       c.dq = ws_dq; c.dq_bs = (int64_t)a.Lq * E; c.dq_ls = E;
       c.dq_ss = (int64_t)a.B * a.Lq * E;
     }
-    if (fuse && mfma_bwd_on(DHV)) {
+    const int mw = fuse ? mfma_bwd_for(DHV, (int64_t)a.B * a.H, a.Lk) : 0;
+    if (mw) {
       dim3 grid((unsigned)((int64_t)a.B * a.H * nkb), (unsigned)sk.n);
 #define VAESNE_BWD_MFMA(NW, AH)                                                            \
   if (p_drop > 0.f)                                                                          \
     hipLaunchKernelGGL((attn_bwd_mfma_kernel<true, NW, AH>), grid, dim3(64 * NW), 0, s, c);  \
   else                                                                                       \
     hipLaunchKernelGGL((attn_bwd_mfma_kernel<false, NW, AH>), grid, dim3(64 * NW), 0, s, c);
-      if (mfma_bwd_waves() == 8) {
+      if (mw == 8) {
         VAESNE_BWD_MFMA(8, false)
       } else if (g_mfma.bwd_ahead) {
         VAESNE_BWD_MFMA(4, true)
@@ -3015,8 +3036,8 @@ VAESNE_API int vaesne_attn_force_geometry(int nt, int np) {
 
 VAESNE_API int vaesne_attn_mfma_config(int fwd_waves, int bwd_waves, int bwd_ahead) {
   if (fwd_waves == -2) { g_mfma = mfma_cfg_from_env(); return 0; }
-  if ((fwd_waves >= 0 && fwd_waves != 0 && fwd_waves != 4 && fwd_waves != 8) ||
-      (bwd_waves >= 0 && bwd_waves != 0 && bwd_waves != 4 && bwd_waves != 8) || bwd_ahead > 1)
+  auto ok = [](int v) { return v < 0 || v == 0 || v == 1 || v == 4 || v == 8; };
+  if (!ok(fwd_waves) || !ok(bwd_waves) || bwd_ahead > 1)
     return (int)hipErrorInvalidValue;
   if (fwd_waves >= 0) g_mfma.fwd = fwd_waves;
   if (bwd_waves >= 0) g_mfma.bwd = bwd_waves;
