@@ -110,21 +110,49 @@ struct __attribute__((aligned(16))) Smem {
   float ctxs[LCMAX * E];
 };
 
-__device__ void stage_w(float* dst, const float* src, int rows) {
-  for (int i = threadIdx.x; i < rows * E; i += NT) dst[(i / E) * LP + (i % E)] = src[i];
+// Prologue staging: every global load of the weights in flight before the LDS stores (the
+// strided-loop form waited for each load in turn: ~40 dependent L2 round trips per
+// workgroup before the first token)
+template <int ROWS>
+__device__ __forceinline__ void load_w(const float* src, float (&r)[ROWS * E / NT]) {
+  static_assert(ROWS * E % NT == 0, "whole rounds of the workgroup");
+#pragma unroll
+  for (int j = 0; j < ROWS * E / NT; ++j) r[j] = src[threadIdx.x + j * NT];
 }
-__device__ void stage_v(float* dst, const float* src, int n) {
-  for (int i = threadIdx.x; i < n; i += NT) dst[i] = src ? src[i] : 0.f;
+template <int ROWS>
+__device__ __forceinline__ void store_w(float* dst, const float (&r)[ROWS * E / NT]) {
+#pragma unroll
+  for (int j = 0; j < ROWS * E / NT; ++j) {
+    const int i = threadIdx.x + j * NT;
+    dst[(i / E) * LP + (i % E)] = r[j];
+  }
 }
+// NV vectors of n floats (n <= NT): thread t < n stages element t of each; a null source
+// stages zeros
+template <int NV>
+__device__ __forceinline__ void stage_vecs(float* const (&dst)[NV], const float* const (&src)[NV],
+                                           int n) {
+  if (threadIdx.x < n) {
+    float r[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) r[v] = src[v] ? src[v][threadIdx.x] : 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) dst[v][threadIdx.x] = r[v];
+  }
+}
+constexpr int MW = E * E / NT;   // per-thread elements of a 32 x 32 weight
 
-__device__ void stage_all(Smem& S, const Tail& a, bool next) {
-  stage_w(S.Wo1, a.Wo1, E); stage_w(S.Wq, a.Wq, E); stage_w(S.Wo2, a.Wo2, E);
-  stage_w(S.W1, a.W1, E); stage_w(S.W2, a.W2, E);
-  if (next) { stage_w(S.Wn, a.Wn, 3 * E); stage_v(S.bn, a.bn, 3 * E); }
-  stage_v(S.bo1, a.bo1, E); stage_v(S.bq, a.bq, E); stage_v(S.bo2, a.bo2, E);
-  stage_v(S.b1, a.b1, E); stage_v(S.b2, a.b2, E);
-  stage_v(S.g1, a.g1, E); stage_v(S.be1, a.be1, E); stage_v(S.g2, a.g2, E);
-  stage_v(S.be2, a.be2, E); stage_v(S.g3, a.g3, E); stage_v(S.be3, a.be3, E);
+__device__ __forceinline__ void stage_all(Smem& S, const Tail& a, bool next) {
+  float w0[MW], w1[MW], w2[MW], w3[MW], w4[MW], wn[3 * MW];
+  load_w<E>(a.Wo1, w0); load_w<E>(a.Wq, w1); load_w<E>(a.Wo2, w2);
+  load_w<E>(a.W1, w3); load_w<E>(a.W2, w4);
+  if (next) load_w<3 * E>(a.Wn, wn);
+  stage_vecs<11>({S.bo1, S.bq, S.bo2, S.b1, S.b2, S.g1, S.be1, S.g2, S.be2, S.g3, S.be3},
+                 {a.bo1, a.bq, a.bo2, a.b1, a.b2, a.g1, a.be1, a.g2, a.be2, a.g3, a.be3}, E);
+  if (next) stage_vecs<1>({S.bn}, {a.bn}, 3 * E);
+  store_w<E>(S.Wo1, w0); store_w<E>(S.Wq, w1); store_w<E>(S.Wo2, w2);
+  store_w<E>(S.W1, w3); store_w<E>(S.W2, w4);
+  if (next) store_w<3 * E>(S.Wn, wn);
 }
 
 // The sequence's projected context k | v into S.kv: the cross in_proj rows [E, 3E)
@@ -137,9 +165,13 @@ __device__ void ctx_kv(Smem& S, const Tail& a, int seq) {
   for (int i = threadIdx.x; i < a.Lc * 2 * E; i += NT) {
     const int j = i >> 6, c = i & 63;
     const float* w = a.Wq + (int64_t)(E + c) * E;
+    float wr[E];   // the weight row's loads all in flight together (dword loads: the row may
+                   // be a view into an optimizer's flat buffer, 4-byte aligned only)
+#pragma unroll
+    for (int k = 0; k < E; ++k) wr[k] = w[k];
     float acc = a.bq[E + c];
-#pragma unroll 8
-    for (int k = 0; k < E; ++k) acc = fmaf(S.ctxs[j * E + k], w[k], acc);
+#pragma unroll
+    for (int k = 0; k < E; ++k) acc = fmaf(S.ctxs[j * E + k], wr[k], acc);
     S.kv[i] = acc;
   }
 }
@@ -689,15 +721,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 }
 
 // ============================ encoder halves ================================
-__device__ void stage_pre(Smem& S, const Tail& a) {
-  stage_w(S.Wo1, a.Wo1, E); stage_w(S.Wq, a.Wq, E);
-  stage_v(S.bo1, a.bo1, E); stage_v(S.bq, a.bq, E); stage_v(S.g1, a.g1, E); stage_v(S.be1, a.be1, E);
+__device__ __forceinline__ void stage_pre(Smem& S, const Tail& a) {
+  float w0[MW], w1[MW];
+  load_w<E>(a.Wo1, w0); load_w<E>(a.Wq, w1);
+  stage_vecs<4>({S.bo1, S.bq, S.g1, S.be1}, {a.bo1, a.bq, a.g1, a.be1}, E);
+  store_w<E>(S.Wo1, w0); store_w<E>(S.Wq, w1);
 }
-__device__ void stage_post(Smem& S, const Tail& a, bool next) {
-  stage_w(S.Wo2, a.Wo2, E); stage_w(S.W1, a.W1, E); stage_w(S.W2, a.W2, E);
-  if (next) { stage_w(S.Wn, a.Wn, 3 * E); stage_v(S.bn, a.bn, 3 * E); }
-  stage_v(S.bo2, a.bo2, E); stage_v(S.b1, a.b1, E); stage_v(S.b2, a.b2, E);
-  stage_v(S.g2, a.g2, E); stage_v(S.be2, a.be2, E); stage_v(S.g3, a.g3, E); stage_v(S.be3, a.be3, E);
+__device__ __forceinline__ void stage_post(Smem& S, const Tail& a, bool next) {
+  float w2[MW], w3[MW], w4[MW], wn[3 * MW];
+  load_w<E>(a.Wo2, w2); load_w<E>(a.W1, w3); load_w<E>(a.W2, w4);
+  if (next) load_w<3 * E>(a.Wn, wn);
+  stage_vecs<7>({S.bo2, S.b1, S.b2, S.g2, S.be2, S.g3, S.be3},
+                {a.bo2, a.b1, a.b2, a.g2, a.be2, a.g3, a.be3}, E);
+  if (next) stage_vecs<1>({S.bn}, {a.bn}, 3 * E);
+  store_w<E>(S.Wo2, w2); store_w<E>(S.W1, w3); store_w<E>(S.W2, w4);
+  if (next) store_w<3 * E>(S.Wn, wn);
 }
 
 // residual dropout of one site: v *= keep / (1 - p); keep bits recorded in m16[slot]
