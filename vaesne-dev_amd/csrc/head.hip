@@ -39,10 +39,16 @@ __device__ __forceinline__ void head_input(const float* __restrict__ x, int64_t 
 }
 
 // W row-major [HE][HE] into LDS, optionally transposed
+// (all of a thread's loads in flight before its LDS stores)
 __device__ __forceinline__ void stage_w(float* dst, const float* __restrict__ W, bool transpose) {
-  for (int k = threadIdx.x; k < HE * HE; k += HNT) {
-    const int o = k / HE, i = k - o * HE;
-    dst[transpose ? i * HE + o : k] = W[k];
+  constexpr int N = HE * HE / HNT;
+  float r[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) r[j] = W[threadIdx.x + j * HNT];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const int k = threadIdx.x + j * HNT, o = k / HE, i = k - o * HE;
+    dst[transpose ? i * HE + o : k] = r[j];
   }
 }
 typedef float f2 __attribute__((ext_vector_type(2)));

@@ -148,11 +148,25 @@ __device__ __forceinline__ void linear_body(const LinArgs& p, int kbn, int nbn) 
   const int LDW = kbn * 32 + 1;             // odd row stride: conflict-free A reads
   float* Ws = smem;                         // [nbn*32][LDW]: Ws[n][k] = W(n, k)
   float* bs = smem + nbn * 32 * LDW;        // [nbn*32]
-  for (int idx = threadIdx.x; idx < nbn * 32 * kbn * 32; idx += NT) {
-    const int n = idx / (kbn * 32), k = idx - n * (kbn * 32);
-    float w = 0.f;
-    if (n < p.N && k < p.K) w = p.w_trans ? p.W[(int64_t)k * p.N + n] : p.W[(int64_t)n * p.K + k];
-    Ws[n * LDW + k] = w;
+  // 8 loads in flight per thread before their LDS stores (the one-element loop waited on
+  // each L2 round trip in turn at the start of every launch)
+  const int wtotal = nbn * 32 * kbn * 32;
+  for (int base = 0; base < wtotal; base += 8 * NT) {
+    float w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = base + u * NT + threadIdx.x;
+      const int n = idx / (kbn * 32), k = idx - n * (kbn * 32);
+      w[u] = 0.f;
+      if (idx < wtotal && n < p.N && k < p.K)
+        w[u] = p.w_trans ? p.W[(int64_t)k * p.N + n] : p.W[(int64_t)n * p.K + k];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = base + u * NT + threadIdx.x;
+      const int n = idx / (kbn * 32), k = idx - n * (kbn * 32);
+      if (idx < wtotal) Ws[n * LDW + k] = w[u];
+    }
   }
   for (int n = threadIdx.x; n < nbn * 32; n += NT) bs[n] = (p.bias && n < p.N) ? p.bias[n] : 0.f;
   __syncthreads();
