@@ -137,17 +137,17 @@ __global__ void uniform_kernel(float* __restrict__ u, int64_t n, const int64_t* 
 }
 
 // z[k, b, j] = loc[b, j] - scale[b, j] * sign(u) * log1p(-|u|)
+// one thread per (sample k, element t): the K samples of an element are independent (a
+// per-element loop over k waited on one load per sample)
 __global__ void rsample_fwd_kernel(const float* __restrict__ loc, const float* __restrict__ scale,
                                    const float* __restrict__ u, int K, int64_t n,
                                    float* __restrict__ z) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  float l = loc[t], s = scale[t];
-  for (int k = 0; k < K; ++k) {
-    float uu = u[(int64_t)k * n + t];
-    float sg = uu > 0.f ? 1.f : (uu < 0.f ? -1.f : 0.f);
-    z[(int64_t)k * n + t] = l - s * sg * log1pf(-fabsf(uu));
-  }
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)K * n) return;
+  const int64_t t = i % n;
+  const float l = loc[t], s = scale[t], uu = u[i];
+  const float sg = uu > 0.f ? 1.f : (uu < 0.f ? -1.f : 0.f);
+  z[i] = l - s * sg * log1pf(-fabsf(uu));
 }
 
 __global__ void rsample_bwd_kernel(const float* __restrict__ dz, const float* __restrict__ u, int K,
@@ -155,12 +155,23 @@ __global__ void rsample_bwd_kernel(const float* __restrict__ dz, const float* __
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   float gl = 0.f, gs = 0.f;
-  for (int k = 0; k < K; ++k) {
-    float g = dz[(int64_t)k * n + t];
-    float uu = u[(int64_t)k * n + t];
-    float sg = uu > 0.f ? 1.f : (uu < 0.f ? -1.f : 0.f);
-    gl += g;
-    gs += g * (-sg * log1pf(-fabsf(uu)));
+  // 8 samples' loads in flight at a time; the sums keep their order over k
+  for (int k0 = 0; k0 < K; k0 += 8) {
+    float g[8], uu[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = k0 + j < K;
+      g[j] = ok ? dz[(int64_t)(k0 + j) * n + t] : 0.f;
+      uu[j] = ok ? u[(int64_t)(k0 + j) * n + t] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (k0 + j < K) {
+        const float sg = uu[j] > 0.f ? 1.f : (uu[j] < 0.f ? -1.f : 0.f);
+        gl += g[j];
+        gs += g[j] * (-sg * log1pf(-fabsf(uu[j])));
+      }
+    }
   }
   dloc[t] = gl;
   dscale[t] = gs;
@@ -502,8 +513,9 @@ VAESNE_API int vaesne_uniform(float* u, int64_t n, const int64_t* rng_state, uin
 VAESNE_API int vaesne_rsample_fwd(const float* loc, const float* scale, const float* u, int K,
                                   int64_t n, float* z, void* stream) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(rsample_fwd_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream,
-                     loc, scale, u, K, n, z);
+  if (K <= 0) return 0;
+  hipLaunchKernelGGL(rsample_fwd_kernel, dim3(blocks_for((int64_t)K * n)), dim3(NT), 0,
+                     (hipStream_t)stream, loc, scale, u, K, n, z);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
