@@ -447,7 +447,7 @@ class LaunchTimer:
                 for k, v in self.ev.items()}
 
 
-def in_step_kernel_times(step, B, reps=3):
+def in_step_kernel_times(step, B, reps=6):
     """Average duration of the spectra decoder's self-attention launches (blocks 2-4:
     N = 2*K*B sequences x 982 tokens) inside `reps` eager training steps, with the
     step's other streams running beside them.  Every rank runs it (the step's
