@@ -122,7 +122,7 @@ class Step:
         self.opt = FusedAdamW([p for p in model.parameters() if p.requires_grad],
                               lr=CFG["lr"] if lr is None else lr,
                               grad_hook=GradAllReduce("sum") if world > 1 else None)
-        self.loss = torch.zeros((), device=device)
+        self._val = torch.zeros((), device=device)   # f of the last step (loss = -f)
         self.graphs = None
         self.use_graph = use_graph
         model.train()
@@ -135,16 +135,17 @@ class Step:
         try:
             from VAESNe.training_util import backward_negated
         except ImportError:
-            def backward_negated(v, out=None):
+            def backward_negated(v, out=None, negate=True):
                 loss = -v
                 loss.backward()
-                return loss if out is None else out.copy_(loss.detach())
+                return v.detach()
         self.opt.zero_grad(set_to_none=True)
         _mark("step")
         with deferred():   # parameter-gradient sums: one batched launch at the end of backward
             value = self.loss_fn(self.model, self.x)
             _mark("loss")
-            backward_negated(value, out=self.loss)   # = (-f).backward(); self.loss = -f
+            # = (-f).backward(); the loss -f is negated when read (no launch in the step)
+            self._val = backward_negated(value, negate=False)
         _mark("backward")
         # the VAEs keep their last posterior parameters (the reference's `_qz_x_params`),
         # which would keep this step's autograd graph -- and its AccumulateGrad nodes,
@@ -153,6 +154,11 @@ class Step:
             if getattr(m, "_qz_x_params", None) is not None:
                 m._qz_x_params = None
         self.opt.pack_grads()
+
+    @property
+    def loss(self):
+        """The last step's loss -f (a device scalar)."""
+        return -self._val
 
     def update(self):
         self.opt.apply_update()

@@ -425,6 +425,19 @@ int vaesne_rsample_fwd(const float* loc, const float* scale, const float* u, int
                        float* z, void* stream);
 int vaesne_rsample_bwd(const float* dz, const float* u, int K, int64_t n, float* dloc,
                        float* dscale, void* stream);
+/* the same with the loss's own gradients of loc / scale added in (dloc_in / dscale_in
+ * nullable): dloc = dloc_in + sum_k dz, dscale = dscale_in + sum_k dz*(-sign(u)log1p(-|u|)),
+ * the autograd sums in front of the posterior head folded into the sampler's launch
+ * (the reference's autograd adds them: training_util.py:42-44 backward) */
+int vaesne_rsample_bwd_acc(const float* dz, const float* u, int K, int64_t n,
+                           const float* dloc_in, const float* dscale_in, float* dloc,
+                           float* dscale, void* stream);
+/* gradient of zcat = cat(z_0 .. z_{G-1}, dim 1) ([K, G*n], G <= 4) read by nsrc <= 4
+ * consumers (the decoders run once over every modality's latents, mmVAE.py:91-106), each
+ * z_g also read by the loss: dz_g [K, n] = sum_j dzcat_j[:, g*n:(g+1)*n] + dzl_g (dzl and
+ * its entries nullable), in one launch */
+int vaesne_cat_grad(const float* const* dzcat, int nsrc, const float* const* dzl, int G, int K,
+                    int64_t n, float* const* dz, void* stream);
 /* px scale = 1 + big*mask, repeated K times: PhotometricVAE.py:91-93 (1e8),
  * SpectraVAE.py:84-86 (1e10) */
 int vaesne_mask_scale(const uint8_t* mask, int64_t n, int K, float big, float* out,

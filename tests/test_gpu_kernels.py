@@ -305,7 +305,7 @@ def test_embedding_sincos_rsample_latent_head():
     u = O.draw_u((3, 5, 4, 4), generator=g).double()
     b_d = bott.float().to(DEV).requires_grad_(True)
     mu, sc = _ops.latent_head(b_d, 4)
-    z = _ops.RsampleFn.apply(mu, sc, u.float().to(DEV))
+    z = _ops.RsampleFn.apply(mu, sc, u.float().to(DEV), False)
     gz = torch.randn(z.shape, generator=g, dtype=torch.float64)
     (z * gz.float().to(DEV)).sum().backward()
     b_r = bott.clone().requires_grad_(True)
@@ -313,6 +313,51 @@ def test_embedding_sincos_rsample_latent_head():
     z_r = O.laplace_rsample(mu_r, sc_r, u)
     (z_r * gz).sum().backward()
     assert _rel(z, z_r) < 1e-5 and _rel(b_d.grad, b_r.grad) < 1e-5
+
+
+def test_posterior_rsample_and_latent_cat_sums_match_autograd():
+    """The loss's gradients of loc / scale added inside the sampler's backward
+    (vaesne_rsample_bwd_acc) and the latent concat's readers + loss gradients summed in one
+    launch (vaesne_cat_grad): bit-identical to autograd's own adds (two-term sums)."""
+    from VAESNe import _ops, rng
+    g = torch.Generator().manual_seed(11)
+    K, B, Lz, Dz = 8, 16, 4, 4
+    locs = [torch.randn(B, Lz, Dz, generator=g).to(DEV).requires_grad_(True) for _ in range(2)]
+    scs = [torch.rand(B, Lz, Dz, generator=g).add(0.1).to(DEV).requires_grad_(True)
+           for _ in range(2)]
+    us = [O.draw_u((K, B, Lz, Dz), generator=g).float().to(DEV) for _ in range(2)]
+    w = [torch.randn(K, 2 * B, Lz, Dz, generator=g).to(DEV) for _ in range(2)]
+    wl = [torch.randn(B, Lz, Dz, generator=g).to(DEV) for _ in range(4)]
+    wz = [torch.randn(K, B, Lz, Dz, generator=g).to(DEV) for _ in range(2)]
+
+    def run(fused):
+        for t in locs + scs:
+            t.grad = None
+        zs, ps = [], []
+        for m in range(2):
+            with rng.inject_uniform([us[m]]):
+                if fused:
+                    z, l, s = _ops.posterior_rsample(locs[m], scs[m], K)
+                else:
+                    z, l, s = _ops.laplace_rsample(locs[m], scs[m], K), locs[m], scs[m]
+            zs.append(z)
+            ps += [l, s]
+        if fused:
+            zcats, zl = _ops.latent_cat(zs, 2)
+        else:
+            zc = torch.cat(zs, dim=1)
+            zcats, zl = (zc, zc), zs
+        f = sum((zcats[d] * w[d]).sum() for d in range(2))
+        f = f + sum((zl[m] * wz[m]).sum() for m in range(2))
+        f = f + sum((ps[i] * wl[i]).sum() for i in range(4))
+        f.backward()
+        return [t.grad.clone() for t in locs + scs], torch.cat(zcats, 0).detach()
+
+    g_ref, z_ref = run(False)
+    g_new, z_new = run(True)
+    assert torch.equal(z_ref, z_new)
+    for a, b in zip(g_ref, g_new):
+        assert torch.equal(a, b)
 
 
 def test_device_uniform_range_and_moments():

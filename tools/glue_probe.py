@@ -38,7 +38,11 @@ class _Glue(torch.utils._python_dispatch.TorchDispatchMode):
             fr = [f"{os.path.relpath(f.filename, ROOT)}:{f.lineno} {f.name}"
                   for f in traceback.extract_stack()
                   if ("VAESNe" in f.filename or "bench.py" in f.filename)]
-            self.where[(name, " <- ".join(reversed(fr[-3:])))] += 1
+            node = torch._C._current_autograd_node()
+            shp = ";".join(f"{tuple(a.shape)}/{a.stride()}" for a in args
+                           if isinstance(a, torch.Tensor))[:120]
+            self.where[(name, " <- ".join(reversed(fr[-3:])) +
+                        (f" [node {node.name()}]" if node is not None else "") + f" {{{shp}}}")] += 1
         return func(*args, **(kwargs or {}))
 
 

@@ -102,8 +102,10 @@ class PhotometricVAE(ReferencePickle, VAE):
 
     def sample(self, params, K=1):
         """q(z|x) of the encoder output `params` and its K reparameterised draws."""
-        self._qz_x_params = params
-        return self._dist(self.qz_x, *params), _ops.laplace_rsample(*params, K)
+        # q(z|x) reads aliases of (loc, scale) whose gradients the sampler's backward adds
+        z, *params = _ops.posterior_rsample(*params, K)
+        self._qz_x_params = tuple(params)
+        return self._dist(self.qz_x, *params), z
 
     def encode(self, x, mean=True):
         flux, time, band, mask = x

@@ -91,6 +91,8 @@ SIGNATURES = {
     "vaesne_uniform": (I32, [P, I64, P, U32, P]),
     "vaesne_rsample_fwd": (I32, [P, P, P, I32, I64, P, P]),
     "vaesne_rsample_bwd": (I32, [P, P, I32, I64, P, P, P]),
+    "vaesne_rsample_bwd_acc": (I32, [P, P, I32, I64, P, P, P, P, P]),
+    "vaesne_cat_grad": (I32, [PP, I32, PP, I32, I32, I64, PP, P]),
     "vaesne_mask_scale": (I32, [P, I64, I32, F32, P, P]),
     "vaesne_bright_input_fwd": (I32, [P, I64, I32, P, I64, I64, P, P]),
     "vaesne_bright_input_bwd": (I32, [P, I32, I64, I32, I64, P, P]),

@@ -23,14 +23,34 @@ def _f32(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
-def _rows(t: torch.Tensor):
-    """View t [..., K] as M rows of K with a uniform row stride; copies only if
-    the leading dims cannot be collapsed.  Returns (t, M, ld)."""
+def _row_stride(t: torch.Tensor):
+    """The uniform row stride of t [..., K] read as rows of K unit-stride floats (the
+    leading dims collapse into one: each stride is the next one times its size), or None.
+    Slices of a wider last dim (a q | k | v or k | v block) qualify."""
     K = t.shape[-1]
-    if t.dim() == 2 and t.stride(-1) == 1 and t.stride(0) >= K:
-        return t, t.shape[0], t.stride(0)
-    t = t.contiguous()
-    return t, (t.numel() // K if K > 0 else 0), K
+    if t.dim() < 2 or t.stride(-1) != 1:
+        return None
+    lead = [(n, st) for n, st in zip(t.shape[:-1], t.stride()[:-1]) if n != 1]
+    if not lead:
+        return K
+    ld = expect = lead[-1][1]
+    for n, st in reversed(lead):
+        if st != expect:
+            return None
+        expect = n * st
+    return ld if ld >= K else None
+
+
+def _rows(t: torch.Tensor):
+    """t [..., K] as M rows of K with a uniform row stride (no copy when the leading
+    dims collapse, _row_stride); copies otherwise.  Returns (t, M, ld): address rows
+    through t.data_ptr() and ld only."""
+    K = t.shape[-1]
+    ld = _row_stride(t)
+    if ld is None:
+        t = t.contiguous()
+        ld = K
+    return t, (t.numel() // K if K > 0 else 0), ld
 
 
 def _ws(nbytes: int, device) -> torch.Tensor:
@@ -86,12 +106,12 @@ class LinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         xr, x2r, W, z = ctx.saved_tensors
         act, M, K, N = ctx.act, ctx.M, ctx.K, ctx.N
-        dy = dy.contiguous()
+        dy, _, lddy = _rows(dy)       # a column slice's gradient is read in place
         dx = dW = db = None
         s = stream()
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[4]:
             dx = torch.empty((M, K), dtype=torch.float32, device=dy.device)
-            lib.linear_bwd_data(dy.data_ptr(), N, ptr(z), N, act, M, N, W.data_ptr(), K,
+            lib.linear_bwd_data(dy.data_ptr(), lddy, ptr(z), N, act, M, N, W.data_ptr(), K,
                                 dx.data_ptr(), K, 0, s)
             dx = dx.view(ctx.xshape)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
@@ -99,12 +119,12 @@ class LinearFn(torch.autograd.Function):
             db = torch.empty((N,), dtype=torch.float32, device=dy.device) if ctx.has_b else None
             ws = _ws(lib.linear_bwd_weight_workspace(M, N, K), dy.device)
             dfr = _defer.target(ctx.params, (dW, db), (ws,))
-            lib.linear_bwd_weight(dy.data_ptr(), N, ptr(z), N, act, xr.data_ptr(), ctx.ldx,
+            lib.linear_bwd_weight(dy.data_ptr(), lddy, ptr(z), N, act, xr.data_ptr(), ctx.ldx,
                                   ptr(x2r), ctx.ldx2, M, N, K, dW.data_ptr(), ptr(db), 0,
                                   ws.data_ptr(), dfr, s)
         return (dx if ctx.needs_input_grad[0] else None, dW, db, None,
                 dx if ctx.needs_input_grad[4] else None,
-                dy.view(*ctx.xshape[:-1], N) if ctx.needs_input_grad[5] else None)
+                dy if ctx.needs_input_grad[5] else None)
 
 
 def linear(x, weight, bias=None, act=None, x2=None, base=None):
@@ -718,14 +738,14 @@ class EmbedFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         (idx,) = ctx.saved_tensors
-        dout = dout.contiguous()
+        dout, _, lddo = _rows(dout)
         n = idx.numel()
         dt = None
         if ctx.needs_input_grad[1]:
             dt = torch.empty((ctx.nb, ctx.E), dtype=torch.float32, device=dout.device)
             ws = _ws(lib.embed_bwd_workspace(n, ctx.E, ctx.nb), dout.device)
             dfr = _defer.target(ctx.params, (dt,), (ws,))
-            lib.embed_bwd(idx.data_ptr(), max(n, 1), n, dout.data_ptr(), ctx.E, ctx.E, ctx.nb,
+            lib.embed_bwd(idx.data_ptr(), max(n, 1), n, dout.data_ptr(), lddo, ctx.E, ctx.nb,
                           dt.data_ptr(), 0, ws.data_ptr(), dfr, stream())
         return None, dt, (dout if ctx.needs_input_grad[2] else None)
 
@@ -822,35 +842,96 @@ def latent_head(bott, latent_len):
 
 
 class RsampleFn(torch.autograd.Function):
+    """z = Laplace(loc, scale).rsample([K]); with `alias`, also aliases of loc and scale
+    for the posterior's other readers (the loss's log q(z|x)): their gradients arrive
+    here separately and the sampler's backward launch adds them (vaesne_rsample_bwd_acc)
+    instead of two autograd adds per tensor."""
+
     @staticmethod
-    def forward(ctx, loc, scale, u):
+    def forward(ctx, loc, scale, u, alias):
         _lib.require_device(loc, scale, u)
-        loc = loc.contiguous()
-        scale = scale.contiguous()
+        ctx.alias = alias
+        locc = loc.contiguous()
+        scalec = scale.contiguous()
         K = u.shape[0]
-        n = loc.numel()
+        n = locc.numel()
         z = torch.empty((K, *loc.shape), dtype=torch.float32, device=loc.device)
-        lib.rsample_fwd(loc.data_ptr(), scale.data_ptr(), u.data_ptr(), K, n, z.data_ptr(),
+        lib.rsample_fwd(locc.data_ptr(), scalec.data_ptr(), u.data_ptr(), K, n, z.data_ptr(),
                         stream())
         ctx.save_for_backward(u)
         ctx.K, ctx.n, ctx.shape = K, n, loc.shape
+        if alias:
+            return z, loc.view_as(loc), scale.view_as(scale)
         return z
 
     @staticmethod
-    def backward(ctx, dz):
+    def backward(ctx, dz, dla=None, dsa=None):
         (u,) = ctx.saved_tensors
-        dz = dz.contiguous()
-        dl = torch.empty(ctx.shape, dtype=torch.float32, device=dz.device)
+        dl = torch.empty(ctx.shape, dtype=torch.float32, device=u.device)
         ds = torch.empty_like(dl)
-        lib.rsample_bwd(dz.data_ptr(), u.data_ptr(), ctx.K, ctx.n, dl.data_ptr(), ds.data_ptr(),
-                        stream())
-        return dl, ds, None
+        if dz is None:
+            dz = torch.zeros((ctx.K, *ctx.shape), dtype=torch.float32, device=u.device)
+        dz = dz.contiguous()
+        dla = dla.contiguous() if dla is not None else None
+        dsa = dsa.contiguous() if dsa is not None else None
+        lib.rsample_bwd_acc(dz.data_ptr(), u.data_ptr(), ctx.K, ctx.n, ptr(dla), ptr(dsa),
+                            dl.data_ptr(), ds.data_ptr(), stream())
+        return dl, ds, None, None
 
 
 def laplace_rsample(loc, scale, K):
     """Laplace(loc, scale).rsample([K]) with a device (or injected) uniform draw."""
     u = rng.draw_uniform((K, *loc.shape), loc.device)
-    return RsampleFn.apply(loc, scale, u)
+    return RsampleFn.apply(loc, scale, u, False)
+
+
+def posterior_rsample(loc, scale, K):
+    """(z, loc', scale'): laplace_rsample plus aliases of loc / scale for q(z|x), whose
+    gradients the sampler's backward adds in its own launch (RsampleFn)."""
+    u = rng.draw_uniform((K, *loc.shape), loc.device)
+    if torch.is_grad_enabled() and (loc.requires_grad or scale.requires_grad):
+        return RsampleFn.apply(loc, scale, u, True)
+    return RsampleFn.apply(loc, scale, u, False), loc, scale
+
+
+class LatentCatFn(torch.autograd.Function):
+    """zcat = cat(zs, dim 1) for `readers` consumers (one alias each) plus aliases of the
+    zs themselves (the loss reads them): the backward sums every reader's gradient slice
+    and the loss's gradient per z in one launch (vaesne_cat_grad) where autograd would
+    add the readers' gradients, slice them and add the loss's (1 + len(zs) launches)."""
+
+    @staticmethod
+    def forward(ctx, readers, *zs):
+        _lib.require_device(*zs)
+        ctx.G, ctx.readers = len(zs), readers
+        ctx.shape = zs[0].shape
+        zcat = torch.cat(zs, dim=1)
+        return (*(zcat.view_as(zcat) for _ in range(readers)), *(z.view_as(z) for z in zs))
+
+    @staticmethod
+    def backward(ctx, *gs):
+        R, G = ctx.readers, ctx.G
+        dcat = [g.contiguous() for g in gs[:R] if g is not None]
+        dzl = [g.contiguous() if g is not None else None for g in gs[R:]]
+        K = ctx.shape[0]
+        n = math.prod(ctx.shape[1:])
+        dev = next(g for g in gs if g is not None).device
+        out = [torch.empty(ctx.shape, dtype=torch.float32, device=dev) for _ in range(G)]
+        if not dcat:
+            dcat = [torch.zeros((K, G * n), dtype=torch.float32, device=dev)]
+        lib.cat_grad(_lib.ptr_array(dcat), len(dcat), _lib.ptr_array(dzl), G, K, n,
+                     _lib.ptr_array(out), stream())
+        return (None, *out)
+
+
+def latent_cat(zs, readers):
+    """(zcat aliases x readers, z aliases): cat(zs, dim 1) for `readers` decoders and the
+    zs for the loss, their gradients summed by one kernel (LatentCatFn)."""
+    if not (torch.is_grad_enabled() and any(z.requires_grad for z in zs)):
+        zcat = torch.cat(zs, dim=1)
+        return (zcat,) * readers, tuple(zs)
+    out = LatentCatFn.apply(int(readers), *zs)
+    return out[:readers], out[readers:]
 
 
 def mask_scale(mask, K, big, shape_like):

@@ -142,14 +142,17 @@ class photospecMMVAE(ReferencePickle, nn.Module):
         px_zs = _CellMatrix([[None for _ in range(n)] for _ in range(n)])
         if all(z.shape == zss[0].shape for z in zss):
             B = zss[0].shape[1]
-            zcat = torch.cat(zss, dim=1)
+            # one zcat alias per decoder and the zs for the loss: their gradients meet in
+            # one kernel (_ops.latent_cat) instead of autograd's adds
+            zcats, zss = _ops.latent_cat(zss, n)
+            zss = list(zss)
             px_zs.merged = [None] * n
             with _Branches(side) as br:
-                br.to_side(zcat, *_tensors(preps))
+                br.to_side(*zcats, *_tensors(preps))
                 for d in range(n):
                     vae = self.vaes[d]
                     with br.on(d):
-                        px_zs.merged[d] = vae.decode_params(zcat, x[d], groups=n,
+                        px_zs.merged[d] = vae.decode_params(zcats[d], x[d], groups=n,
                                                             prepared=preps[d])
                         _stamps.mark(f"dec{d}")
                 br.to_main(*px_zs.merged[0])

@@ -150,8 +150,12 @@ __global__ void rsample_fwd_kernel(const float* __restrict__ loc, const float* _
   z[i] = l - s * sg * log1pf(-fabsf(uu));
 }
 
+// dloc_in / dscale_in (nullable): the gradients the loss sends to loc / scale directly,
+// added here instead of by autograd launches after this one
 __global__ void rsample_bwd_kernel(const float* __restrict__ dz, const float* __restrict__ u, int K,
-                                   int64_t n, float* __restrict__ dloc, float* __restrict__ dscale) {
+                                   int64_t n, const float* __restrict__ dloc_in,
+                                   const float* __restrict__ dscale_in, float* __restrict__ dloc,
+                                   float* __restrict__ dscale) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   float gl = 0.f, gs = 0.f;
@@ -173,8 +177,32 @@ __global__ void rsample_bwd_kernel(const float* __restrict__ dz, const float* __
       }
     }
   }
-  dloc[t] = gl;
-  dscale[t] = gs;
+  dloc[t] = dloc_in ? gl + dloc_in[t] : gl;
+  dscale[t] = dscale_in ? gs + dscale_in[t] : gs;
+}
+
+// Gradient of the latent batch concat zcat = cat(z_0 .. z_{G-1}, dim 1) [K, G*n] read by
+// nsrc consumers, each z_g also read directly (by the loss): dz_g = sum_j dzcat_j[:, g] +
+// dzl_g, the sums in autograd's order (the readers' sum first), one launch for every g
+constexpr int CAT_MAX = 4;
+struct CatGradArgs {
+  const float* src[CAT_MAX];
+  const float* extra[CAT_MAX];
+  float* out[CAT_MAX];
+  int nsrc, G, K;
+  int64_t n;
+};
+__global__ void cat_grad_kernel(CatGradArgs a) {
+  const int64_t per = (int64_t)a.K * a.n;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= per * a.G) return;
+  const int g = (int)(i / per);
+  const int64_t r = i - g * per, k = r / a.n, t = r - k * a.n;
+  const int64_t at = (k * a.G + g) * a.n + t;
+  float s = a.src[0][at];
+  for (int j = 1; j < a.nsrc; ++j) s += a.src[j][at];
+  if (a.extra[g]) s += a.extra[g][r];
+  a.out[g][r] = s;
 }
 
 __global__ void mask_scale_kernel(const uint8_t* __restrict__ mask, int64_t n, int K, float big,
@@ -520,11 +548,39 @@ VAESNE_API int vaesne_rsample_fwd(const float* loc, const float* scale, const fl
   return 0;
 }
 
-VAESNE_API int vaesne_rsample_bwd(const float* dz, const float* u, int K, int64_t n, float* dloc,
-                                  float* dscale, void* stream) {
+VAESNE_API int vaesne_rsample_bwd_acc(const float* dz, const float* u, int K, int64_t n,
+                                      const float* dloc_in, const float* dscale_in, float* dloc,
+                                      float* dscale, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(rsample_bwd_kernel, dim3(blocks_for(n)), dim3(NT), 0, (hipStream_t)stream,
-                     dz, u, K, n, dloc, dscale);
+                     dz, u, K, n, dloc_in, dscale_in, dloc, dscale);
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+VAESNE_API int vaesne_rsample_bwd(const float* dz, const float* u, int K, int64_t n, float* dloc,
+                                  float* dscale, void* stream) {
+  return vaesne_rsample_bwd_acc(dz, u, K, n, nullptr, nullptr, dloc, dscale, stream);
+}
+
+VAESNE_API int vaesne_cat_grad(const float* const* dzcat, int nsrc, const float* const* dzl, int G,
+                               int K, int64_t n, float* const* dz, void* stream) {
+  if (nsrc < 1 || nsrc > CAT_MAX || G < 1 || G > CAT_MAX || K < 0 || n < 0 || !dzcat || !dz)
+    return (int)hipErrorInvalidValue;
+  if (K == 0 || n == 0) return 0;
+  CatGradArgs a{};
+  a.nsrc = nsrc; a.G = G; a.K = K; a.n = n;
+  for (int j = 0; j < nsrc; ++j) {
+    if (!dzcat[j]) return (int)hipErrorInvalidValue;
+    a.src[j] = dzcat[j];
+  }
+  for (int g = 0; g < G; ++g) {
+    if (!dz[g]) return (int)hipErrorInvalidValue;
+    a.out[g] = dz[g];
+    a.extra[g] = dzl ? dzl[g] : nullptr;
+  }
+  hipLaunchKernelGGL(cat_grad_kernel, dim3(blocks_for((int64_t)G * K * n)), dim3(NT), 0,
+                     (hipStream_t)stream, a);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
