@@ -329,33 +329,39 @@ __device__ __forceinline__ void wgrad_body(const WgtArgs& p, int nib, float* dW,
   float cs = 0.f;
   const int64_t chunks = (p.M + 31) / 32;
   const int64_t stride = (int64_t)gridDim.x * (NT / 64);
-  // two chunks' loads in flight per trip (a wave waited one HBM round trip per 32 rows);
-  // the chunks still enter the accumulator in the one-chunk order
-  for (int64_t ch = (int64_t)blockIdx.x * (NT / 64) + wave; ch < chunks; ch += 2 * stride) {
-    float gv[2][16], zv[2][16], xv[2][16], x2v[2][16];
+  // WD chunks' loads in flight per trip (a wave waited one HBM round trip per 32 rows); the
+  // chunks still enter the accumulator in the one-chunk order, and a chunk past the end
+  // (wave-uniform test) is neither loaded nor multiplied
+  constexpr int WD = 4;
+  for (int64_t ch = (int64_t)blockIdx.x * (NT / 64) + wave; ch < chunks; ch += WD * stride) {
+    float gv[WD][16], zv[WD][16], xv[WD][16], x2v[WD][16];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < WD; ++c) {
+      if (ch + c * stride < chunks) {
 #pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) {
-        const int64_t r = min((ch + c * stride) * 32 + 2 * s2 + hh, p.M - 1);
-        gv[c][s2] = p.dy[r * p.lddy + oc];
-        if (ACT) zv[c][s2] = p.z[r * p.ldz + oc];
-        xv[c][s2] = p.x[r * p.ldx + ic];
-        if (X2) x2v[c][s2] = p.x2[r * p.ldx2 + ic];
+        for (int s2 = 0; s2 < 16; ++s2) {
+          const int64_t r = min((ch + c * stride) * 32 + 2 * s2 + hh, p.M - 1);
+          gv[c][s2] = p.dy[r * p.lddy + oc];
+          if (ACT) zv[c][s2] = p.z[r * p.ldz + oc];
+          xv[c][s2] = p.x[r * p.ldx + ic];
+          if (X2) x2v[c][s2] = p.x2[r * p.ldx2 + ic];
+        }
       }
     }
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < WD; ++c) {
+      if (ch + c * stride < chunks) {
 #pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) {
-        const bool ok = (ch + c * stride) * 32 + 2 * s2 + hh < p.M;
-        float gg = gv[c][s2], xx = xv[c][s2];
-        if (ACT) gg *= act_grad(ACT, zv[c][s2]);
-        if (X2) xx += x2v[c][s2];
-        gg = (ok && oin) ? gg : 0.f;
-        xx = (ok && iin) ? xx : 0.f;
-        cs += gg;
-        acc = mfma(gg, xx, acc);
+        for (int s2 = 0; s2 < 16; ++s2) {
+          const bool ok = (ch + c * stride) * 32 + 2 * s2 + hh < p.M;
+          float gg = gv[c][s2], xx = xv[c][s2];
+          if (ACT) gg *= act_grad(ACT, zv[c][s2]);
+          if (X2) xx += x2v[c][s2];
+          gg = (ok && oin) ? gg : 0.f;
+          xx = (ok && iin) ? xx : 0.f;
+          cs += gg;
+          acc = mfma(gg, xx, acc);
+        }
       }
     }
   }
