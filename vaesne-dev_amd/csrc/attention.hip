@@ -2811,7 +2811,10 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
 // forward fnp query pairs per lane.  VAESNE_REP="fnt,frc,bnt,bnp,brc,bwgs,fnp" overrides
 // (tuning / tests).
 struct RepCfg { int fnt, frc, bnt, bnp, brc, bwgs, fnp; };
-const RepCfg kRepDefault{0, 2, 256, 1, 16, 1536, 1};
+// bwgs 768: the block-1 backward now runs beside the encoders' backward chain (since the
+// latent gradient sums moved into their own kernels), and half the workgroups leave that
+// latency-bound chain more free slots (step A/B 8.79 vs 8.82 ms, profiles/r04_ab/rep_bwgs.txt)
+const RepCfg kRepDefault{0, 2, 256, 1, 16, 768, 1};
 RepCfg g_rep = [] {
   RepCfg c = kRepDefault;
   if (const char* e = getenv("VAESNE_REP"))
