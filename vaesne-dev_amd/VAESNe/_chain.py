@@ -248,18 +248,11 @@ class EncChainFn(torch.autograd.Function):
         lib.enc_chain_bwd(G, groups, dfr, s)
         _stamps.mark("enc_chain_bwd_end")
         grads = []
+        # the context gradients first (the context paths' backward waits for them), the k | v
+        # projection weight gradients (read only by the flush) after every item's
         for sp, B, Lk, nctx, ctxs, params, dkv, gflat, gviews, wsk, dx0, dy in work:
             nb = sp.nb
             M = B * Lk
-            rows = []
-            for blk in range(nb):       # k | v projection weight gradients, in place in gflat
-                c = ctxs[0 if sp.shared else blk]
-                o = blk * pblk + offs[6]
-                rows.append((dkv[blk].data_ptr(), 2 * E, c.data_ptr(), E,
-                             gflat.data_ptr() + 4 * (o + E * E),
-                             gflat.data_ptr() + 4 * (blk * pblk + offs[7] + E)))
-            lib.linear_bwd_weight_group(nb, _ops.wgt_groups(rows), M, 2 * E, E, wsk.data_ptr(),
-                                        dfr, s)
             if sp.shared:
                 # dctx = sum_blk dkv_blk Wkv_blk: per-block products in one launch, then one
                 # fixed-order sum over the blocks
@@ -277,6 +270,16 @@ class EncChainFn(torch.autograd.Function):
                 lib.linear_bwd_data_group(nb, _ops.lin_groups(rows), E, 2 * E, s)
             grads += [dx0] + dctxs + gviews
             _stamps.mark(f"enc_dctx{Lk}")
+        for sp, B, Lk, nctx, ctxs, params, dkv, gflat, gviews, wsk, dx0, dy in work:
+            rows = []
+            for blk in range(sp.nb):    # k | v projection weight gradients, in place in gflat
+                c = ctxs[0 if sp.shared else blk]
+                o = blk * pblk + offs[6]
+                rows.append((dkv[blk].data_ptr(), 2 * E, c.data_ptr(), E,
+                             gflat.data_ptr() + 4 * (o + E * E),
+                             gflat.data_ptr() + 4 * (blk * pblk + offs[7] + E)))
+            lib.linear_bwd_weight_group(sp.nb, _ops.wgt_groups(rows), B * Lk, 2 * E, E,
+                                        wsk.data_ptr(), dfr, s)
         out = [None]
         for i, gr in enumerate(grads):
             out.append(gr if ng[1 + i] else None)
