@@ -323,7 +323,7 @@ def roofline(device, B, in_step=None):
     def fwd():
         lib.attn_fwd(b, s3, 3 * E, b + 4 * E, s3, 3 * E, b + 8 * E, s3, 3 * E,
                      kbias.data_ptr(), L, o.data_ptr(), L * E, E, lse.data_ptr(),
-                     N, H, L, L, dh, pd, st.data_ptr(), 7, bits.data_ptr(), 0,
+                     N, H, L, L, dh, pd, st.data_ptr(), 7, bits.data_ptr(),
                      None, _lib.stream())
 
     def bwd(fn):
@@ -336,12 +336,8 @@ def roofline(device, B, in_step=None):
     fwd()
     scores = N * H * L * L
     res = {}
-    mf = os.environ.get("VAESNE_ATTN_MFMA_FWD", "0") not in ("0", "1")   # auto: VALU at this grid
-    mb = os.environ.get("VAESNE_ATTN_MFMA_BWD", "0") not in ("0", "1")
-    for name, kern, fn, fl in [("fwd", "attn_fwd_mfma_kernel" if mf else "attn_fwd_kernel", fwd,
-                                4 * dh),
-                               ("bwd", "attn_bwd_mfma_kernel" if mb else "attn_bwd_kv_kernel",
-                                bwd(lib.attn_bwd), 8 * dh)]:
+    for name, kern, fn, fl in [("fwd", "attn_fwd_kernel", fwd, 4 * dh),
+                               ("bwd", "attn_bwd_kv_kernel", bwd(lib.attn_bwd), 8 * dh)]:
         t = time_kernel(fn, 20, device)
         res[name] = dict(kernel=kern, ms=t * 1e3, tflops=scores * fl / t / 1e12,
                          flops_per_launch=scores * fl)

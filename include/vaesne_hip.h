@@ -126,8 +126,7 @@ int vaesne_reduce_partials(const float* partial, int G, int F, float* out0, floa
  * lse [B,H,Lq] (log2 domain) is saved for the backward.  dh in {8, 16}.
  * Dropout (p_drop > 0): the forward draws the keep mask from the counter RNG
  * and stores it in keep_bits (1 bit per score, vaesne_attn_keep_bits_size
- * bytes), or with bits_in = 1 reads it there (vaesne_attn_keep_bits made it);
- * the backward reads it.
+ * bytes); the backward of the same shape reads it.
  * workspace (may be null): vaesne_attn_workspace(..., bwd) bytes.  Shapes whose
  * grid cannot fill the chip (the encoder's 983-token context self-attention,
  * B*H = 64) then run as key / query chunks with a fixed-order combine. */
@@ -139,14 +138,7 @@ int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k, 
                     const float* kbias, int64_t kb_bs, float* o, int64_t o_bs, int64_t o_ls,
                     float* lse, int B, int H, int Lq, int Lk, int dh, float p_drop,
                     const int64_t* rng_state, uint32_t call_id, uint32_t* keep_bits,
-                    int bits_in, float* workspace, void* stream);
-/* The keep bitmap a query-tiled forward (Lq > 16) with this shape, rng_state and
- * call_id draws, generated ahead of it (bit-identical).  Data-independent, so it
- * can run on a side stream before the attention's inputs exist (e.g. beside the
- * latency-bound encoders); the forward then reads it with bits_in = 1 instead of
- * hashing (its dropout VALU work falls by ~85 %), and the backward as usual. */
-int vaesne_attn_keep_bits(int B, int H, int Lq, int Lk, float p_drop, const int64_t* rng_state,
-                          uint32_t call_id, uint32_t* keep_bits, void* stream);
+                    float* workspace, void* stream);
 /* Backward.  Query-tiled shapes read the forward's keep_bits; the few-query
  * path (Lq <= 16: the encoders' latent tokens, one fused key-parallel kernel)
  * re-derives the keep decisions from (rng_state, call_id), which must be the
@@ -220,17 +212,6 @@ int vaesne_attn_rep_config(int fnt, int frc, int bnt, int bnp, int brc, int bwgs
  * per workgroup in {64, 128, 256}, np in {1, 2}: 2*np rows per lane); nt = 0 restores
  * the automatic choice.  Process-wide; not for use while launches are in flight. */
 int vaesne_attn_force_geometry(int nt, int np);
-
-/* Test / tuning hook: the head_dim-8 matrix-core attention kernels (S = Q K^T and, in the
- * fused backward, dP and dQ on v_mfma_f32_16x16x4_f32).  fwd_waves / bwd_waves: 0 = the
- * packed-VALU kernel, 4 or 8 = the matrix-core kernel with that many waves per workgroup,
- * 1 = auto (the matrix-core kernel only where the packed-VALU launch would be split --
- * grids too small to fill the chip -- and the axis spans >= 256 rows).  Default 0: every
- * matrix-core setting is slower in the training step;
- * bwd_ahead: 1 = issue each sub-tile's products one sub-tile ahead.  A negative argument
- * keeps its setting (initially VAESNE_ATTN_MFMA_FWD / _BWD / _BWD_AHEAD); fwd_waves = -2
- * restores those load-time settings.  Process-wide; not while launches are in flight. */
-int vaesne_attn_mfma_config(int fwd_waves, int bwd_waves, int bwd_ahead);
 
 /* ---- fused decoder-block tail --------------------------------------------------
  * Everything of a decoder TransformerBlock after its masked self-attention core
@@ -553,9 +534,11 @@ int vaesne_stamp(uint64_t* buf, int slot, void* stream);
 /* a training batch's verdict words in one launch (training_util.training_step, the
  * reference's loss.item() + its NaN checks, training_util.py:46 / PhotometricVAE.py:160):
  * out[0] = value[0] * scale (scale = -w: the negated objective, weighted by the rank's
- * batch share), out[1..2] = the guard flag int32[2] as floats (0 when flag is null).
+ * batch share), out[1..2] = the guard flag int32[2] as floats (0 when flag is null).  A
+ * non-finite out[0] sets flag[1] = 1 and out[2] = 1 (losses built from torch ops flag
+ * nothing themselves; the update behind this launch reads the flag as its skip word).
  * The data-parallel exchange writes them after the flat gradient (distributed.FlatExchange). */
-int vaesne_loss_stat(const float* value, float scale, const int32_t* flag, float* out,
+int vaesne_loss_stat(const float* value, float scale, int32_t* flag, float* out,
                      void* stream);
 /* gather (unpack=0) / scatter (unpack=1) `count` tensors to/from a flat buffer */
 int vaesne_pack(const float* const* srcs, const int64_t* offs, const int64_t* ns, int count,

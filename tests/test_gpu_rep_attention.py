@@ -45,7 +45,7 @@ def _plain_fwd(lib, qkv, kb, N, L, p, st, cid):
     b = qkv.data_ptr()   # no workspace: one unsplit launch (a split one sums key chunks)
     rc = lib.attn_fwd(b, L * 3 * E, 3 * E, b + 4 * E, L * 3 * E, 3 * E, b + 8 * E, L * 3 * E, 3 * E,
                       None if kb is None else kb.data_ptr(), L, o.data_ptr(), L * E, E, lse.data_ptr(),
-                      N, H, L, L, 8, p, st.data_ptr(), cid, bits.data_ptr(), 0, None,
+                      N, H, L, L, 8, p, st.data_ptr(), cid, bits.data_ptr(), None,
                       _lib.stream())
     assert rc == 0
     return o, lse, bits

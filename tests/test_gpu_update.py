@@ -89,7 +89,7 @@ def test_adamw_list_against_torch_adamw(monkeypatch):
 
 
 def _script_run(device_update, monkeypatch, epochs=2, n=12, B=4, opt_kind="torch",
-                batches=None):
+                batches=None, loss=None):
     sys.path.insert(0, ROOT)
     import bench
     from VAESNe import _update, rng
@@ -107,7 +107,7 @@ def _script_run(device_update, monkeypatch, epochs=2, n=12, B=4, opt_kind="torch
         x = bench.synthetic_batch(n, 7, "cpu")
         batches = DataLoader(multimodalDataset(TensorDataset(*x[0]), TensorDataset(*x[1])),
                              batch_size=B, shuffle=False)
-    fn = lambda m, xx: m_iwae(m, xx, K=3)
+    fn = loss or (lambda m, xx: m_iwae(m, xx, K=3))
     losses, err = [], None
     try:
         for _ in range(epochs):
@@ -192,3 +192,47 @@ def test_loss_stat_words():
     assert _lib.lib.loss_stat(v.data_ptr(), 1.0, None, out.data_ptr(), _lib.stream()) == 0
     torch.cuda.synchronize()
     assert out.tolist() == [3.5, 0.0, 0.0]
+    # a non-finite value raises the loss flag word on the device (and in out[2])
+    for bad in (float("nan"), float("inf")):
+        v.fill_(bad)
+        flag.zero_()
+        assert _lib.lib.loss_stat(v.data_ptr(), 2.0, flag.data_ptr(), out.data_ptr(),
+                                  _lib.stream()) == 0
+        torch.cuda.synchronize()
+        assert flag.tolist() == [0, 1] and out[1:].tolist() == [0.0, 1.0]
+        assert not np.isfinite(out[0].item())
+    assert _lib.lib.loss_stat(v.data_ptr(), 1.0, None, out.data_ptr(), _lib.stream()) == 0
+    torch.cuda.synchronize()
+    assert out[1:].tolist() == [0.0, 1.0]
+
+
+def test_nonfinite_custom_torch_loss_rolls_back(monkeypatch):
+    """A loss_fn composed of torch ops (no HIP loss kernel flags it) turns non-finite on
+    batch 2 of 4: the verdict words flag it on the device, so the update queued behind them
+    is skipped; training_step raises, and the model and torch.optim.AdamW (moments and host
+    step counts) are bit for bit those of a run over batches 0 and 1."""
+    from VAESNe import _stepgraph, guard
+
+    def with_scale(batches, bad_at=None):
+        # a third batch entry the model never sees: the loss's multiplier (NaN at bad_at)
+        out = []
+        for i, x in enumerate(batches):
+            w = torch.full((x[0][0].shape[0], 1), float("nan") if i == bad_at else 1.0)
+            out.append([x[0], x[1], (w,)])
+        return out
+
+    from VAESNe.losses import m_iwae
+    fn = lambda m, xx: m_iwae(m, [xx[0], xx[1]], K=3) * xx[2][0].mean()
+    ref = _script_run(True, monkeypatch, epochs=1, batches=with_scale(_batches()[:2]), loss=fn)
+    _stepgraph.clear()
+    got = _script_run(True, monkeypatch, epochs=1, batches=with_scale(_batches(), bad_at=2),
+                      loss=fn)
+    _stepgraph.clear()
+    assert ref[3] is None
+    assert got[3] is not None and "non-finite" in got[3], got[3]
+    assert guard.status("cuda") == (False, False)
+    for a, b in zip(got[0], ref[0]):
+        assert torch.equal(a, b)
+    _state_equal(got[2], ref[2])
+    steps = {float(s["step"]) for s in got[2].state_dict()["state"].values()}
+    assert steps == {2.0}, steps

@@ -250,3 +250,50 @@ def test_dp_step_has_one_collective_and_one_host_read_per_batch():
         assert pr.exitcode == 0, f"rank exit code {pr.exitcode}"
     for rank, counts, nb in sorted(q.get() for _ in range(ws)):
         assert counts == {"all_reduce": nb, "tolist": nb, "item": 0}, (rank, counts)
+
+
+def _mismatch_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(ws), LOCAL_RANK=str(rank))
+    try:
+        from VAESNe.losses import elbo
+        from VAESNe.training_util import training_step
+        torch.set_num_threads(1)
+        torch.manual_seed(0)
+        model = _ToyVAE()
+        batches = [_data(4)[0] for _ in range(3)]
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+        calls = type("Calls", (), {"n": 0})()    # an object: the step signature keys it by id
+
+        def fn(m, x):
+            calls.n += 1
+            loss = elbo(m, x)
+            if calls.n == 2 and dist.get_rank() == 1:   # beyond the pattern batch 0 agreed
+                loss = loss + 0.0 * m.unused.sum()
+            return loss
+        try:
+            training_step(model, opt, batches, loss_fn=fn)
+            q.put((rank, ""))
+        except RuntimeError as e:
+            q.put((rank, str(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_gradient_pattern_mismatch_raises_on_every_rank():
+    """a rank whose gradients go beyond the cached agreed pattern does not raise
+    alone (the others would wait in the next collective): the mismatch rides the batch's
+    one all-reduce, every rank skips the update and raises the same error."""
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mismatch_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(120)
+        assert pr.exitcode == 0, f"rank exit code {pr.exitcode} (a hang ends in -15 / None)"
+    for rank, msg in sorted(q.get() for _ in range(ws)):
+        assert "agreed pattern" in msg, (rank, msg)

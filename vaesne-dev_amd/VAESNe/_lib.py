@@ -48,8 +48,7 @@ SIGNATURES = {
     "vaesne_attn_keep_bits_size": (I64, [I32, I32, I32, I32]),
     "vaesne_attn_workspace": (I64, [I32, I32, I32, I32, I32, I32]),
     "vaesne_attn_fwd": (I32, [P, I64, I64, P, I64, I64, P, I64, I64, P, I64, P, I64, I64, P, I32,
-                              I32, I32, I32, I32, F32, P, U32, P, I32, P, P]),
-    "vaesne_attn_keep_bits": (I32, [I32, I32, I32, I32, F32, P, U32, P, P]),
+                              I32, I32, I32, I32, F32, P, U32, P, P, P]),
     "vaesne_attn_bwd": _ATTN_BWD,
     "vaesne_attn_bwd_kv": _ATTN_BWD,
     "vaesne_attn_bwd_q": _ATTN_BWD,
@@ -61,7 +60,6 @@ SIGNATURES = {
     "vaesne_dec_tail_force_path": (I32, [I32]),
     "vaesne_enc_block_workspace": (I64, [I32]),
     "vaesne_attn_force_geometry": (I32, [I32, I32]),
-    "vaesne_attn_mfma_config": (I32, [I32, I32, I32]),
     "vaesne_attn_rep_workspace": (I64, [I32, I32, I32, I32, I32, F32]),
     "vaesne_attn_rep_fwd": (I32, [P, I64, I64, P, I64, P, I64, I64, P, I32, I32, I32, I32, I32, F32,
                                   P, U32, P, P]),

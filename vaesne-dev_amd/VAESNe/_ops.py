@@ -552,7 +552,7 @@ def _attn_fwd(q, qb, ql, k, kb, kl, v, vb, vl, kbias, B, H, Lq, Lk, dh, p, dev):
     ws = _attn_ws(B, H, Lq, Lk, dh, 0, dev)
     _timed("attn_fwd", B * H * Lq * Lk, lambda: lib.attn_fwd(
         q, qb, ql, k, kb, kl, v, vb, vl, ptr(kbias), Lk, o.data_ptr(), Lq * E, E,
-        lse.data_ptr(), B, H, Lq, Lk, dh, float(p), ptr(st), cid, ptr(bits), 0, ptr(ws),
+        lse.data_ptr(), B, H, Lq, Lk, dh, float(p), ptr(st), cid, ptr(bits), ptr(ws),
         stream()))
     return o, lse, bits, st, cid
 

@@ -181,11 +181,22 @@ class TorchAdamWUpdater(Updater):
             vs.append(st["exp_avg_sq"])
             ns.append(p.numel())
             sets.append(k)
-        self.hist.append(stepped)
         n = len(ps)
-        _lib.lib.adamw_list(_lib.ptr_array(ps), _lib.ptr_array(gs), _lib.ptr_array(ms),
-                            _lib.ptr_array(vs), (C.c_int64 * n)(*ns), (C.c_int32 * n)(*sets),
-                            (C.c_float * len(coefs))(*coefs), n, skip, TORCH_FMA, _lib.stream())
+        try:
+            _lib.lib.adamw_list(_lib.ptr_array(ps), _lib.ptr_array(gs), _lib.ptr_array(ms),
+                                _lib.ptr_array(vs), (C.c_int64 * n)(*ns),
+                                (C.c_int32 * n)(*sets), (C.c_float * len(coefs))(*coefs), n,
+                                skip, TORCH_FMA, _lib.stream())
+        except BaseException:
+            # a failed enqueue (a checked hipError partway): undo this update's host
+            # bookkeeping, so the step counts never run ahead of launched updates
+            for p, created in stepped:
+                st = self.opt.state[p]
+                st["step"] -= 1
+                if created:
+                    del self.opt.state[p]
+            raise
+        self.hist.append(stepped)
 
     def rollback(self, n):
         """Undo the host bookkeeping of the last n updates (the device skipped them)."""

@@ -234,16 +234,21 @@ class FlatExchange:
     def skip_ptr(self):
         return self.buf[self.n + 1:].data_ptr()
 
+    # added to the loss-flag word by a rank whose gradients go beyond the agreed pattern:
+    # the word rides in the batch's one collective, so every rank skips the update and
+    # raises together (a rank raising alone would leave the others in the next collective)
+    MISMATCH = 1 << 20
+
     def agree(self, key):
         local = tuple(p.grad is not None for p in self.params)
         mask = self.patterns.get(key)
+        self.mismatch = False
         if mask is None:
             t = torch.tensor(local, dtype=torch.int32, device=self.device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             mask = self.patterns[key] = tuple(bool(v) for v in t.tolist())
         elif any(a and not b for a, b in zip(local, mask)):
-            raise RuntimeError("VAESNe data parallel: a parameter got a gradient that the "
-                               "agreed pattern of this step signature does not have")
+            self.mismatch = True
         return mask
 
     def run(self, val, scale, mean, flag, mask):
@@ -271,6 +276,8 @@ class FlatExchange:
         weight = abs(scale)
         if mean and weight != 1.0:
             self.buf[:n].mul_(weight)
+        if getattr(self, "mismatch", False) and flag is not None:
+            flag[1:].add_(self.MISMATCH)     # sticky: every later update is skipped too
         if _lib is not None:
             v = val.detach()
             if v.dtype != torch.float32 or not v.is_contiguous():
@@ -283,6 +290,8 @@ class FlatExchange:
                 self.buf[n + 1:].zero_()
             else:
                 self.buf[n + 1:].copy_(flag)
+            if getattr(self, "mismatch", False) and flag is None:
+                self.buf[n + 2] += self.MISMATCH
         dist.all_reduce(self.buf, op=dist.ReduceOp.SUM)
         for p, v, m in zip(self.params, self.views, mask):
             p.grad = v if m else None

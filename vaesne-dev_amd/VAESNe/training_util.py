@@ -162,6 +162,12 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
                     # every rank read the same reduced verdict: leave together, so no rank
                     # tears the group down while another is still in a collective
                     torch.distributed.barrier()
+                    if loss_bad >= D.FlatExchange.MISMATCH:
+                        guard.reset(device)
+                        raise RuntimeError(
+                            "VAESNe data parallel: a parameter got a gradient that the agreed "
+                            "pattern of this step signature does not have (on some rank); the "
+                            "update was not applied")
                 guard.raise_for(device, (post_bad > 0, loss_bad > 0 or not math.isfinite(loss_v)),
                                 "training_step")
             total_loss += loss_v

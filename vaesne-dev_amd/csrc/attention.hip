@@ -402,37 +402,13 @@ __device__ __forceinline__ void stage(float* dst, const float* __restrict__ src,
   }
 }
 
-// 0/1 float masks of the 4 bits of a nibble (bit j -> component j)
-__device__ __forceinline__ float4 nibble_mask(uint32_t i) {
-  return make_float4((float)(i & 1u), (float)((i >> 1) & 1u), (float)((i >> 2) & 1u),
-                     (float)((i >> 3) & 1u));
-}
-
 // ============================== forward ====================================
 // lane owns 2*NP queries: pair p = {i + (2p) NTT, i + (2p+1) NTT}
-// BITSIN (with DROP): the keep bitmap was generated ahead by attn_keep_bits_kernel
-// (bit-identical to what this kernel's hashing path writes); the kernel reads it
-// instead of hashing: per 8 keys and query pair, the two rows' keep bytes are
-// bit-interleaved through an LDS spread table and each key pair's 4 decisions
-// become one LDS float4 mask (~40 VALU ops per 8-key x 4-query trip instead of
-// ~250 for the hash and decisions).
-template <int DH, int NTT, int NP, bool DROP, bool BITSIN = false>
+template <int DH, int NTT, int NP, bool DROP>
 __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float Ks[TK * DH];
   __shared__ __attribute__((aligned(16))) float Vs[TK * DH];
   __shared__ __attribute__((aligned(16))) float Kb[TK];
-  __shared__ uint32_t Sp[BITSIN ? 256 : 1];              // byte -> bits at even positions
-  __shared__ __attribute__((aligned(16))) float4 Mn[BITSIN ? 16 : 1];   // nibble -> masks
-  if (BITSIN) {
-    for (int i = threadIdx.x; i < 256; i += NTT) {
-      uint32_t x = (uint32_t)i;
-      x = (x | (x << 4)) & 0x0f0fu;
-      x = (x | (x << 2)) & 0x3333u;
-      x = (x | (x << 1)) & 0x5555u;
-      Sp[i] = x;
-    }
-    if (threadIdx.x < 16) Mn[threadIdx.x] = nibble_mask(threadIdx.x);
-  }
   constexpr int R = 2 * NP;
   constexpr int QB = R * NTT;
   const int nqb = (a.Lq + QB - 1) / QB;
@@ -465,7 +441,7 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
   }
   uint32_t rk[R];
   uint32_t skey = 0u;
-  if (DROP && !BITSIN) {
+  if (DROP) {
     skey = key_of(a.rng_state, a.call_id);
 #pragma unroll
     for (int u = 0; u < R; ++u) rk[u] = attn_row_key(skey, (uint32_t)((int64_t)bh * a.Lq + qc[u]));
@@ -510,14 +486,6 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
     uint32_t w[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) w[u] = 0u;
-    uint32_t wb[R][2];   // BITSIN: this tile's two keep words per row
-    if (DROP && BITSIN) {
-#pragma unroll
-      for (int t = 0; t < R; ++t) {
-        wb[t][0] = bitp[(int64_t)(kt >> 5) * a.Lq + qc[t]];
-        wb[t][1] = (kt >> 5) + 1 < a.nw ? bitp[(int64_t)((kt >> 5) + 1) * a.Lq + qc[t]] : 0u;
-      }
-    }
     for (int g0 = 0; g0 < kend; g0 += 8) {
       f2 s[NP][8];
       f2 x[NP];
@@ -544,13 +512,6 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int p = 0; p < NP; ++p)
         mu[p] = m[p];
-      uint32_t z[NP];   // BITSIN: rows (2p, 2p+1) keep bits of these 8 keys, interleaved
-      if (DROP && BITSIN) {
-        const int ws = g0 >> 5, sh = g0 & 31;
-#pragma unroll
-        for (int p = 0; p < NP; ++p)
-          z[p] = Sp[(wb[2 * p][ws] >> sh) & 0xffu] | (Sp[(wb[2 * p + 1][ws] >> sh) & 0xffu] << 1);
-      }
 #pragma unroll
       for (int u = 0; u < 8; u += 2) {
         f2 p0[NP], p1[NP];
@@ -560,14 +521,7 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
           p1[p] = ex2(s[p][u + 1] - mu[p]);
           l[p] += p0[p] + p1[p];
         }
-        if (DROP && BITSIN) {
-#pragma unroll
-          for (int p = 0; p < NP; ++p) {
-            const float4 mk = Mn[(z[p] >> (2 * u)) & 15u];
-            p0[p] *= (f2){mk.x, mk.y};
-            p1[p] *= (f2){mk.z, mk.w};
-          }
-        } else if (DROP) {
+        if (DROP) {
           const uint32_t kpm = attn_keypair_mix(skey, (uint32_t)((kt + g0 + u) >> 1));
           bool klo[R], khi[R];
 #pragma unroll
@@ -600,7 +554,7 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
           }
         }
       }
-      if (DROP && !BITSIN && (((g0 + 8) & 31) == 0 || g0 + 8 >= kend)) {
+      if (DROP && (((g0 + 8) & 31) == 0 || g0 + 8 >= kend)) {
         const int word = (kt + g0) >> 5, n = (g0 & 31) + 8;
 #pragma unroll
         for (int t = 0; t < R; ++t) {
@@ -646,286 +600,6 @@ __global__ __launch_bounds__(NTT) void attn_fwd_kernel(AttnArgs a) {
     if (i1 < a.Lq) {
       str<DH>(a.o_out + (int64_t)b * a.o_bs + (int64_t)i1 * a.o_ls + h * DH, r1);
       a.lse[(int64_t)bh * a.Lq + i1] = m[p].y + __log2f(l[p].y);
-    }
-  }
-}
-
-// ======================= forward, scores on the matrix cores ==================
-// head_dim 8.  S = Q K^T runs on v_mfma_f32_16x16x4_f32 -- bit for bit the VALU kernel's
-// fmaf chain kbias + q0 k0 + ... + q7 k7 (the accumulator starts at the key bias, the two
-// 4-deep k-steps chain) -- so the matrix cores take the score FMAs off the VALU, which
-// keeps the softmax, the dropout hash and decisions and P V (VALU issue is the binding
-// limit of the attention kernels).
-// Wave: 64 queries, four 16-query column tiles; lane l owns queries 16n + (l & 15) and,
-// of every 64-key tile, the 16 keys 16g .. 16g + 15 (g = l >> 4): the A operand's rows
-// are permuted (row 4G + I of m-tile mt = key 16G + 4mt + I) so each accumulator's four
-// registers are four consecutive keys of the lane's query.  Each lane keeps its own
-// online-softmax state (m, l, o) over its keys; the four lanes of a query combine at the
-// end.  The keep bitmap keeps its layout: a lane assembles its 16 decisions of a tile
-// and one v_permlane16_swap joins the two halves of each 32-key word.
-// max3 as one instruction: fmaxf on an MFMA result makes hipcc canonicalise it first
-// (a v_max_f32 x, x per operand)
-__device__ __forceinline__ float vmax3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-// o[n][j] += p * v[j] for the four queries n of a lane and the 8 dims of one key, the key's
-// probability the lo (H = 0) or hi (H = 1) half of pn[n]: one statement (no pads)
-#define VAESNE_PV_ROW(H, n)                                                                   \
-  "v_pk_fma_f32 %" #n "0, %16, %" #n "P, %" #n "0 " H "\n"
-template <int H>
-__device__ __forceinline__ void pv_key(f2 (&o)[4][4], const f2 (&vr)[4], const f2 (&pn)[4]) {
-  if constexpr (H == 0)
-    asm("v_pk_fma_f32 %0, %16, %20, %0 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %4, %16, %21, %4 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %8, %16, %22, %8 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %12, %16, %23, %12 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %1, %17, %20, %1 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %5, %17, %21, %5 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %9, %17, %22, %9 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %13, %17, %23, %13 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %2, %18, %20, %2 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %6, %18, %21, %6 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %10, %18, %22, %10 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %14, %18, %23, %14 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %3, %19, %20, %3 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %7, %19, %21, %7 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %11, %19, %22, %11 op_sel_hi:[1,0,1]\n"
-        "v_pk_fma_f32 %15, %19, %23, %15 op_sel_hi:[1,0,1]"
-        : "+v"(o[0][0]), "+v"(o[0][1]), "+v"(o[0][2]), "+v"(o[0][3]), "+v"(o[1][0]),
-          "+v"(o[1][1]), "+v"(o[1][2]), "+v"(o[1][3]), "+v"(o[2][0]), "+v"(o[2][1]),
-          "+v"(o[2][2]), "+v"(o[2][3]), "+v"(o[3][0]), "+v"(o[3][1]), "+v"(o[3][2]), "+v"(o[3][3])
-        : "v"(vr[0]), "v"(vr[1]), "v"(vr[2]), "v"(vr[3]), "v"(pn[0]), "v"(pn[1]), "v"(pn[2]),
-          "v"(pn[3]));
-  else
-    asm("v_pk_fma_f32 %0, %16, %20, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %4, %16, %21, %4 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %8, %16, %22, %8 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %12, %16, %23, %12 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %1, %17, %20, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %5, %17, %21, %5 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %9, %17, %22, %9 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %13, %17, %23, %13 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %2, %18, %20, %2 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %6, %18, %21, %6 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %10, %18, %22, %10 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %14, %18, %23, %14 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %3, %19, %20, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %7, %19, %21, %7 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %11, %19, %22, %11 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-        "v_pk_fma_f32 %15, %19, %23, %15 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
-        : "+v"(o[0][0]), "+v"(o[0][1]), "+v"(o[0][2]), "+v"(o[0][3]), "+v"(o[1][0]),
-          "+v"(o[1][1]), "+v"(o[1][2]), "+v"(o[1][3]), "+v"(o[2][0]), "+v"(o[2][1]),
-          "+v"(o[2][2]), "+v"(o[2][3]), "+v"(o[3][0]), "+v"(o[3][1]), "+v"(o[3][2]), "+v"(o[3][3])
-        : "v"(vr[0]), "v"(vr[1]), "v"(vr[2]), "v"(vr[3]), "v"(pn[0]), "v"(pn[1]), "v"(pn[2]),
-          "v"(pn[3]));
-}
-#undef VAESNE_PV_ROW
-typedef float f4v __attribute__((ext_vector_type(4)));
-// NWV waves per workgroup (64 queries each) share each staged key tile
-template <bool DROP, int NWV>
-__global__ __launch_bounds__(64 * NWV) void attn_fwd_mfma_kernel(AttnArgs a) {
-  constexpr int FM_NT = 64 * NWV, FM_QB = 64 * NWV;
-  __shared__ __attribute__((aligned(16))) float Ka[TK * 8];   // A-operand image of the K tile
-  __shared__ __attribute__((aligned(16))) float Vs[TK * 8];
-  __shared__ __attribute__((aligned(16))) float Kb[TK];
-  __shared__ uint32_t Kp[TK / 2];                            // the tile's key-pair hash mixes
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int col = lane & 15, g = lane >> 4;
-  const int nqb = (a.Lq + FM_QB - 1) / FM_QB;
-  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int qb = wg % nqb, bh = wg / nqb;
-  const int b = bh / a.H, h = bh - b * a.H;
-  int qrow[4];
-  float qop[4][2];            // B operands: Q[query][4c + g] * scale_log2
-  f2 o[4][4];                 // o[n][dims 2j, 2j + 1]
-  float m[4];
-  f2 l[4];                    // l[n]: two partial sums (even / odd keys), added at the end
-  uint32_t rk[4], w[4];
-  uint32_t skey = 0u;
-  if (DROP) skey = key_of(a.rng_state, a.call_id);
-  {
-    const float* qbase = a.q + (int64_t)b * a.q_bs + h * 8 + g;
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      qrow[n] = qb * FM_QB + wave * 64 + 16 * n + col;
-      const int qc = min(qrow[n], a.Lq - 1);
-      qop[n][0] = qbase[(int64_t)qc * a.q_ls] * a.scale_log2;
-      qop[n][1] = qbase[(int64_t)qc * a.q_ls + 4] * a.scale_log2;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[n][j] = bc(0.f);
-      m[n] = M_INIT;
-      l[n] = bc(0.f);
-      w[n] = 0u;
-      if (DROP) rk[n] = attn_row_key(skey, (uint32_t)((int64_t)bh * a.Lq + qc));
-    }
-  }
-  const float* kg = a.k + (int64_t)b * a.k_bs + h * 8;
-  const float* vg = a.v + (int64_t)b * a.v_bs + h * 8;
-  const float* kbg = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
-  uint32_t* bitp = DROP ? a.bits + (int64_t)bh * a.nw * a.Lq : nullptr;
-  const int kbeg = blockIdx.y * a.kchunk, klim = min(a.Lk, kbeg + a.kchunk);
-  // issue-early / write-late staging of the next tile (as attn_fwd_kernel's ASYNC path):
-  // thread t < 128 holds K float4 (row t/2, half t%2), t >= 128 the V float4 of row (t-128)/2,
-  // t < 64 the key bias of row t
-  float4 rKV = make_float4(0.f, 0.f, 0.f, 0.f);
-  float rB = -INFINITY;
-  const int st = threadIdx.x, shalf = st & 1, srow = (st & 127) >> 1;
-  auto issue = [&](int kt) {
-    if (st >= 256) return;
-    const bool ok = kt + srow < klim;
-    const int64_t kc = min(kt + srow, klim - 1);
-    const float* src = st < 128 ? kg + kc * a.k_ls : vg + kc * a.v_ls;
-    rKV = ok ? *reinterpret_cast<const float4*>(src + 4 * shalf) : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (st < TK) rB = kt + st < klim ? (kbg ? kbg[kt + st] : 0.f) : -INFINITY;
-  };
-  if (kbeg < klim) issue(kbeg);
-  for (int kt = kbeg; kt < klim; kt += TK) {
-    __syncthreads();
-    if (st < 128) {
-      // key srow, dims 4 shalf + k -> A operand (m-tile mt, k-step c = shalf) of lane
-      // rho + 16 k, rho = 4 (srow >> 4) + (srow & 3), mt = (srow >> 2) & 3
-      const int rho = 4 * (srow >> 4) + (srow & 3), mt = (srow >> 2) & 3;
-      float* dst = Ka + (mt * 64 + rho) * 2 + shalf;
-      dst[0] = rKV.x; dst[32] = rKV.y; dst[64] = rKV.z; dst[96] = rKV.w;
-    } else if (st < 256) {
-      *reinterpret_cast<float4*>(Vs + srow * 8 + 4 * shalf) = rKV;
-    }
-    if (st < TK) Kb[st] = rB;
-    if (DROP && st < TK / 2) Kp[st] = attn_keypair_mix(skey, (uint32_t)((kt >> 1) + st));
-    __syncthreads();
-    if (kt + TK < klim) issue(kt + TK);   // next tile's loads fly under this compute
-    // the next m-tile's scores are issued before this one's VALU work (their matrix-core
-    // latency hides under it)
-    auto scores = [&](int mt, f4v (&s)[4]) {
-      const f2 ka = *reinterpret_cast<const f2*>(Ka + (mt * 64 + lane) * 2);
-      const float4 kb4 = *reinterpret_cast<const float4*>(Kb + 16 * g + 4 * mt);
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        f4v acc = {kb4.x, kb4.y, kb4.z, kb4.w};
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ka.x, qop[n][0], acc, 0, 0, 0);
-        s[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(ka.y, qop[n][1], acc, 0, 0, 0);
-      }
-    };
-    f4v sn[4];
-    scores(0, sn);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      f4v s[4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) s[n] = sn[n];
-      if (mt < 3) scores(mt + 1, sn);
-      // lazy rescaling (attn_fwd_kernel): the origin moves when a score passes it by 8
-      bool move = false;
-      float x[4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        x[n] = vmax3(vmax3(m[n], s[n].x, s[n].y), s[n].z, s[n].w);
-        move |= x[n] > m[n] + 8.f;
-      }
-      if (__any(move)) {
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          const float c = ex2(m[n] - x[n]);
-          m[n] = x[n];
-          l[n] *= bc(c);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[n][j] *= c;
-        }
-      }
-      f2 p[4][2];   // p[n][pair]: keys (2 pair, 2 pair + 1) of this m-tile
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        p[n][0] = ex2((f2){s[n].x, s[n].y} - bc(m[n]));
-        p[n][1] = ex2((f2){s[n].z, s[n].w} - bc(m[n]));
-        l[n] += p[n][0] + p[n][1];
-      }
-      if (DROP) {
-        const uint2 kpm = *reinterpret_cast<const uint2*>(Kp + 8 * g + 2 * mt);
-        bool klo[4][2], khi[4][2];
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const uint32_t bits = attn_pair_bits_mixed(rk[n], j ? kpm.y : kpm.x);
-            klo[n][j] = (bits & 0xffffu) >= a.thr;
-            khi[n][j] = (bits >> 16) >= a.thr;
-          }
-        }
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            w[n] = push_bit(push_bit(w[n], __builtin_amdgcn_ballot_w64(klo[n][j])),
-                            __builtin_amdgcn_ballot_w64(khi[n][j]));
-            p[n][j] = sel2(klo[n][j], khi[n][j], p[n][j]);
-          }
-        }
-      }
-      // o[n] += p[n][key] * v[key] over the lane's four keys of this m-tile
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        f2 vr[4];
-        lrow2<8>(Vs + (16 * g + 4 * mt + i) * 8, vr);
-        const f2 pn[4] = {p[0][i >> 1], p[1][i >> 1], p[2][i >> 1], p[3][i >> 1]};
-        if (i & 1)
-          pv_key<1>(o, vr, pn);
-        else
-          pv_key<0>(o, vr, pn);
-      }
-    }
-    if (DROP) {
-      // this lane's 16 decisions (key 16g + b at bit b), the two halves of each 32-key word
-      // joined across lane rows (g, g ^ 1); the bits the VALU kernel would not write (keys
-      // past the last 8-key group it visits) cleared
-      const int kend = min(TK, klim - kt);
-      const int word = (kt >> 5) + (g >> 1);
-      const int nvalid = min(32, max(0, ((kend + 7) & ~7) - 32 * (g >> 1)));
-      const uint32_t vmask = nvalid >= 32 ? 0xffffffffu : ((1u << nvalid) - 1u);
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const uint32_t f = __builtin_bitreverse32(w[n] << 16);
-        const auto r = __builtin_amdgcn_permlane16_swap(f, f, false, false);
-        const uint32_t wd = (r[0] | (r[1] << 16)) & vmask;
-        if ((g & 1) == 0 && nvalid > 0 && qrow[n] < a.Lq) bitp[(int64_t)word * a.Lq + qrow[n]] = wd;
-        w[n] = 0u;
-      }
-    }
-  }
-  // the four lanes of a query (l, l ^ 16, l ^ 32, l ^ 48) combine their states
-  const float ik = DROP ? a.inv_keep : 1.f;
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    float M = fmaxf(m[n], __shfl_xor(m[n], 16));
-    M = fmaxf(M, __shfl_xor(M, 32));
-    const float c = ex2(m[n] - M);
-    float L = (l[n].x + l[n].y) * c;
-    L += __shfl_xor(L, 16);
-    L += __shfl_xor(L, 32);
-    float r[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float u0 = o[n][j].x * c, u1 = o[n][j].y * c;
-      u0 += __shfl_xor(u0, 16);
-      u1 += __shfl_xor(u1, 16);
-      u0 += __shfl_xor(u0, 32);
-      u1 += __shfl_xor(u1, 32);
-      r[2 * j] = u0;
-      r[2 * j + 1] = u1;
-    }
-    const int q = qrow[n];
-    if (g != 0 || q >= a.Lq) continue;
-    if (a.ml) {   // split launch: un-normalised partial o and (m, l) of this key chunk
-      str<8>(a.o_out + blockIdx.y * a.o_ss + (int64_t)b * a.o_bs + (int64_t)q * a.o_ls + h * 8, r);
-      *reinterpret_cast<float2*>(a.ml + ((int64_t)blockIdx.y * a.B * a.H + bh) * a.Lq * 2 + 2 * q) =
-          make_float2(M, L);
-    } else {
-      const float inv = ik / L;    // L == 0 (every key masked) -> NaN, as the reference
-#pragma unroll
-      for (int d = 0; d < 8; ++d) r[d] *= inv;
-      str<8>(a.o_out + (int64_t)b * a.o_bs + (int64_t)q * a.o_ls + h * 8, r);
-      a.lse[(int64_t)bh * a.Lq + q] = M + __log2f(L);
     }
   }
 }
@@ -1252,307 +926,6 @@ __global__ __launch_bounds__(NTT) void attn_bwd_kv_kernel(AttnArgs a) {
     for (int d = 0; d < DH; ++d) { r0[d] = dv[p][d].x; r1[d] = dv[p][d].y; }
     if (j0 < a.Lk) str<DH>(dvb + (int64_t)j0 * a.dv_ls, r0);
     if (j1 < a.Lk) str<DH>(dvb + (int64_t)j1 * a.dv_ls, r1);
-  }
-}
-
-// ============== dK, dV, dQ with the score products on the matrix cores ================
-// head_dim 8, fused dQ.  Wave wv of the workgroup owns the 64 keys kb*KB + 64 wv .. + 63 as
-// four 16-key m-tiles; queries stream through the staged 64-query tiles in 16-query
-// sub-tiles.  Per (m-tile, sub-tile), v_mfma_f32_16x16x4_f32 gives S^T = K Q^T (starting at
-// the key bias: bit for bit the forward's score chain) and dP^T = V dO^T, lane l holding
-// query l & 15 and keys 16m + 4r + (l >> 4), r = 0..3 (the A rows are permuted so that
-// register r of dS is the B operand of dQ's key chunk r).  P and dS on the VALU (the
-// keep bits of a lane's four keys gathered from the bitmap word by one multiply);
-// dQ^T += K^T dS^T on the matrix cores; aP and dS are transposed through LDS so that dV and
-// dK accumulate on the packed VALU with lane = key 16m + (l & 15) over queries 4 (l >> 4) + i;
-// the four lanes of a key are summed once at the end.
-// Of the ~27 VALU instructions per score pair of attn_bwd_kv_kernel (score and dP chains,
-// dQ sums) about half remain: the exponentials, the dS algebra and the dV / dK updates.
-__device__ __forceinline__ uint32_t keep_nib(uint32_t w, int sh) {
-  // bits sh, sh + 4, sh + 8, sh + 12 of w -> bits 0..3 (0x1248 moves bit 4r to 12 + r; the
-  // other partial products land on distinct bits, so nothing carries into 12..15)
-  return (((w >> sh) & 0x1111u) * 0x1248u) >> 12 & 15u;
-}
-// AHEAD: each sub-tile's S^T / dP^T products issued one sub-tile ahead (under the previous
-// sub-tile's VALU work) instead of at its start.  Measured variants (interleaving via
-// sched_group_barrier, unpacked dV / dK FMAs, plain vector code): profiles/r04_mfma_bwd.
-template <bool DROP, int NWV, bool AHEAD>
-__global__ __launch_bounds__(64 * NWV) void attn_bwd_mfma_kernel(AttnArgs a) {
-  constexpr bool PREF = AHEAD;
-  constexpr int DH = 8, NTT = 64 * NWV, KB = 64 * NWV;
-  constexpr int NWB = KB / 32, NWBP = NWB + 1;
-  constexpr int TS = 20;                          // transpose row stride (16-byte rows)
-  __shared__ __attribute__((aligned(16))) float Qs[TK * DH];
-  __shared__ __attribute__((aligned(16))) float Ds_[TK * DH];   // dO tile * 1/(1-p)
-  __shared__ float Ls[TK], Dd[TK];
-  __shared__ uint32_t Ws[TK * NWBP];
-  constexpr int QWS = 16;                         // per-wave dQ row stride (rows d 0..15)
-  __shared__ __attribute__((aligned(16))) float Qw[NWV * TK * QWS];         // per-wave dQ
-  __shared__ __attribute__((aligned(16))) float Tr[NWV * 4 * 2 * 16 * TS];  // aP / dS transposes
-  __shared__ float4 Mt[16];
-  if (DROP && threadIdx.x < 16)
-    Mt[threadIdx.x] = make_float4((float)(threadIdx.x & 1), (float)((threadIdx.x >> 1) & 1),
-                                  (float)((threadIdx.x >> 2) & 1), (float)((threadIdx.x >> 3) & 1));
-  const int nkb = (a.Lk + KB - 1) / KB;
-  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int kb = wg % nkb, bh = wg / nkb;
-  const int b = bh / a.H, h = bh - b * a.H;
-  const int t = threadIdx.x, wv = t >> 6, l = t & 63, c16 = l & 15, g = l >> 4;
-  const int kw0 = kb * KB + 64 * wv;
-  // constant operands: S / dP A rows (row c16 of m-tile m = key 4 (c16 & 3) + (c16 >> 2)),
-  // dQ's A = K^T (row d = c16 < 8, key chunk cc: key 4 cc + g), the key biases of the
-  // accumulator rows (register r = key 4r + g; -inf past Lk)
-  float kA[4][2], vA[4][2], kT[4][4];
-  f4v kb4[4];
-  f2 dv[4][4], dk[4][4];
-  {
-    const float* kbase = a.k + (int64_t)b * a.k_bs + h * DH;
-    const float* vbase = a.v + (int64_t)b * a.v_bs + h * DH;
-    const float* kbp = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int64_t ja = min(kw0 + 16 * m + 4 * (c16 & 3) + (c16 >> 2), a.Lk - 1);
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        kA[m][c] = kbase[ja * a.k_ls + 4 * c + g];
-        vA[m][c] = vbase[ja * a.v_ls + 4 * c + g];
-      }
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc) {
-        const int64_t jt = min(kw0 + 16 * m + 4 * cc + g, a.Lk - 1);
-        kT[m][cc] = c16 < DH ? kbase[jt * a.k_ls + c16] : 0.f;
-      }
-      float bb[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = kw0 + 16 * m + 4 * r + g;
-        bb[r] = j < a.Lk ? (kbp ? kbp[j] : 0.f) : -INFINITY;
-      }
-      kb4[m] = (f4v){bb[0], bb[1], bb[2], bb[3]};
-#pragma unroll
-      for (int p = 0; p < 4; ++p) { dv[m][p] = bc(0.f); dk[m][p] = bc(0.f); }
-    }
-  }
-  const float* qg = a.q + (int64_t)b * a.q_bs + h * DH;
-  const float* dg = a.dout + (int64_t)b * a.do_bs + h * DH;
-  const float* og = a.o + (int64_t)b * a.o_bs + h * DH;
-  const float* lg = a.lse + (int64_t)bh * a.Lq;
-  const uint32_t* bitp = DROP ? a.bits + (int64_t)bh * a.nw * a.Lq : nullptr;
-  const int wfirst = (kb * KB) >> 5;
-  const int qbeg = blockIdx.y * a.qchunk, qlim = min(a.Lq, qbeg + a.qchunk);
-  // issue-early / write-late staging (attn_bwd_kv_kernel's ASYNC path): t < 128 dO and O
-  // float4 (row t/2, half t%2), 128 <= t < 256 the Q float4 of row (t-128)/2, t < 64 the
-  // lse of row t, every thread NWS keep words
-  constexpr int NWS = DROP ? (TK * NWB) / NTT : 1;
-  static_assert((TK * NWB) % NTT == 0, "keep words per thread");
-  float4 rA = make_float4(0.f, 0.f, 0.f, 0.f), rO = rA;
-  float rL = INFINITY;
-  uint32_t rW[NWS];
-  auto issue = [&](int qt) {
-    const int half = t & 1, row = (t & 127) >> 1, qi = qt + row;
-    const bool ok = qi < qlim;
-    const int64_t qc = min(qi, qlim - 1);
-    if (t < 128) {
-      rA = ok ? *reinterpret_cast<const float4*>(dg + qc * a.do_ls + 4 * half) : make_float4(0.f, 0.f, 0.f, 0.f);
-      rO = ok ? *reinterpret_cast<const float4*>(og + qc * a.o_ls + 4 * half) : make_float4(0.f, 0.f, 0.f, 0.f);
-    } else if (t < 256) {
-      rA = ok ? *reinterpret_cast<const float4*>(qg + qc * a.q_ls + 4 * half) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if (t < TK) rL = qt + t < qlim ? lg[qt + t] : INFINITY;
-    if (DROP) {
-#pragma unroll
-      for (int j = 0; j < NWS; ++j) {
-        const int idx = j * NTT + t, i = idx % TK, w = idx / TK;
-        const int word = wfirst + w;
-        rW[j] = (qt + i < qlim && word < a.nw) ? bitp[(int64_t)word * a.Lq + qt + i] : 0u;
-      }
-    }
-  };
-  auto commit = [&]() {
-    const int half = t & 1, row = (t & 127) >> 1;
-    if (t < 128) {
-      // D = rowsum(dO * O) in the fmaf order over d = 0..7 (attn_bwd_kv_kernel)
-      float pd = fmaf(rA.x, rO.x, 0.f);
-      pd = fmaf(rA.y, rO.y, pd);
-      pd = fmaf(rA.z, rO.z, pd);
-      pd = fmaf(rA.w, rO.w, pd);
-      const float p0 = __shfl_xor(pd, 1);
-      if (half) {
-        float Di = fmaf(rA.x, rO.x, p0);
-        Di = fmaf(rA.y, rO.y, Di);
-        Di = fmaf(rA.z, rO.z, Di);
-        Di = fmaf(rA.w, rO.w, Di);
-        Dd[row] = Di;
-      }
-      const float m = a.inv_keep;
-      *reinterpret_cast<float4*>(Ds_ + row * DH + 4 * half) =
-          make_float4(rA.x * m, rA.y * m, rA.z * m, rA.w * m);
-    } else if (t < 256) {
-      const float m = a.scale_log2;
-      *reinterpret_cast<float4*>(Qs + row * DH + 4 * half) =
-          make_float4(rA.x * m, rA.y * m, rA.z * m, rA.w * m);
-    }
-    if (t < TK) Ls[t] = rL;      // +inf for padding rows -> p = 0
-    if (DROP) {
-#pragma unroll
-      for (int j = 0; j < NWS; ++j) {
-        const int idx = j * NTT + t, i = idx % TK, w = idx / TK;
-        Ws[i * NWBP + w] = rW[j];
-      }
-    }
-  };
-  float* trw = Tr + wv * (4 * 2 * 16 * TS);
-  if (qbeg < qlim) issue(qbeg);
-  for (int qt = qbeg; qt < qlim; qt += TK) {
-    __syncthreads();
-    commit();
-    __syncthreads();
-    if (qt + TK < qlim) issue(qt + TK);   // next tile's loads fly under this compute
-    const int qend = min(TK, qlim - qt);
-    // S^T / dP^T of sub-tile j (the matrix-core half of its work); each sub-tile's products
-    // are issued one sub-tile ahead, so the matrix cores run them under the previous
-    // sub-tile's VALU work (dS algebra, dV / dK updates) instead of in front of it
-    auto scores = [&](int j, f4v (&S)[4], f4v (&G)[4]) {
-      const int qq = 16 * j + c16;
-      const float qB0 = Qs[qq * DH + g], qB1 = Qs[qq * DH + 4 + g];
-      const float dB0 = Ds_[qq * DH + g], dB1 = Ds_[qq * DH + 4 + g];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        S[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(kA[m][0], qB0, kb4[m], 0, 0, 0);
-        S[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(kA[m][1], qB1, S[m], 0, 0, 0);
-        G[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(vA[m][0], dB0, (f4v){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        G[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(vA[m][1], dB1, G[m], 0, 0, 0);
-      }
-    };
-    f4v S[4], G[4];
-    if (PREF) scores(0, S, G);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (16 * j < qend) {
-        if (!PREF) scores(j, S, G);
-        const int qq = 16 * j + c16;
-        const f2 li = bc(Ls[qq]), Di = bc(Dd[qq]);
-        uint32_t wd0 = 0u, wd1 = 0u;
-        if (DROP) { wd0 = Ws[qq * NWBP + 2 * wv]; wd1 = Ws[qq * NWBP + 2 * wv + 1]; }
-        f4v dq0 = {0.f, 0.f, 0.f, 0.f}, dq1 = dq0;
-        // (the transposes through Tr need no barrier: LDS runs a wave's accesses in order,
-        // and the compiler cannot reorder these writes and reads, whose addresses may alias)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const f2 p0 = ex2((f2){S[m].x, S[m].y} - li), p1 = ex2((f2){S[m].z, S[m].w} - li);
-          const f2 g0 = {G[m].x, G[m].y}, g1 = {G[m].z, G[m].w};
-          f2 aP0 = p0, aP1 = p1, d0, d1;
-          if (DROP) {
-            // dS = pr * (keep * g - Di) = aP * g - pr * Di (attn_bwd_kv_kernel's order)
-            const float4 km = Mt[keep_nib(m < 2 ? wd0 : wd1, 16 * (m & 1) + g)];
-            aP0 = p0 * (f2){km.x, km.y};
-            aP1 = p1 * (f2){km.z, km.w};
-            d0 = fma2(aP0, g0, -(p0 * Di));
-            d1 = fma2(aP1, g1, -(p1 * Di));
-          } else {
-            d0 = p0 * (g0 - Di);
-            d1 = p1 * (g1 - Di);
-          }
-          f4v& acc = (m & 1) ? dq1 : dq0;
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kT[m][0], d0.x, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kT[m][1], d0.y, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kT[m][2], d1.x, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kT[m][3], d1.y, acc, 0, 0, 0);
-          // T[key 4r + g][query c16]
-          float* tp = trw + m * (2 * 16 * TS) + g * TS + c16;
-          tp[0] = aP0.x; tp[4 * TS] = aP0.y; tp[8 * TS] = aP1.x; tp[12 * TS] = aP1.y;
-          tp += 16 * TS;
-          tp[0] = d0.x; tp[4 * TS] = d0.y; tp[8 * TS] = d1.x; tp[12 * TS] = d1.y;
-        }
-        // the next sub-tile's products (its rows are staged: padding rows are zeros)
-        if (PREF && j < 3) scores(j + 1, S, G);
-        // dV[key] += aP[q, key] dO[q]  over this lane's queries 16j + 4g + i
-        {
-          f2 dr[4][4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) lrow2<8>(Ds_ + (16 * j + 4 * g + i) * DH, dr[i]);
-#pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            const float4 ap = *reinterpret_cast<const float4*>(trw + m * (2 * 16 * TS) + c16 * TS + 4 * g);
-            const f2 a01 = {ap.x, ap.y}, a23 = {ap.z, ap.w};
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-              dv[m][p] = fma2_lo(dr[0][p], a01, dv[m][p]);
-              dv[m][p] = fma2_hi(dr[1][p], a01, dv[m][p]);
-              dv[m][p] = fma2_lo(dr[2][p], a23, dv[m][p]);
-              dv[m][p] = fma2_hi(dr[3][p], a23, dv[m][p]);
-            }
-          }
-        }
-        // dK[key] += dS[q, key] Qs[q]
-        {
-          f2 qr[4][4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) lrow2<8>(Qs + (16 * j + 4 * g + i) * DH, qr[i]);
-#pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            const float4 ds = *reinterpret_cast<const float4*>(trw + m * (2 * 16 * TS) + 16 * TS +
-                                                               c16 * TS + 4 * g);
-            const f2 s01 = {ds.x, ds.y}, s23 = {ds.z, ds.w};
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-              dk[m][p] = fma2_lo(qr[0][p], s01, dk[m][p]);
-              dk[m][p] = fma2_hi(qr[1][p], s01, dk[m][p]);
-              dk[m][p] = fma2_lo(qr[2][p], s23, dk[m][p]);
-              dk[m][p] = fma2_hi(qr[3][p], s23, dk[m][p]);
-            }
-          }
-        }
-        // dQ^T rows d = 4g + r of this sub-tile -> the wave's slot (rows 8..15 are zero:
-        // stored anyway, so no branch splits this block)
-        *reinterpret_cast<f4v*>(Qw + (wv * TK + qq) * QWS + 4 * g) = dq0 + dq1;
-      }
-    }
-    // dQ rows of this tile: the waves' key ranges summed (fixed order); key block kb's
-    // share (nkb > 1: a partial slot, summed after the launch)
-    __syncthreads();
-    float* dqb = a.dq + kb * a.dq_ss + (int64_t)b * a.dq_bs + h * DH;
-    for (int idx = t; idx < qend * (DH / 4); idx += NTT) {
-      const int i = idx / (DH / 4), c = (idx - i * (DH / 4)) * 4;
-      float4 acc = *reinterpret_cast<const float4*>(Qw + i * QWS + c);
-#pragma unroll
-      for (int w = 1; w < NWV; ++w) {
-        const float4 u = *reinterpret_cast<const float4*>(Qw + (w * TK + i) * QWS + c);
-        acc.x += u.x; acc.y += u.y; acc.z += u.z; acc.w += u.w;
-      }
-      acc.x *= a.scale; acc.y *= a.scale; acc.z *= a.scale; acc.w *= a.scale;
-      *reinterpret_cast<float4*>(dqb + (int64_t)(qt + i) * a.dq_ls + c) = acc;
-    }
-  }
-  // the four lanes of a key (g = 0..3) hold partial dV / dK over their queries: a
-  // transposing butterfly (permlane32, then permlane16 swaps) leaves lane g with the totals
-  // of m-tile g -- component e = 16m + x: x < 8 dV dim x, x >= 8 dK dim x - 8
-  auto comp = [&](int e) -> float {
-    const int m = e >> 4, x = e & 15;
-    const f2 v = x < 8 ? dv[m][x >> 1] : dk[m][(x - 8) >> 1];
-    return (x & 1) ? v.y : v.x;
-  };
-  float u[32], s[16];
-#pragma unroll
-  for (int e = 0; e < 32; ++e) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(comp(e)),
-                                                    __float_as_uint(comp(e + 32)), false, false);
-    u[e] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(u[e]),
-                                                    __float_as_uint(u[e + 16]), false, false);
-    s[e] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-  const int key = kw0 + 16 * g + c16;
-  if (key < a.Lk) {
-    const float kf = a.scale / a.scale_log2;
-    float rv[DH], rk[DH];
-#pragma unroll
-    for (int d = 0; d < DH; ++d) { rv[d] = s[d]; rk[d] = s[8 + d] * kf; }
-    str<DH>(a.dv + blockIdx.y * a.dk_ss + (int64_t)b * a.dv_bs + (int64_t)key * a.dv_ls + h * DH, rv);
-    str<DH>(a.dk + blockIdx.y * a.dk_ss + (int64_t)b * a.dk_bs + (int64_t)key * a.dk_ls + h * DH, rk);
   }
 }
 
@@ -2321,42 +1694,6 @@ __global__ __launch_bounds__(SNT) void attn_bwd_smallq_kernel(AttnArgs a) {
   }
 }
 
-// The keep bitmap of a query-tiled forward launch, generated ahead of it:
-// bit-identical to what attn_fwd_kernel's hashing path writes for the same
-// (rng_state, call_id, shape) -- keys below round_up(Lk, 8) hashed, the rest 0.
-// lane = query (coalesced [word][query] stores), grid.y = word chunks.  Pure
-// integer VALU work with no data inputs, so it can run on a side stream while
-// the latency-bound encoders leave the chip idle (bits per layer: B*H*Lq*Lk).
-constexpr int GEN_NT = 256, GEN_WORDS = 8;
-__global__ __launch_bounds__(GEN_NT) void attn_keep_bits_kernel(int BH, int Lq, int Lk, int nw,
-                                                               uint32_t thr,
-                                                               const int64_t* rng_state,
-                                                               uint32_t call_id,
-                                                               uint32_t* __restrict__ bits) {
-  const int nqb = (Lq + GEN_NT - 1) / GEN_NT;
-  const int bh = blockIdx.x / nqb, qb = blockIdx.x - bh * nqb;
-  const int q = qb * GEN_NT + threadIdx.x;
-  if (bh >= BH) return;
-  const uint32_t skey = key_of(rng_state, call_id);
-  const uint32_t rk = attn_row_key(skey, (uint32_t)((int64_t)bh * Lq + min(q, Lq - 1)));
-  const int klim = (Lk + 7) & ~7;
-  const int w0 = blockIdx.y * GEN_WORDS, w1 = min(nw, w0 + GEN_WORDS);
-  uint32_t* out = bits + (int64_t)bh * nw * Lq + q;
-  for (int wd = w0; wd < w1; ++wd) {
-    uint32_t w = 0u;
-#pragma unroll 4
-    for (int j = 0; j < 32; j += 2) {
-      const int key = wd * 32 + j;
-      if (key < klim) {
-        const uint32_t kpm = attn_keypair_mix(skey, (uint32_t)(key >> 1));
-        const uint32_t hb = attn_pair_bits_mixed(rk, kpm);
-        w |= (((hb & 0xffffu) >= thr ? 1u : 0u) | ((hb >> 16) >= thr ? 2u : 0u)) << j;
-      }
-    }
-    if (q < Lq) out[(int64_t)wd * Lq] = w;
-  }
-}
-
 __global__ void mask_bias_kernel(const uint8_t* __restrict__ m, int64_t n, float* __restrict__ out) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < n) out[t] = m[t] ? -INFINITY : 0.f;
@@ -2384,21 +1721,12 @@ void fill_common(AttnArgs& a, int B, int H, int Lq, int Lk, int dh, float p_drop
 // row-slot efficiency; the small encoder grids (B*H = 64) fall through to NP=1
 // / 64 threads.
 struct Geo { int nt, np; };
-// forced geometry: VAESNE_ATTN_GEO="nt,np" at load, or vaesne_attn_force_geometry()
-// (tuning and tests: every geometry is reachable on small shapes); nt = 0 -> auto
-Geo g_forced = [] {
-  Geo f{0, 0};
-  if (const char* e = getenv("VAESNE_ATTN_GEO")) sscanf(e, "%d,%d", &f.nt, &f.np);
-  return f;
-}();
-// geometry of the split launches (grids that leave a split in place: the encoder's
-// context self-attention): 256 x 2 (staging shared by 4 waves; A/B 9.52 -> 9.49 ms per
-// step); VAESNE_ATTN_SPLIT_GEO="nt,np" at load, "0,0" = the row-slot rule
-Geo g_split = [] {
-  Geo f{256, 2};
-  if (const char* e = getenv("VAESNE_ATTN_SPLIT_GEO")) sscanf(e, "%d,%d", &f.nt, &f.np);
-  return f;
-}();
+// forced geometry: vaesne_attn_force_geometry() (tests: every geometry is reachable on
+// small shapes); nt = 0 -> auto
+Geo g_forced{0, 0};
+// geometry of the split launches (grids that leave a split in place): 256 x 2 (staging
+// shared by 4 waves; A/B 9.52 -> 9.49 ms per step against the row-slot rule)
+constexpr Geo kSplitGeo{256, 2};
 Geo pick_geo(int64_t bh, int L) {
   if (g_forced.nt > 0) return g_forced;
   // among geometries with >= 1024 workgroups, the one wasting the fewest row
@@ -2414,66 +1742,15 @@ Geo pick_geo(int64_t bh, int L) {
       const double eff = (double)L / (double)(rows * nb);
       if (bh * nb >= 1024 && eff > best_eff + 1e-9) { best = {nt, np}; best_eff = eff; }
     }
-  if (g_split.nt > 0 && L >= 256) {   // this pick would be split (< 2048 waves): g_split
+  if (L >= 256) {   // this pick would be split (< 2048 waves): the split geometry
     const int64_t waves = bh * ((L + 2 * best.np * best.nt - 1) / (2 * best.np * best.nt)) *
                           (best.nt / 64);
-    if (waves < 2048) return g_split;
+    if (waves < 2048) return kSplitGeo;
   }
   return best;
 }
 
-// matrix-core attention kernels (head_dim 8).  Forward / fused backward: 0 = the packed-
-// VALU kernels (default), 4 or 8 = the matrix-core kernel with that many waves per
-// workgroup, 1 = auto: the matrix-core kernel (4 waves) only for grids too small to fill
-// the chip (the split launches: the encoders' 983-token context self-attention, B*H = 64),
-// where it is faster alone (fwd 0.065 vs 0.088 ms, bwd 0.10 vs 0.13 ms).  In the step every
-// matrix-core setting is slower (auto 9.09 vs 8.85 ms): its MFMAs stall the packed-VALU
-// attention kernels running beside it on the other stream (profiles/r04_ab).
-// bwd_ahead: issue each sub-tile's products one sub-tile ahead.  From VAESNE_ATTN_MFMA_FWD /
-// _BWD / _BWD_AHEAD at load, or vaesne_attn_mfma_config().  A forced geometry selects the
-// packed-VALU kernels.
-struct MfmaCfg { int fwd, bwd, bwd_ahead; };
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-int mfma_mode(int v) { return v == 0 ? 0 : (v == 1 ? 1 : (v == 8 ? 8 : 4)); }
-MfmaCfg mfma_cfg_from_env() {
-  MfmaCfg c;
-  c.fwd = mfma_mode(env_int("VAESNE_ATTN_MFMA_FWD", 0));
-  c.bwd = mfma_mode(env_int("VAESNE_ATTN_MFMA_BWD", 0));
-  c.bwd_ahead = env_int("VAESNE_ATTN_MFMA_BWD_AHEAD", 0) != 0;
-  return c;
-}
-MfmaCfg g_mfma = mfma_cfg_from_env();
-
-// tuning / A/B hook: VAESNE_ATTN_FUSED_DQ=0 keeps dQ in its own kernel
-bool fused_dq_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("VAESNE_ATTN_FUSED_DQ");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 int64_t waves_of(int64_t bh, int L);
-// waves per workgroup of the matrix-core forward / fused backward for this launch (0: the
-// packed-VALU kernel); auto picks it where the packed-VALU launch would be split
-int mfma_pick(int mode, int64_t bh, int L) {
-  if (g_forced.nt != 0 || mode == 0) return 0;
-  if (mode == 1) return waves_of(bh, L) < 2048 ? 4 : 0;
-  return mode;
-}
-int mfma_fwd_for(int dh, int64_t bh, int Lq) {
-  if (dh != 8) return 0;
-  const int w = mfma_pick(g_mfma.fwd, bh, Lq);
-  return g_mfma.fwd == 1 && Lq < 256 ? 0 : w;   // auto: full 256-query blocks only
-}
-int mfma_bwd_for(int dh, int64_t bh, int Lk) {
-  if (dh != 8 || !fused_dq_enabled()) return 0;
-  const int w = mfma_pick(g_mfma.bwd, bh, Lk);
-  return g_mfma.bwd == 1 && Lk < 256 ? 0 : w;   // auto: full 256-key blocks only
-}
 
 // Split launches for grids too small to fill the chip (the encoder's 983-token
 // context self-attention: B*H = 64 sequences -> 512 one-wave workgroups): the
@@ -2482,15 +1759,12 @@ int mfma_bwd_for(int dh, int64_t bh, int Lk) {
 // grid row; partial results go to the workspace and a fixed-order combine
 // kernel finishes them (bitwise reproducible).
 struct Split { int n, chunk; };
-// target waves of a split launch: VAESNE_ATTN_SPLIT_WAVES at load (tuning)
-const int64_t g_split_waves = [] {
-  const char* e = getenv("VAESNE_ATTN_SPLIT_WAVES");
-  return e ? std::max<int64_t>(1024, atoll(e)) : (int64_t)4096;
-}();
+// target waves of a split launch (2048 / 8192 measured slower in the step)
+constexpr int64_t kSplitWaves = 4096;
 Split pick_split(int64_t waves, int L) {
   Split sp{1, L};
   if (waves >= 2048 || L < 256) return sp;
-  int n = (int)std::min<int64_t>(16, (g_split_waves + waves - 1) / waves);
+  int n = (int)std::min<int64_t>(16, (kSplitWaves + waves - 1) / waves);
   n = std::min(n, L / 128);
   if (n <= 1) return sp;
   sp.chunk = ((L + n - 1) / n + 63) / 64 * 64;
@@ -2589,10 +1863,6 @@ int64_t fwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sp) {
 }
 // key blocks of the dK/dV launch (the fused dQ's partial count)
 int kv_blocks(int64_t bh, int Lk, int dh) {
-  if (const int nw = mfma_bwd_for(dh, bh, Lk)) {
-    const int kb = 64 * nw;
-    return (Lk + kb - 1) / kb;
-  }
   const Geo g = pick_geo(bh, Lk);
   return (Lk + 2 * g.np * g.nt - 1) / (2 * g.np * g.nt);
 }
@@ -2610,10 +1880,7 @@ int64_t bwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sq, Split& sk
   sk = {1, Lq};   // dK/dV: query chunks
   if (Lq <= 2 * SQ) return 0;
   sq = pick_split(waves_of((int64_t)B * H, Lq), Lk);
-  const int mw = mfma_bwd_for(dh, (int64_t)B * H, Lk);
-  const int64_t kv_waves = mw ? (int64_t)B * H * kv_blocks((int64_t)B * H, Lk, dh) * mw
-                              : waves_of((int64_t)B * H, Lk);
-  sk = pick_split(kv_waves, Lq);
+  sk = pick_split(waves_of((int64_t)B * H, Lk), Lq);
   return bwd_dq_floats(B, H, Lq, Lk, dh, sq) +
          (int64_t)(sk.n > 1 ? sk.n : 0) * B * Lk * H * dh * 2;
 }
@@ -2636,7 +1903,7 @@ int64_t bwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sq, Split& sk
   }
 
 template <int DHV>
-int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s, bool bits_in) {
+int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s) {
   if (a.Lq <= 2 * SQ) {
     dim3 grid((unsigned)((int64_t)a.B * a.H), (unsigned)((a.Lq + SQ - 1) / SQ));
     if (p_drop > 0.f)
@@ -2657,34 +1924,15 @@ int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s, bool b
   } else {
     sp = {1, a.Lk};
   }
-  const int nwv = bits_in ? 0 : mfma_fwd_for(DHV, (int64_t)a.B * a.H, a.Lq);
-  if (nwv) {
-    const int qb = 64 * nwv;
-    dim3 grid((unsigned)((int64_t)a.B * a.H * ((a.Lq + qb - 1) / qb)), (unsigned)sp.n);
-    if (nwv == 8) {
-      if (p_drop > 0.f)
-        hipLaunchKernelGGL((attn_fwd_mfma_kernel<true, 8>), grid, dim3(512), 0, s, c);
-      else
-        hipLaunchKernelGGL((attn_fwd_mfma_kernel<false, 8>), grid, dim3(512), 0, s, c);
-    } else {
-      if (p_drop > 0.f)
-        hipLaunchKernelGGL((attn_fwd_mfma_kernel<true, 4>), grid, dim3(256), 0, s, c);
-      else
-        hipLaunchKernelGGL((attn_fwd_mfma_kernel<false, 4>), grid, dim3(256), 0, s, c);
-    }
-  } else {
   const Geo g = pick_geo((int64_t)a.B * a.H, a.Lq);
   VAESNE_GEO_SWITCH(g, {
     const int nqb = (a.Lq + 2 * NP * NTT - 1) / (2 * NP * NTT);
     dim3 grid((unsigned)((int64_t)a.B * a.H * nqb), (unsigned)sp.n);
-    if (p_drop > 0.f && bits_in)
-      hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, true, true>), grid, dim3(NTT), 0, s, c);
-    else if (p_drop > 0.f)
+    if (p_drop > 0.f)
       hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, true>), grid, dim3(NTT), 0, s, c);
     else
       hipLaunchKernelGGL((attn_fwd_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, c);
   })
-  }
   VAESNE_CHECK_LAUNCH();
   if (sp.n > 1) {
     const int64_t n = (int64_t)a.B * a.H * a.Lq;
@@ -2718,8 +1966,7 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
   // fused dK/dV/dQ (head_dim 8): one key block covers the whole key axis (dQ
   // written directly), or several write dQ partials into the workspace
   const int nkb = kv_blocks((int64_t)a.B * a.H, a.Lk, DHV);
-  const bool fuse = DHV == 8 && part == 3 && fused_dq_enabled() &&
-                    (nkb == 1 || (ws && wsf > 0));
+  const bool fuse = DHV == 8 && part == 3 && (nkb == 1 || (ws && wsf > 0));
   if (part & 1) {
     AttnArgs c = a;
     if (sk.n > 1) {   // chunked queries: partial dK / dV per chunk
@@ -2732,23 +1979,6 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
       c.dq = ws_dq; c.dq_bs = (int64_t)a.Lq * E; c.dq_ls = E;
       c.dq_ss = (int64_t)a.B * a.Lq * E;
     }
-    const int mw = fuse ? mfma_bwd_for(DHV, (int64_t)a.B * a.H, a.Lk) : 0;
-    if (mw) {
-      dim3 grid((unsigned)((int64_t)a.B * a.H * nkb), (unsigned)sk.n);
-#define VAESNE_BWD_MFMA(NW, AH)                                                            \
-  if (p_drop > 0.f)                                                                          \
-    hipLaunchKernelGGL((attn_bwd_mfma_kernel<true, NW, AH>), grid, dim3(64 * NW), 0, s, c);  \
-  else                                                                                       \
-    hipLaunchKernelGGL((attn_bwd_mfma_kernel<false, NW, AH>), grid, dim3(64 * NW), 0, s, c);
-      if (mw == 8) {
-        VAESNE_BWD_MFMA(8, false)
-      } else if (g_mfma.bwd_ahead) {
-        VAESNE_BWD_MFMA(4, true)
-      } else {
-        VAESNE_BWD_MFMA(4, false)
-      }
-#undef VAESNE_BWD_MFMA
-    } else {
     const Geo gk = pick_geo((int64_t)a.B * a.H, a.Lk);
     VAESNE_GEO_SWITCH(gk, {
       const int nkb = (a.Lk + 2 * NP * NTT - 1) / (2 * NP * NTT);
@@ -2766,7 +1996,6 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
         hipLaunchKernelGGL((attn_bwd_kv_kernel<DHV, NTT, NP, false>), grid, dim3(NTT), 0, s, c);
       }
     })
-    }
     VAESNE_CHECK_LAUNCH();
     if (sk.n > 1) {
       launch_sum_chunks(c.dk, c.dk_ss, sk.n, a.B, a.Lk, E, a.dk, a.dk_bs, a.dk_ls, s);
@@ -2808,19 +2037,13 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
 // forward: fnt threads x 2 queries per lane, frc copies per workgroup (frc sets of
 // 8 packed accumulators); backward: bnt threads x 2*bnp keys per lane, brc copies
 // per staged tile, query chunks sized so the grid has ~bwgs workgroups.
-// forward fnp query pairs per lane.  VAESNE_REP="fnt,frc,bnt,bnp,brc,bwgs,fnp" overrides
-// (tuning / tests).
+// forward fnp query pairs per lane.  vaesne_attn_rep_config() overrides (tests).
 struct RepCfg { int fnt, frc, bnt, bnp, brc, bwgs, fnp; };
 // bwgs 768: the block-1 backward now runs beside the encoders' backward chain (since the
 // latent gradient sums moved into their own kernels), and half the workgroups leave that
 // latency-bound chain more free slots (step A/B 8.79 vs 8.82 ms, profiles/r04_ab/rep_bwgs.txt)
 const RepCfg kRepDefault{0, 2, 256, 1, 16, 768, 1};
-RepCfg g_rep = [] {
-  RepCfg c = kRepDefault;
-  if (const char* e = getenv("VAESNE_REP"))
-    sscanf(e, "%d,%d,%d,%d,%d,%d,%d", &c.fnt, &c.frc, &c.bnt, &c.bnp, &c.brc, &c.bwgs, &c.fnp);
-  return c;
-}();
+RepCfg g_rep = kRepDefault;
 bool rep_cfg_ok(const RepCfg& c) {
   return (c.fnt == 0 || c.fnt == 64 || c.fnt == 128 || c.fnt == 256) &&
          (c.frc == 2 || c.frc == 4 || c.frc == 8) && (c.bnt == 128 || c.bnt == 256) &&
@@ -3037,17 +2260,6 @@ VAESNE_API int vaesne_attn_force_geometry(int nt, int np) {
   return 0;
 }
 
-VAESNE_API int vaesne_attn_mfma_config(int fwd_waves, int bwd_waves, int bwd_ahead) {
-  if (fwd_waves == -2) { g_mfma = mfma_cfg_from_env(); return 0; }
-  auto ok = [](int v) { return v < 0 || v == 0 || v == 1 || v == 4 || v == 8; };
-  if (!ok(fwd_waves) || !ok(bwd_waves) || bwd_ahead > 1)
-    return (int)hipErrorInvalidValue;
-  if (fwd_waves >= 0) g_mfma.fwd = fwd_waves;
-  if (bwd_waves >= 0) g_mfma.bwd = bwd_waves;
-  if (bwd_ahead >= 0) g_mfma.bwd_ahead = bwd_ahead;
-  return 0;
-}
-
 VAESNE_API int vaesne_mask_bias(const uint8_t* mask, int64_t n, float* out, void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(mask_bias_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
@@ -3067,35 +2279,16 @@ VAESNE_API int64_t vaesne_attn_workspace(int B, int H, int Lq, int Lk, int dh, i
   return f * (int64_t)sizeof(float);
 }
 
-VAESNE_API int vaesne_attn_keep_bits(int B, int H, int Lq, int Lk, float p_drop,
-                                     const int64_t* rng_state, uint32_t call_id,
-                                     uint32_t* keep_bits, void* stream) {
-  if (B <= 0 || Lq <= 0) return 0;
-  if (Lk <= 0 || Lq <= 2 * SQ || p_drop <= 0.f || !keep_bits || !rng_state)
-    return (int)hipErrorInvalidValue;
-  const int nw = (Lk + 31) / 32;
-  const int64_t BH = (int64_t)B * H;
-  const dim3 grid((unsigned)(BH * ((Lq + GEN_NT - 1) / GEN_NT)),
-                  (unsigned)((nw + GEN_WORDS - 1) / GEN_WORDS));
-  hipLaunchKernelGGL(attn_keep_bits_kernel, grid, dim3(GEN_NT), 0, (hipStream_t)stream, (int)BH,
-                     Lq, Lk, nw, drop_thr16(p_drop), rng_state, call_id, keep_bits);
-  VAESNE_CHECK_LAUNCH();
-  return 0;
-}
-
 VAESNE_API int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const float* k,
                                int64_t k_bs, int64_t k_ls, const float* v, int64_t v_bs,
                                int64_t v_ls, const float* kbias, int64_t kb_bs, float* o,
                                int64_t o_bs, int64_t o_ls, float* lse, int B, int H, int Lq,
                                int Lk, int dh, float p_drop, const int64_t* rng_state,
-                               uint32_t call_id, uint32_t* keep_bits, int bits_in,
-                               float* workspace, void* stream) {
+                               uint32_t call_id, uint32_t* keep_bits, float* workspace,
+                               void* stream) {
   if (B <= 0 || Lq <= 0) return 0;
   if (Lk <= 0 || (dh != 8 && dh != 16)) return (int)hipErrorInvalidValue;
   if (p_drop > 0.f && (!keep_bits || !rng_state)) return (int)hipErrorInvalidValue;
-  // a pre-generated bitmap is read by the query-tiled kernels (the few-query path
-  // never uses one)
-  if (bits_in && (Lq <= 2 * SQ || p_drop <= 0.f)) return (int)hipErrorInvalidValue;
   if (!aligned16(q, q_ls) || !aligned16(k, k_ls) || !aligned16(v, v_ls) || !aligned16(o, o_ls))
     return (int)hipErrorInvalidValue;
   AttnArgs a{};
@@ -3108,8 +2301,8 @@ VAESNE_API int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const
   a.bits = keep_bits;
   fill_common(a, B, H, Lq, Lk, dh, p_drop, rng_state, call_id);
   hipStream_t s = (hipStream_t)stream;
-  if (dh == 8) return launch_fwd<8>(a, p_drop, workspace, s, bits_in != 0);
-  return launch_fwd<16>(a, p_drop, workspace, s, bits_in != 0);
+  if (dh == 8) return launch_fwd<8>(a, p_drop, workspace, s);
+  return launch_fwd<16>(a, p_drop, workspace, s);
 }
 
 namespace {

@@ -67,15 +67,8 @@ __global__ void __launch_bounds__(1024) colsum4_kernel(const float* __restrict__
   }
 }
 
-bool colsum_vec_on() {   // VAESNE_COLSUM_VEC=0: 1 column per thread everywhere (A/B)
-  static const bool on = [] {
-    const char* v = getenv("VAESNE_COLSUM_VEC");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
 bool colsum_vec_ok(const float* P, int F, int64_t ld) {
-  return colsum_vec_on() && ld % 4 == 0 && F % 4 == 0 && (uintptr_t)P % 16 == 0;
+  return ld % 4 == 0 && F % 4 == 0 && (uintptr_t)P % 16 == 0;
 }
 
 __global__ void __launch_bounds__(1024) colsum_kernel(const float* __restrict__ P, int G, int F, int64_t ld,

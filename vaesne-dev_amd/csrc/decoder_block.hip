@@ -1636,16 +1636,12 @@ int dispatch_fused(const Tail& a, int grid, hipStream_t s) {
 #undef VAESNE_FUSED_CASE
 }
 
-// long sequences take the fused backward (VAESNE_TAIL_FUSED=0, or
-// vaesne_dec_tail_force_path(2): the two-kernel path; force_path(1): fused always)
+// long sequences take the fused backward (vaesne_dec_tail_force_path(2): the two-kernel
+// path; force_path(1): fused always)
 int g_tail_path = 0;
 bool use_fused(int L) {
-  static const bool env_off = [] {
-    const char* e = getenv("VAESNE_TAIL_FUSED");
-    return e && e[0] == '0';
-  }();
   if (g_tail_path == 1) return true;
-  if (g_tail_path == 2 || env_off) return false;
+  if (g_tail_path == 2) return false;
   return L >= 256;
 }
 

@@ -712,14 +712,23 @@ VAESNE_API int vaesne_step_advance(float* step, int64_t* rng_state, void* stream
 }
 
 // out[0] = value[0] * scale; out[1], out[2] = flag[0], flag[1] as floats (0 without a flag)
+// A non-finite value also raises the loss flag word (flag[1] and out[2]): losses composed
+// of torch ops (a custom loss_fn, negInfoNCE) set no flag themselves, and this launch runs on
+// the stream ahead of the update that reads flag / out[2] as its skip word.
 __global__ void loss_stat_kernel(const float* __restrict__ value, float scale,
-                                 const int32_t* __restrict__ flag, float* __restrict__ out) {
+                                 int32_t* __restrict__ flag, float* __restrict__ out) {
   const int t = threadIdx.x;
-  if (t == 0) out[0] = value[0] * scale;
-  else if (t < 3) out[t] = flag ? (float)flag[t - 1] : 0.f;
+  const float v = value[0] * scale;
+  const bool bad = !isfinite(v);
+  if (t == 0) {
+    out[0] = v;
+    if (bad && flag) flag[1] = 1;
+  } else if (t < 3) {
+    out[t] = (t == 2 && bad) ? 1.f : (flag ? (float)flag[t - 1] : 0.f);
+  }
 }
 
-VAESNE_API int vaesne_loss_stat(const float* value, float scale, const int32_t* flag, float* out,
+VAESNE_API int vaesne_loss_stat(const float* value, float scale, int32_t* flag, float* out,
                                 void* stream) {
   if (!value || !out) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(loss_stat_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, value, scale,

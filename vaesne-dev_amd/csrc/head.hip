@@ -41,6 +41,7 @@ __device__ __forceinline__ void head_input(const float* __restrict__ x, int64_t 
 // W row-major [HE][HE] into LDS, optionally transposed
 // (all of a thread's loads in flight before its LDS stores)
 __device__ __forceinline__ void stage_w(float* dst, const float* __restrict__ W, bool transpose) {
+  static_assert(HE * HE % HNT == 0, "stage_w: every thread stages the same count of W");
   constexpr int N = HE * HE / HNT;
   float r[N];
 #pragma unroll
