@@ -57,6 +57,11 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 matrix peak (spec)
+F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: BF16 / F16 dense MFMA peak (spec)
+# f16 MFMA FLOPs the split-f16 attention issues per score: forward S^T and P V (P V as hi and lo
+# B operands: 2 MFMAs per 16x16 output tile of 32 keys), backward S, dP, dV, dK, dQ -- each
+# 16x16x32 MFMA = 16384 FLOPs over 256 (forward: 512) scores
+SF16_MFMA_FLOPS_PER_SCORE = {"fwd": 4 * 16384 / 512, "bwd": 5 * 16384 / 256}
 HBM_PEAK_GBS = 8000.0
 
 CFG = dict(workload="ZTF_photospect MMVAE training step (cfg 5)", num_bands=2, latent_len=4,
@@ -297,8 +302,11 @@ def roofline(device, B, in_step=None):
     is reported beside it.  Algorithmic FLOPs per score on SURVEY.md §8(d)'s
     FlopCounterMode basis: fwd 4*dh (QK^T, PV), bwd 8*dh (= 2x forward: dP, dV,
     dK, dQ).  The flash backward also recomputes S (2*dh more per score):
-    reported separately as flops_incl_recompute, never in `achieved`.  The kernel
-    is packed-VALU fp32 (v_pk_fma_f32), so the peak is the FP32 vector rate.
+    reported separately as flops_incl_recompute, never in `achieved`.  The head_dim-8
+    kernels are the split-f16 matrix-core ones (attention_sf16.hip): fp32-grade products
+    (hi*hi + hi*lo + lo*hi on v_mfma_f32_16x16x32_f16), so `achieved` is fp32-basis
+    algorithmic FLOP/s against the FP32 peak; `mfma_f16` reports the f16 matrix-core
+    FLOP/s they issue against the f16 MFMA peak.
     `in_step`: {"attn_fwd" / "attn_bwd": (avg ms, launches)} timed with HIP events
     around the decoder-shape launches inside the training step (in_step_kernel_times);
     the headline `achieved` uses it, the isolated launches are reported beside it."""
@@ -336,11 +344,12 @@ def roofline(device, B, in_step=None):
     fwd()
     scores = N * H * L * L
     res = {}
-    for name, kern, fn, fl in [("fwd", "attn_fwd_kernel", fwd, 4 * dh),
-                               ("bwd", "attn_bwd_kv_kernel", bwd(lib.attn_bwd), 8 * dh)]:
+    for name, kern, fn, fl in [("fwd", "attn_fwd_sf16_kernel", fwd, 4 * dh),
+                               ("bwd", "attn_bwd_sf16_kernel", bwd(lib.attn_bwd), 8 * dh)]:
         t = time_kernel(fn, 20, device)
         res[name] = dict(kernel=kern, ms=t * 1e3, tflops=scores * fl / t / 1e12,
-                         flops_per_launch=scores * fl)
+                         flops_per_launch=scores * fl,
+                         mfma_f16_tflops=scores * SF16_MFMA_FLOPS_PER_SCORE[name] / t / 1e12)
         tr, src = _rocprof_avg_ms(kern)   # the committed kernel-trace average inside the step
         if tr is not None:
             res[name].update(ms_rocprof=tr, tflops_rocprof=scores * fl / (tr * 1e-3) / 1e12,
@@ -377,7 +386,9 @@ def roofline(device, B, in_step=None):
         if in_step and key in in_step:
             ms, n = in_step[key]
             res[name].update(ms_in_step=ms, launches_in_step=n,
-                             tflops_in_step=scores * fl / (ms * 1e-3) / 1e12)
+                             tflops_in_step=scores * fl / (ms * 1e-3) / 1e12,
+                             mfma_f16_tflops_in_step=scores * SF16_MFMA_FLOPS_PER_SCORE[name]
+                             / (ms * 1e-3) / 1e12)
     r = res["bwd"]
     a = r.get("tflops_in_step", r["tflops"])
     traffic, tsrc = None, None
@@ -387,7 +398,8 @@ def roofline(device, B, in_step=None):
         tsrc = t["source"] + "; " + t["correction"]
     except (OSError, KeyError, ValueError):
         pass
-    out = dict(bound="valu_fp32", kernel=r["kernel"], achieved=round(a, 3), peak=FP32_PEAK_TFLOPS,
+    mf = r.get("mfma_f16_tflops_in_step", r["mfma_f16_tflops"])
+    out = dict(bound="fp32_flops", kernel=r["kernel"], achieved=round(a, 3), peak=FP32_PEAK_TFLOPS,
                unit="TFLOP/s", frac=round(a / FP32_PEAK_TFLOPS, 4), traffic=traffic,
                traffic_source=tsrc,
                launch_ms=round(r.get("ms_in_step", r["ms"]), 4),
@@ -401,8 +413,16 @@ def roofline(device, B, in_step=None):
                algorithmic_bytes_per_launch=attn_bwd_algorithmic_bytes(N, H, L, dh, pd),
                detail={k: {kk: (round(vv, 4) if isinstance(vv, float) else vv)
                            for kk, vv in v.items()} for k, v in res.items()},
-               note="fp32 packed-VALU kernel (v_pk_fma_f32); peak = FP32 157.3 TF (vector = "
-                    "f32-MFMA rate on gfx950); FLOPs per score 8*dh (FlopCounterMode: backward = "
+               mfma_f16=dict(achieved=round(mf, 2), peak=F16_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                             frac=round(mf / F16_MFMA_PEAK_TFLOPS, 4),
+                             flops_per_score=SF16_MFMA_FLOPS_PER_SCORE["bwd"]),
+               product_scheme=("split-f16 on v_mfma_f32_16x16x32_f16: x = hi + lo (f16 each, "
+                               "2^-22 relative), x*y = hi*hi + hi*lo + lo*hi with fp32 "
+                               "accumulation (<= 2^-20 relative per product, "
+                               "tests/test_gpu_sf16.py)"),
+               note="split-f16 matrix-core kernel, fp32-grade products; achieved = fp32-basis "
+                    "algorithmic FLOP/s, peak = FP32 157.3 TF; FLOPs per score 8*dh "
+                    "(FlopCounterMode: backward = "
                     "2x forward, S recompute excluded); scores per launch = 2*K*B*H*982^2 = %d; "
                     "launch_ms = in-step HIP events (headline), launch_ms_isolated = the same "
                     "launch alone on a stream, ms_rocprof = the committed kernel-trace "

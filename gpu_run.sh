@@ -9,6 +9,7 @@ ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 1 = assertion failures, not a GPU
 STAGES="${STAGES:-tests smoke bench prof}"
 for s in $STAGES; do
   case $s in
+    probe) timeout -k 10 120 python tools/probe/mfma_probe.py > gpurun_out/probe.log 2>&1; rc=$?;;
     tests) timeout -k 10 1100 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1; rc=$?;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?;;
     bench) timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?;;

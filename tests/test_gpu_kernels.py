@@ -75,8 +75,8 @@ def test_mha_forward_backward_vs_oracle(B, Lq, Lk, self_attn, pm):
     out, _ = mha(xq_d, xk_d, xk_d, key_padding_mask=None if mask is None else mask.to(DEV))
     (out * go.float().to(DEV)).sum().backward()
     assert _rel(out, ref) < 2e-5
-    if Lk == 1:   # softmax over one key is constant: dQ is analytically 0 (fp32 rounding only)
-        assert xq_d.grad.abs().max().item() < 1e-6
+    if Lk == 1:   # softmax over one key is constant: dQ is analytically 0 (rounding only)
+        assert xq_d.grad.abs().max().item() < 1e-5
     else:
         assert _rel(xq_d.grad, xq_r.grad) < 1e-4
     if not self_attn:
@@ -88,7 +88,7 @@ def test_mha_forward_backward_vs_oracle(B, Lq, Lk, self_attn, pm):
     bref = pr["a.in_proj_bias"].grad
     bgot = mha.in_proj_bias.grad
     if Lk == 1:
-        assert bgot[:E_].abs().max().item() < 1e-6
+        assert bgot[:E_].abs().max().item() < 1e-5
     else:
         assert _rel(bgot[:E_], bref[:E_]) < 1e-4
     assert _rel(bgot[2 * E_:], bref[2 * E_:]) < 1e-4
@@ -677,9 +677,8 @@ def test_forward_is_bitwise_reproducible_and_keep_rate(geo, B, H, Lq, Lk, dh):
             runs.append((o, lse, bits))
         (o0, l0, b0), (o1, l1, b1) = runs
         assert torch.equal(o0, o1) and torch.equal(l0, l1) and torch.equal(b0, b1)
-        w = b0.view(B * H, (Lk + 31) // 32, Lq).cpu().numpy().view(np.uint32)
-        bitsv = np.unpackbits(w.view(np.uint8), bitorder="little").reshape(B * H, -1, Lq, 32)
-        keep = bitsv.transpose(0, 2, 1, 3).reshape(B * H, Lq, -1)[:, :, :Lk]
+        from test_gpu_sf16 import _decode_bits   # the split-f16 path (default, dh 8) or the VALU one
+        keep = _decode_bits(b0, B, Lq, Lk, geo == (0, 0) and dh == 8, H=H).numpy()
         rate = 1 - keep.mean()
         assert abs(rate - p) < 5 * math.sqrt(p * (1 - p) / keep.size), rate
     finally:

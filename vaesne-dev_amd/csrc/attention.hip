@@ -23,49 +23,17 @@
 #include <cstdio>
 #include <cstdlib>
 
-#include "common.h"
+#include "attn_common.h"
 
 using namespace vaesne;
 
 namespace {
 
 constexpr int TK = 64;   // keys (or queries) per LDS tile
-// running-max origin of the forward kernels before any key is seen: finite, so neither
-// the exponent origin nor a rescale needs a -inf fix-up per group (a row's first finite
-// score always moves it, through the lazy rescale, before any exponential reads it;
-// fully masked rows keep it with l = 0 -> o = NaN, lse = -inf, as before)
-constexpr float M_INIT = -1e30f;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-struct AttnArgs {
-  const float* q; int64_t q_bs, q_ls;
-  const float* k; int64_t k_bs, k_ls;
-  const float* v; int64_t v_bs, v_ls;
-  const float* kbias; int64_t kb_bs;        // [B, Lk] additive key bias (0 / -inf) or null
-  const float* o; int64_t o_bs, o_ls;       // fwd output (bwd input)
-  float* o_out;
-  float* lse;                               // [B, H, Lq] log2 domain
-  const float* dout; int64_t do_bs, do_ls;
-  float* dq; int64_t dq_bs, dq_ls;
-  float* dk; int64_t dk_bs, dk_ls;
-  float* dv; int64_t dv_bs, dv_ls;
-  uint32_t* bits;                           // [B*H][nw][Lq] keep bitmap (dropout only)
-  int B, H, Lq, Lk, nw;
-  float scale;        // 1/sqrt(dh)
-  float scale_log2;   // log2(e)/sqrt(dh)
-  uint32_t thr; float inv_keep;
-  const int64_t* rng_state; uint32_t call_id;
-  // split launches (gridDim.y chunks, small grids only): chunk y covers keys
-  // [y*kchunk, ..) (forward, dQ) or queries [y*qchunk, ..) (dK/dV) and writes
-  // partial results at +y*(o_ss | dq_ss | dk_ss); the forward's partial o is
-  // un-normalised, with (m, l) per query in ml.  Unsplit: chunk = whole axis.
-  int kchunk, qchunk;
-  int64_t o_ss, dq_ss, dk_ss;
-  float* ml;                                // [split][B*H*Lq][2] or null
-};
-
-__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+using vaesne::ex2;
 __device__ __forceinline__ f2 ex2(f2 x) { return (f2){ex2(x.x), ex2(x.y)}; }
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 bc(float s) { return (f2){s, s}; }
@@ -95,21 +63,6 @@ __device__ __forceinline__ void lrow(const float* s, float (&r)[DH]) {
     float4 a = *reinterpret_cast<const float4*>(s + d);
     r[d] = a.x; r[d + 1] = a.y; r[d + 2] = a.z; r[d + 3] = a.w;
   }
-}
-
-// keep-bitmap assembly: w = 2 w + (this lane's bit of the lane mask m) -- one
-// v_addc with the compare's lane mask as carry-in, instead of select-to-0/1, shift, or.
-// Bits enter at the bottom, so after n pushes the first decision sits at bit n - 1:
-// keep_word() shifts and bit-reverses a word of n pushes into the bitmap layout (key j
-// of the word at bit j).
-__device__ __forceinline__ uint32_t push_bit(uint32_t w, uint64_t m) {
-  uint32_t r;
-  uint64_t co;
-  asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(w), "s"(m));
-  return r;
-}
-__device__ __forceinline__ uint32_t keep_word(uint32_t w, int n) {
-  return __builtin_bitreverse32(w << (32 - n));
 }
 
 // broadcast-operand packed FMA: c + a * {r_d, r_d} with r_d one half of an LDS
@@ -1853,10 +1806,21 @@ void launch_sum_chunks(const float* ws, int64_t ss, int n, int B, int L, int E, 
                        0, s, ws, ss, n, B, L, E, out, bs, ls);
 }
 
+// the split-f16 matrix-core kernels (attention_sf16.hip) for head_dim 8 unless a test forces
+// a packed-VALU geometry
+bool use_sf16(int dh, int64_t bh, int Lq, int Lk, bool bwd) {
+  static const int dbg_only = [] { const char* e = getenv("SF16_DBG_ONLY_L"); return e ? atoi(e) : 0; }();
+  static const int dbg_f = [] { const char* e = getenv("SF16_DBG_FWD"); return e ? atoi(e) : 1; }();
+  static const int dbg_b = [] { const char* e = getenv("SF16_DBG_BWD"); return e ? atoi(e) : 1; }();
+  if (dbg_only && Lq != dbg_only) return false;
+  if (bwd ? !dbg_b : !dbg_f) return false;
+  return g_forced.nt == 0 && sf16_path(dh, bh, Lq, Lk);
+}
+
 // workspace of a split launch (bytes; 0 = no split for this shape)
 int64_t fwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sp) {
   sp = {1, Lk};
-  if (Lq <= 2 * SQ) return 0;
+  if (Lq <= 2 * SQ || use_sf16(dh, (int64_t)B * H, Lq, Lk, false)) return 0;
   sp = pick_split(waves_of((int64_t)B * H, Lq), Lk);
   if (sp.n <= 1) return 0;
   return (int64_t)sp.n * B * Lq * H * dh + (int64_t)sp.n * B * H * Lq * 2;
@@ -1879,6 +1843,7 @@ int64_t bwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sq, Split& sk
   sq = {1, Lk};   // dQ: key chunks
   sk = {1, Lq};   // dK/dV: query chunks
   if (Lq <= 2 * SQ) return 0;
+  if (use_sf16(dh, (int64_t)B * H, Lq, Lk, true)) return sf16_bwd_ws_floats(B, H, Lq, Lk);
   sq = pick_split(waves_of((int64_t)B * H, Lq), Lk);
   sk = pick_split(waves_of((int64_t)B * H, Lk), Lq);
   return bwd_dq_floats(B, H, Lq, Lk, dh, sq) +
@@ -1913,6 +1878,7 @@ int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s) {
     VAESNE_CHECK_LAUNCH();
     return 0;
   }
+  if (use_sf16(DHV, (int64_t)a.B * a.H, a.Lq, a.Lk, false)) return sf16_fwd(a, p_drop, s);
   Split sp;
   const int64_t wsf = fwd_ws_floats(a.B, a.H, a.Lq, a.Lk, DHV, sp);
   AttnArgs c = a;
@@ -1957,6 +1923,8 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
     VAESNE_CHECK_LAUNCH();
     return 0;
   }
+  // the split-f16 backward is one fused kernel: every part runs it whole
+  if (use_sf16(DHV, (int64_t)a.B * a.H, a.Lq, a.Lk, true)) return sf16_bwd(a, p_drop, ws, s);
   Split sq, sk;
   const int64_t wsf = bwd_ws_floats(a.B, a.H, a.Lq, a.Lk, DHV, sq, sk);
   if (wsf == 0 || !ws) { sq = {1, a.Lk}; sk = {1, a.Lq}; }
@@ -2269,7 +2237,9 @@ VAESNE_API int vaesne_mask_bias(const uint8_t* mask, int64_t n, float* out, void
 }
 
 VAESNE_API int64_t vaesne_attn_keep_bits_size(int B, int H, int Lq, int Lk) {
-  return (int64_t)B * H * ((Lk + 31) / 32) * Lq * (int64_t)sizeof(uint32_t);
+  // either kernel family's layout fits (the split-f16 one pads queries to 16, keys to 128)
+  return std::max((int64_t)B * H * ((Lk + 31) / 32) * Lq * (int64_t)sizeof(uint32_t),
+                  sf16_bits_bytes(B, H, Lq, Lk));
 }
 
 VAESNE_API int64_t vaesne_attn_workspace(int B, int H, int Lq, int Lk, int dh, int bwd) {

@@ -1,0 +1,731 @@
+// Masked multi-head attention of head_dim 8 on the f16 matrix cores, at fp32 accuracy.
+//
+// The arithmetic is attention.hip's (util_layers.py:289 -> torch/nn/functional.py:6559-6594:
+// S = q k^T / sqrt(dh) + key bias, P = softmax(S), A = Dropout_p(P), O = A v, and the
+// backward of each), flash-style in the log2 domain.  What changes is where the products
+// run: every one of them (S, P V in the forward; S, dP, dV, dK, dQ in the backward) is a
+// v_mfma_f32_16x16x32_f16 on SPLIT operands.  An fp32 value x is carried as two f16,
+// hi = f16(x) and lo = f16(x - hi) (the difference is exact in fp32, rounded once), so
+// x = hi + lo to 2^-22 relative; a product x y is taken as hi_x hi_y + hi_x lo_y + lo_x hi_y
+// (the dropped lo_x lo_y is 2^-22 of it) with fp32 accumulation.  f16 MFMA issue is 16x the
+// fp32 rate (MI355X_MICROARCH.md, Matrix cores), so the three terms cost far less than the
+// packed-fp32 VALU FMAs they replace, and the VALU keeps only what is not a product: the
+// exponentials, the dropout hash and keep decisions, dS and the hi / lo conversions.
+//
+// Operand terms.  With head_dim 8, one 32-deep MFMA holds a whole dot product in its four
+// 8-element slots: lane group g (lanes 16g .. 16g + 15) carries term g.  Scores:
+//   A = Q:  [q_hi | q_hi | q_lo | 1, 1, 0..]    B = K: [k_hi | k_lo | k_hi | bias_hi, bias_lo, 0..]
+// (the fourth slot adds the key bias: 0 / -inf key padding), value products likewise.  The
+// contraction sums over slots, and A's slot (g, j) meets B's slot (g, j) whichever k the
+// hardware gives it, so the term layout needs only that A and B share one slot map.
+// Contractions over the 16 rows of an accumulator tile (P V, dV = P^T dO, dK = dS^T Q,
+// dQ = dS K) pack each value pair (x_a, x_b) as a hi pair and a lo pair in adjacent slots;
+// the other operand supplies [y_hi(a), y_hi(b), y_hi(a), y_hi(b)] for the hi rows of its
+// tile and [y_lo(a), y_lo(b), 0, 0] for its lo rows (rows f and f + 8 of the result summed
+// at the end: the same three terms).
+//
+// Range.  Softmax probabilities enter scaled, P' = 2^c P (c = 7 forward with the lazy
+// running max, 14 backward), so they sit in f16's normal range; the gradient operands of the
+// backward are scaled by per-(sequence, head) powers of two chosen from their maxima (a
+// prologue over dO and O), so dS stays below 2^15.  q, k and v enter unscaled: an element
+// beyond f16's range (65504) becomes inf and the output NaN (loud), and elements below 2^-3
+// keep an absolute error of 2^-25 instead of a relative one -- for the softmax only the
+// absolute score error matters, and it is then 2^-25 per feature product, fp32's own scale.
+//
+// Dropout.  The forward hashes each (query, key pair) exactly as attn_fwd_kernel does
+// (attn_pair_bits_mixed: the same keep decisions for the same (seed, counter, call id,
+// row, key)) and writes the keep bits in this path's own layout, which the backward reads:
+// word ((bh * NT8 + key / 128) * 4 + (key % 16) / 4) * Lqp + query, bit
+// 4 ((key % 128) / 16) + key % 4  (NT8 = ceil(Lk / 128), Lqp = Lq rounded up to 16).
+#include <algorithm>
+
+#include "attn_common.h"
+
+namespace vaesne {
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 mma(u4 a, u4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b),
+                                                c, 0, 0, 0);
+}
+// f16x2 (round to nearest even) of (a, b): the hi halves
+__device__ __forceinline__ uint32_t pk_hi(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, h2v));
+}
+// f16x2 of (a - hi.x, b - hi.y): the differences are exact in fp32, rounded once.  Plain
+// code, no inline asm: the compiler's hazard recognizer pads every producer / consumer of
+// these registers (exp results read here, MFMA operands written here), which an asm
+// statement hides from it
+__device__ __forceinline__ uint32_t pk_lo(float a, float b, uint32_t hi) {
+  const f2v h = __builtin_convertvector(__builtin_bit_cast(h2v, hi), f2v);
+  return pk_hi(a - h.x, b - h.y);
+}
+__device__ __forceinline__ _Float16 f16_hi(float x) { return (_Float16)x; }
+__device__ __forceinline__ _Float16 f16_lo(float x) {
+  return isfinite(x) ? (_Float16)(x - (float)(_Float16)x) : (_Float16)0.f;
+}
+__device__ __forceinline__ uint32_t pack2(_Float16 a, _Float16 b) {
+  return __builtin_bit_cast(uint32_t, (h2v){a, b});
+}
+__device__ __forceinline__ float max4(f4 v) { return fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])); }
+__device__ __forceinline__ f4 splat(float x) { return (f4){x, x, x, x}; }
+__device__ __forceinline__ u4 ldu4(const uint32_t* p) { return *reinterpret_cast<const u4*>(p); }
+__device__ __forceinline__ uint32_t as_u(float x) { return __float_as_uint(x); }
+
+constexpr uint32_t ONES_F16X2 = 0x3C003C00u;   // (1.0h, 1.0h): the bias slot's multipliers
+
+// =================================== forward ===================================
+// Workgroup: NW waves (NW = 1, 2, 4), wave w owns the 64 queries qb*64NW + 64w + 16n + c
+// (n = 0..3 query tiles, c = lane & 15), all keys of one (batch, head) in chunks of 32 NW
+// (one (key, half-row) staging item per thread).  Scores as S^T tiles: A = the staged K
+// image (16 keys), B = the wave's resident Q operand, C = (7 - m) per query column, so the
+// MFMA leaves S - m + 7 and p' = exp2 of it directly.  Lane (g, c) holds keys 4g..4g+3 of
+// each 16-key tile for query c: its (m, l) partial state covers its own keys, the origin m
+// is shared by the column's four lane groups (moved only together, in the rare rescale).
+// P' V: per 32 keys (two tiles), B = the lane's eight p' (hi / lo pairs), A = the staged
+// V^T image (16 rows: v_hi features 0..7, v_lo features 0..7), accumulating O^T.
+constexpr int FNW_MAX = 4;
+constexpr int FKC_MAX = 32 * FNW_MAX;
+
+template <bool DROP>
+__global__ __launch_bounds__(256, 3) void attn_fwd_sf16_kernel(AttnArgs a, int NT8, int Lqp) {
+  // per staged key: [hi 4 u32 | lo 4 | bias (hi, lo), 0 ...]; V^T per 32-key pair: 16 rows
+  // x 32 f16; key-pair mixes for the dropout hash
+  __shared__ __attribute__((aligned(16))) uint32_t Ki[2][FKC_MAX * 12];
+  __shared__ __attribute__((aligned(16))) uint32_t Vi[2][FKC_MAX * 8];
+  __shared__ __attribute__((aligned(16))) uint32_t Kp[2][FKC_MAX / 2];
+  const int NW = blockDim.x >> 6, KC = 32 * NW, QB = 64 * NW;
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, c = l & 15;
+  const int nqb = (a.Lq + QB - 1) / QB;
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int qb = wg % nqb, bh = wg / nqb;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const float* kg = a.k + (int64_t)b * a.k_bs + h * 8;
+  const float* vg = a.v + (int64_t)b * a.v_bs + h * 8;
+  const float* kbg = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
+  const uint32_t skey = DROP ? key_of(a.rng_state, a.call_id) : 0u;
+
+  // resident Q operands (term g of lane group g), running state
+  u4 Qop[4];
+  f4 Cm[4], O[4];
+  float m[4], lsum[4];
+  uint32_t rk[4], wb[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int q = qb * QB + 64 * w + 16 * n + c;
+    const int qc = min(q, a.Lq - 1);
+    const float* qp = a.q + (int64_t)b * a.q_bs + (int64_t)qc * a.q_ls + h * 8;
+    const float4 x0 = *reinterpret_cast<const float4*>(qp);
+    const float4 x1 = *reinterpret_cast<const float4*>(qp + 4);
+    const float s = a.scale_log2;
+    const float x[8] = {x0.x * s, x0.y * s, x0.z * s, x0.w * s,
+                        x1.x * s, x1.y * s, x1.z * s, x1.w * s};
+    u4 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      hi[j] = pk_hi(x[2 * j], x[2 * j + 1]);
+      lo[j] = pk_lo(x[2 * j], x[2 * j + 1], hi[j]);
+    }
+    const u4 ones = {ONES_F16X2, 0u, 0u, 0u};
+    Qop[n] = g == 3 ? ones : (g == 1 ? lo : hi);
+    m[n] = M_INIT;
+    Cm[n] = splat(7.f - M_INIT);
+    O[n] = splat(0.f);
+    lsum[n] = 0.f;
+    wb[n] = 0u;
+    rk[n] = DROP ? attn_row_key(skey, (uint32_t)((int64_t)bh * a.Lq + qc)) : 0u;
+  }
+  // K image term of lane group g: hi, hi, lo, bias
+  const int toff = g == 2 ? 4 : (g == 3 ? 8 : 0);
+
+  // staging item: key kk_i of the chunk, features 4 hf .. 4 hf + 3
+  const int kk_i = t >> 1, hf = t & 1;
+  float4 rK = make_float4(0.f, 0.f, 0.f, 0.f), rV = rK;
+  float rB = 0.f;
+  auto issue = [&](int ks) {
+    const int key = ks + kk_i;
+    const bool ok = key < a.Lk;
+    const int64_t kc = min(key, a.Lk - 1);
+    rK = ok ? *reinterpret_cast<const float4*>(kg + kc * a.k_ls + 4 * hf) : make_float4(0.f, 0.f, 0.f, 0.f);
+    rV = ok ? *reinterpret_cast<const float4*>(vg + kc * a.v_ls + 4 * hf) : make_float4(0.f, 0.f, 0.f, 0.f);
+    rB = ok ? (kbg ? kbg[key] : 0.f) : -INFINITY;
+  };
+  auto commit = [&](int ks, int buf) {
+    uint32_t* K_ = Ki[buf] + kk_i * 12;
+    const uint32_t h0 = pk_hi(rK.x, rK.y), h1 = pk_hi(rK.z, rK.w);
+    K_[2 * hf] = h0;
+    K_[2 * hf + 1] = h1;
+    K_[4 + 2 * hf] = pk_lo(rK.x, rK.y, h0);
+    K_[5 + 2 * hf] = pk_lo(rK.z, rK.w, h1);
+    if (hf == 0) {
+      K_[8] = pack2(f16_hi(rB), f16_lo(rB));
+      K_[9] = 0u;
+    } else {
+      K_[10] = 0u;
+      K_[11] = 0u;
+    }
+    // V^T: pair pp, slot of key kq in it: 8 gg + 4 tt + jj (kq = 16 tt + 4 gg + jj)
+    const int pp = kk_i >> 5, kq = kk_i & 31;
+    const int slot = 8 * ((kq & 15) >> 2) + 4 * (kq >> 4) + (kq & 3);
+    _Float16* V_ = reinterpret_cast<_Float16*>(Vi[buf]) + pp * 512 + slot;
+    const float v4[4] = {rV.x, rV.y, rV.z, rV.w};
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      V_[(4 * hf + f) * 32] = f16_hi(v4[f]);
+      V_[(8 + 4 * hf + f) * 32] = f16_lo(v4[f]);
+    }
+    if (DROP && hf == 0 && (kk_i & 1) == 0)
+      Kp[buf][kk_i >> 1] = attn_keypair_mix(skey, (uint32_t)((ks + kk_i) >> 1));
+  };
+
+  const int nch = (a.Lk + KC - 1) / KC;
+  const int Tlast = 2 * ((a.Lk + 31) / 32) - 1;     // last 16-key tile processed (pairs)
+  uint32_t* bitp = DROP ? a.bits + (int64_t)bh * NT8 * 4 * Lqp : nullptr;
+  issue(0);
+  commit(0, 0);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const int ks = ch * KC, buf = ch & 1;
+    if (ch + 1 < nch) issue(ks + KC);
+    const uint32_t* K_ = Ki[buf];
+    const uint32_t* V_ = Vi[buf];
+    for (int p = 0; p < NW; ++p) {
+      if (ks + 32 * p >= a.Lk) break;
+      const u4 A0 = ldu4(K_ + (32 * p + c) * 12 + toff);
+      const u4 A1 = ldu4(K_ + (32 * p + 16 + c) * 12 + toff);
+      f4 S0[4], S1[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        S0[n] = mma(A0, Qop[n], Cm[n]);
+        S1[n] = mma(A1, Qop[n], Cm[n]);
+      }
+      // lazy origin: p' <= 2^15 while no score passes m by more than 8
+      bool mv = false;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) mv |= fmaxf(max4(S0[n]), max4(S1[n])) > 15.f;
+      if (__builtin_amdgcn_ballot_w64(mv)) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const f4 z = splat(0.f);
+          const f4 R0 = mma(A0, Qop[n], z), R1 = mma(A1, Qop[n], z);
+          float x = fmaxf(max4(R0), max4(R1));
+          x = xmax32(x);
+          x = xmax16(x);                     // the column's max over its four lane groups
+          const float mn = fmaxf(m[n], x);
+          const float al = ex2(m[n] - mn);
+          lsum[n] *= al;
+          O[n] *= al;
+          m[n] = mn;
+          const float cc = 7.f - mn;
+          Cm[n] = splat(cc);
+          S0[n] = R0 + cc;
+          S1[n] = R1 + cc;
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          S0[n][r] = ex2(S0[n][r]);
+          S1[n][r] = ex2(S1[n][r]);
+        }
+        lsum[n] += ((S0[n][0] + S0[n][1]) + (S0[n][2] + S0[n][3])) +
+                   ((S1[n][0] + S1[n][1]) + (S1[n][2] + S1[n][3]));
+      }
+      if (DROP) {
+        // key pairs of this lane: tile 2p keys 32p + 4g + {0,1}, {2,3}; tile 2p+1 + 16
+        const uint32_t* kp = Kp[buf] + 16 * p + 2 * g;
+        const uint32_t kpm[4] = {kp[0], kp[1], kp[8], kp[9]};
+        const int T0 = ks / 16 + 2 * p;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            f4& P = u ? S1[n] : S0[n];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const uint32_t bits = attn_pair_bits_mixed(rk[n], kpm[2 * u + j]);
+              const bool klo = (bits & 0xffffu) >= a.thr, khi = (bits >> 16) >= a.thr;
+              wb[n] = push_bit(push_bit(wb[n], __builtin_amdgcn_ballot_w64(klo)),
+                               __builtin_amdgcn_ballot_w64(khi));
+              P[2 * j] = klo ? P[2 * j] : 0.f;
+              P[2 * j + 1] = khi ? P[2 * j + 1] : 0.f;
+            }
+            const int Tg = T0 + u;
+            if ((Tg & 7) == 7 || Tg == Tlast) {
+              const int q = qb * QB + 64 * w + 16 * n + c;
+              if (q < a.Lq)
+                bitp[((int64_t)(Tg >> 3) * 4 + g) * Lqp + q] = keep_word(wb[n], 4 * ((Tg & 7) + 1));
+              wb[n] = 0u;
+            }
+          }
+        }
+      }
+      // O^T += V^T P' over the 32 keys of this pair
+      const u4 VT = ldu4(V_ + p * 256 + c * 16 + g * 4);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        u4 Bh, Bl;
+        Bh[0] = pk_hi(S0[n][0], S0[n][1]);
+        Bh[1] = pk_hi(S0[n][2], S0[n][3]);
+        Bh[2] = pk_hi(S1[n][0], S1[n][1]);
+        Bh[3] = pk_hi(S1[n][2], S1[n][3]);
+        Bl[0] = pk_lo(S0[n][0], S0[n][1], Bh[0]);
+        Bl[1] = pk_lo(S0[n][2], S0[n][3], Bh[1]);
+        Bl[2] = pk_lo(S1[n][0], S1[n][1], Bh[2]);
+        Bl[3] = pk_lo(S1[n][2], S1[n][3], Bh[3]);
+        O[n] = mma(VT, Bh, O[n]);
+        O[n] = mma(VT, Bl, O[n]);
+      }
+    }
+    if (ch + 1 < nch) commit(ks + KC, buf ^ 1);
+    __syncthreads();
+  }
+  // rows f (lane groups 0, 1) + rows f + 8 (groups 2, 3); l over the column's four groups
+  const float ik = DROP ? a.inv_keep : 1.f;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const float lt = xsum16(xsum32(lsum[n]));
+    f4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = xsum32(O[n][r]);
+    const int q = qb * QB + 64 * w + 16 * n + c;
+    if (q < a.Lq && g < 2) {
+      const float sc = ik / lt;        // l == 0 (every key masked) -> NaN, as the reference
+      *reinterpret_cast<float4*>(a.o_out + (int64_t)b * a.o_bs + (int64_t)q * a.o_ls + h * 8 + 4 * g) =
+          make_float4(o[0] * sc, o[1] * sc, o[2] * sc, o[3] * sc);
+      if (g == 0) a.lse[(int64_t)bh * a.Lq + q] = m[n] + __log2f(lt) - 7.f;
+    }
+  }
+}
+
+// =================================== backward ===================================
+// Workgroup: NW waves (<= 8), wave w owns the 128 keys kb*128NW + 128w + 16t + c
+// (t = 0..7 key tiles), the lane holding key c of each tile; queries stream in tiles of 16.
+// Per (key tile, query tile), with the key on the lane and 4 queries per lane group:
+//   S' = Q K^T + bias + (14 - lse)        (C: the row constant)  -> p' = exp2(S') = 2^14 P
+//   dP' = dO' V'^T - D'                    (C: -D' = -2^s D)
+//   t = keep ? dP' : -D',  dS'' = p' t     (= 2^(14+s) dS)
+//   dV^T += dO'^T [keep p']   dK^T += Q^T dS''   (B: the lane's four values as hi / lo pairs)
+//   dQ^T += K^T dS''^T: dS'' crosses a wave-private LDS image once (8-byte row writes,
+//   ds_read_b64_tr_b16 column reads), K^T from a per-wave image built in the prologue.
+// dQ of a query tile is summed over the waves in LDS and stored (or, with several key blocks
+// per sequence, stored as a partial and summed after the launch).  Prologue: D = rowsum(dO O)
+// per query and the maxima of |dO|, |D|, |v| choose the powers of two 2^s (|t| <= 2, so
+// |dS''| <= 2^15) and 2^cs (dO' = dO sd 2^(s+cs), v' = v 2^-cs: balanced magnitudes).
+constexpr int BNW_MAX = 8;
+constexpr int BKT = 8;             // key tiles per wave
+constexpr int BLQ_MAX = 2048;      // queries of the prologue arrays
+
+template <bool DROP>
+__global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int nkb, int NT8, int Lqp) {
+  __shared__ __attribute__((aligned(16))) float Cs_l[BLQ_MAX];     // 14 - lse (-inf past Lq)
+  __shared__ __attribute__((aligned(16))) float Cd_l[BLQ_MAX];     // D, then -2^s D
+  __shared__ __attribute__((aligned(16))) uint32_t KTi[BNW_MAX * BKT * 256];   // K^T A operands
+  // staged query tile: Q A operand [16][hi | lo | ones], dO' [16][hi | lo | 0], Q^T and
+  // dO'^T A operands [16 rows][32 slots]
+  __shared__ __attribute__((aligned(16))) uint32_t Qa[2][16 * 12];
+  __shared__ __attribute__((aligned(16))) uint32_t Da[2][16 * 12];
+  __shared__ __attribute__((aligned(16))) uint32_t QT[2][256];
+  __shared__ __attribute__((aligned(16))) uint32_t DT[2][256];
+  __shared__ __attribute__((aligned(16))) uint32_t Sc[BNW_MAX][2][256];    // dS'' transposes
+  __shared__ __attribute__((aligned(16))) float Qp[2][BNW_MAX * 128];      // dQ partials
+  __shared__ float Red[3][BNW_MAX];
+  const int NW = blockDim.x >> 6, KB = 128 * NW;
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, c = l & 15;
+  const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int kb = wg % nkb, bh = wg / nkb;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int key0 = kb * KB + 128 * w;
+  const int ntile = key0 < a.Lk ? min(BKT, (a.Lk - key0 + 15) / 16) : 0;   // wave-uniform
+  const int nqt = (a.Lq + 15) / 16, Lq16 = 16 * nqt;
+  const float* qg = a.q + (int64_t)b * a.q_bs + h * 8;
+  const float* dg = a.dout + (int64_t)b * a.do_bs + h * 8;
+  const float* og = a.o + (int64_t)b * a.o_bs + h * 8;
+
+  // ---- prologue: D, row constants, maxima ----
+  float mdo = 0.f, md = 0.f, mv = 0.f;
+  for (int q = t; q < Lq16; q += blockDim.x) {
+    float D = 0.f, cs = -INFINITY;
+    if (q < a.Lq) {
+      const float* dp = dg + (int64_t)q * a.do_ls;
+      const float* op = og + (int64_t)q * a.o_ls;
+      const float4 d0 = *reinterpret_cast<const float4*>(dp), d1 = *reinterpret_cast<const float4*>(dp + 4);
+      const float4 o0 = *reinterpret_cast<const float4*>(op), o1 = *reinterpret_cast<const float4*>(op + 4);
+      const float dd[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+      const float oo[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+#pragma unroll
+      for (int f = 0; f < 8; ++f) {
+        D = fmaf(dd[f], oo[f], D);
+        mdo = fmaxf(mdo, fabsf(dd[f]));
+      }
+      md = fmaxf(md, fabsf(D));
+      cs = 14.f - a.lse[(int64_t)bh * a.Lq + q];
+    }
+    Cd_l[q] = D;
+    Cs_l[q] = cs;
+  }
+  // resident K operands, K^T image, max |v|
+  u4 Kop[BKT], Vop[BKT];
+  const float* kg = a.k + (int64_t)b * a.k_bs + h * 8;
+  const float* vg = a.v + (int64_t)b * a.v_bs + h * 8;
+  const float* kbg = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
+  _Float16* KT_ = reinterpret_cast<_Float16*>(KTi + (w * BKT) * 256);
+#pragma unroll
+  for (int tt = 0; tt < BKT; ++tt) {
+    Kop[tt] = (u4){0u, 0u, 0u, 0u};
+    if (tt < ntile) {
+      const int key = key0 + 16 * tt + c;
+      const bool ok = key < a.Lk;
+      const int64_t kc = min(key, a.Lk - 1);
+      float kr[8], vr[8];
+      {
+        const float4 k0 = *reinterpret_cast<const float4*>(kg + kc * a.k_ls);
+        const float4 k1 = *reinterpret_cast<const float4*>(kg + kc * a.k_ls + 4);
+        const float4 v0 = *reinterpret_cast<const float4*>(vg + kc * a.v_ls);
+        const float4 v1 = *reinterpret_cast<const float4*>(vg + kc * a.v_ls + 4);
+        const float kk[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+        const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+          kr[f] = ok ? kk[f] : 0.f;
+          vr[f] = ok ? vv[f] : 0.f;
+          mv = fmaxf(mv, fabsf(vr[f]));
+        }
+      }
+      const float bias = ok ? (kbg ? kbg[key] : 0.f) : -INFINITY;
+      u4 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        hi[j] = pk_hi(kr[2 * j], kr[2 * j + 1]);
+        lo[j] = pk_lo(kr[2 * j], kr[2 * j + 1], hi[j]);
+      }
+      const u4 bs = {pack2(f16_hi(bias), f16_lo(bias)), 0u, 0u, 0u};
+      Kop[tt] = g == 3 ? bs : (g == 1 ? lo : hi);
+      // K^T image of tile tt: row f (hi) / f + 8 (lo), slot 8 gs + j <-> (key 4 gs + 2 (j/4) +
+      // j%2, precision (j/2)%2); this lane (key c) writes features 2g, 2g + 1
+      const int gs = c >> 2, jb = 4 * ((c & 3) >> 1) + (c & 1);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int f = 2 * g + e;
+        const _Float16 kh = f16_hi(kr[f]), kl = f16_lo(kr[f]);
+        _Float16* row = KT_ + tt * 512 + f * 32 + 8 * gs + jb;
+        row[0] = kh;                 // (hi row, prec 0)
+        row[2] = kh;                 // (hi row, prec 1)
+        row[8 * 32] = kl;            // (lo row, prec 0)
+        row[8 * 32 + 2] = (_Float16)0.f;
+      }
+    }
+  }
+  // maxima over the workgroup
+  mdo = wave_max(mdo);
+  md = wave_max(md);
+  mv = wave_max(mv);
+  if (l == 0) {
+    Red[0][w] = mdo;
+    Red[1][w] = md;
+    Red[2][w] = mv;
+  }
+  __syncthreads();
+  float Mdo = 0.f, Md = 0.f, Mv = 0.f;
+  for (int i = 0; i < NW; ++i) {
+    Mdo = fmaxf(Mdo, Red[0][i]);
+    Md = fmaxf(Md, Red[1][i]);
+    Mv = fmaxf(Mv, Red[2][i]);
+  }
+  const float sd = DROP ? a.inv_keep : 1.f;
+  const float bnd = 8.f * Mdo * sd * Mv + Md;       // >= |keep sd dP - D|
+  int s = 0;
+  if (bnd > 0.f && isfinite(bnd)) {
+    int e;
+    frexpf(bnd, &e);                                  // bnd = m 2^e, m in [0.5, 1)
+    s = max(-100, min(100, 1 - e));                   // 2^s bnd < 2
+  }
+  int cs = 0;
+  if (Mdo > 0.f && Mv > 0.f && isfinite(Mdo) && isfinite(Mv))
+    cs = max(-30, min(30, (int)rintf(0.5f * (log2f(Mv) - log2f(Mdo * sd) - (float)s))));
+  const float fdo = ldexpf(sd, s + cs), fv = ldexpf(1.f, -cs), fd = ldexpf(1.f, s);
+  for (int q = t; q < Lq16; q += blockDim.x) Cd_l[q] *= -fd;
+  // resident V' operands
+#pragma unroll
+  for (int tt = 0; tt < BKT; ++tt) {
+    Vop[tt] = (u4){0u, 0u, 0u, 0u};
+    if (tt < ntile) {
+      const int key = key0 + 16 * tt + c;
+      const bool ok = key < a.Lk;
+      const int64_t kc = min(key, a.Lk - 1);
+      const float4 v0 = *reinterpret_cast<const float4*>(vg + kc * a.v_ls);
+      const float4 v1 = *reinterpret_cast<const float4*>(vg + kc * a.v_ls + 4);
+      const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      float vr[8];
+#pragma unroll
+      for (int f = 0; f < 8; ++f) vr[f] = ok ? vv[f] * fv : 0.f;
+      u4 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        hi[j] = pk_hi(vr[2 * j], vr[2 * j + 1]);
+        lo[j] = pk_lo(vr[2 * j], vr[2 * j + 1], hi[j]);
+      }
+      Vop[tt] = g == 3 ? (u4){0u, 0u, 0u, 0u} : (g == 1 ? lo : hi);
+    }
+  }
+  f4 dV[BKT], dK[BKT];
+#pragma unroll
+  for (int tt = 0; tt < BKT; ++tt) {
+    dV[tt] = splat(0.f);
+    dK[tt] = splat(0.f);
+  }
+
+  // ---- query tiles ----
+  // staging item (threads 0..63): query qi = t >> 2 of the tile, part 0/1: q features
+  // 4 part.., part 2/3: dO features
+  const int qi = t >> 2, part = t & 3;
+  float4 rX = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto issue = [&](int q0) {
+    if (t >= 64) return;
+    const int q = q0 + qi;
+    if (q >= a.Lq) {
+      rX = make_float4(0.f, 0.f, 0.f, 0.f);
+      return;
+    }
+    const float* src = part < 2 ? qg + (int64_t)q * a.q_ls + 4 * part
+                                : dg + (int64_t)q * a.do_ls + 4 * (part - 2);
+    rX = *reinterpret_cast<const float4*>(src);
+  };
+  auto commit = [&](int buf) {
+    if (t >= 64) return;
+    const bool isq = part < 2;
+    const int f0 = 4 * (part & 1);
+    const float m_ = isq ? a.scale_log2 : fdo;
+    const float x[4] = {rX.x * m_, rX.y * m_, rX.z * m_, rX.w * m_};
+    uint32_t* A_ = (isq ? Qa[buf] : Da[buf]) + qi * 12;
+    const uint32_t h0 = pk_hi(x[0], x[1]), h1 = pk_hi(x[2], x[3]);
+    A_[(f0 >> 1)] = h0;
+    A_[(f0 >> 1) + 1] = h1;
+    A_[4 + (f0 >> 1)] = pk_lo(x[0], x[1], h0);
+    A_[5 + (f0 >> 1)] = pk_lo(x[2], x[3], h1);
+    if (f0 == 0) {
+      A_[8] = isq ? ONES_F16X2 : 0u;
+      A_[9] = 0u;
+    } else {
+      A_[10] = 0u;
+      A_[11] = 0u;
+    }
+    // transposed A operand: rows f / f + 8, slots 8 gs + j of query qi = 4 gs + i:
+    // j = 4 (i/2) + i%2 (precision 0) and + 2 (precision 1)
+    _Float16* T_ = reinterpret_cast<_Float16*>(isq ? QT[buf] : DT[buf]);
+    const int gs = qi >> 2, i = qi & 3, j0 = 4 * (i >> 1) + (i & 1);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int f = f0 + e;
+      const _Float16 xh = f16_hi(x[e]), xl = f16_lo(x[e]);
+      _Float16* row = T_ + f * 32 + 8 * gs + j0;
+      row[0] = xh;
+      row[2] = xh;
+      row[8 * 32] = xl;
+      row[8 * 32 + 2] = (_Float16)0.f;
+    }
+  };
+  // keep words of this lane: 4 queries (q0 + 4g + r), key residue c, the wave's 128 keys
+  const uint32_t* bitw = DROP && ntile > 0
+                             ? a.bits + (((int64_t)bh * NT8 + (kb * NW + w)) * 4 + (c >> 2)) * Lqp + 4 * g
+                             : nullptr;
+  auto words = [&](int q0) -> u4 {
+    if (!DROP || ntile == 0 || q0 >= a.Lq) return (u4){0u, 0u, 0u, 0u};
+    return *reinterpret_cast<const u4*>(bitw + q0);
+  };
+  // dQ unscale: 2^-(14+s) * scale; dK: 2^-(14+s) * scale / scale_log2; dV: 2^-(14+s+cs)
+  const float uq = ldexpf(a.scale, -14 - s);
+  float* dqb = a.dq + (nkb > 1 ? (int64_t)kb * a.dq_ss : 0) + (int64_t)b * a.dq_bs + h * 8;
+  auto dq_reduce = [&](int q0, int buf) {
+    for (int i0 = t; i0 < 128; i0 += blockDim.x) {
+      const int qq = i0 >> 3, f = i0 & 7;
+      float acc = 0.f;
+      for (int i = 0; i < NW; ++i) acc += Qp[buf][i * 128 + qq * 8 + f];
+      if (q0 + qq < a.Lq) dqb[(int64_t)(q0 + qq) * a.dq_ls + f] = acc * uq;
+    }
+  };
+
+  issue(0);
+  u4 kw = words(0);
+  commit(0);
+  __syncthreads();
+  for (int it = 0; it < nqt; ++it) {
+    const int q0 = 16 * it, buf = it & 1;
+    if (it > 0) dq_reduce(q0 - 16, buf ^ 1);
+    if (it + 1 < nqt) issue(q0 + 16);
+    const u4 kwn = it + 1 < nqt ? words(q0 + 16) : (u4){0u, 0u, 0u, 0u};
+    f4 dQa = splat(0.f);
+    if (ntile > 0) {
+      const u4 QA = ldu4(Qa[buf] + c * 12 + (g == 2 ? 4 : (g == 3 ? 8 : 0)));
+      const u4 DA = ldu4(Da[buf] + c * 12 + (g == 2 ? 4 : (g == 3 ? 8 : 0)));
+      const u4 QTA = ldu4(QT[buf] + c * 16 + 4 * g);
+      const u4 DTA = ldu4(DT[buf] + c * 16 + 4 * g);
+      const f4 CS = *reinterpret_cast<const f4*>(Cs_l + q0 + 4 * g);
+      const f4 CD = *reinterpret_cast<const f4*>(Cd_l + q0 + 4 * g);
+#pragma unroll
+      for (int tt = 0; tt < BKT; ++tt) {
+        if (tt < ntile) {
+          const f4 S = mma(QA, Kop[tt], CS);
+          const f4 dP = mma(DA, Vop[tt], CD);
+          float P[4], Pd[4], dS[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            P[r] = ex2(S[r]);
+            if (DROP) {
+              const uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe((int)kw[r], 4 * tt + (c & 3), 1);
+              Pd[r] = __uint_as_float(as_u(P[r]) & mk);
+              const float tq = __uint_as_float((as_u(dP[r]) & mk) | (as_u(CD[r]) & ~mk));
+              dS[r] = P[r] * tq;
+            } else {
+              Pd[r] = P[r];
+              dS[r] = P[r] * dP[r];
+            }
+          }
+          u4 Bv, Bk;
+          Bv[0] = pk_hi(Pd[0], Pd[1]);
+          Bv[2] = pk_hi(Pd[2], Pd[3]);
+          Bv[1] = pk_lo(Pd[0], Pd[1], Bv[0]);
+          Bv[3] = pk_lo(Pd[2], Pd[3], Bv[2]);
+          Bk[0] = pk_hi(dS[0], dS[1]);
+          Bk[2] = pk_hi(dS[2], dS[3]);
+          Bk[1] = pk_lo(dS[0], dS[1], Bk[0]);
+          Bk[3] = pk_lo(dS[2], dS[3], Bk[2]);
+          dV[tt] = mma(DTA, Bv, dV[tt]);
+          dK[tt] = mma(QTA, Bk, dK[tt]);
+          // dS'' through LDS: row R = 4 (c/2) + 2 prec + c%2 holds queries 0..15 (32 B)
+          uint32_t* sc = Sc[w][tt & 1];
+          const int R = 4 * (c >> 1) + (c & 1);
+          *reinterpret_cast<uint2*>(sc + R * 8 + 2 * g) = make_uint2(Bk[0], Bk[2]);
+          *reinterpret_cast<uint2*>(sc + (R + 2) * 8 + 2 * g) = make_uint2(Bk[1], Bk[3]);
+          // the other lanes' rows must have landed before the transposed reads gather them
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          // B[slot 8g + j][query c] = row 8g + j: two 4-row transposed reads
+          const int rq = (c >> 2), cp = (c & 3);
+          const s4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s4*)(sc + (8 * g + rq) * 8 + 2 * cp));
+          const s4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s4*)(sc + (8 * g + 4 + rq) * 8 + 2 * cp));
+          const u4 Bq = {__builtin_bit_cast(uint2, r0).x, __builtin_bit_cast(uint2, r0).y,
+                         __builtin_bit_cast(uint2, r1).x, __builtin_bit_cast(uint2, r1).y};
+          const u4 KA = ldu4(KTi + (w * BKT + tt) * 256 + c * 16 + 4 * g);
+          dQa = mma(KA, Bq, dQa);
+        }
+      }
+    }
+    // this wave's dQ partial: rows f (groups 0, 1) + f + 8 (groups 2, 3)
+    f4 dq;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dq[r] = xsum32(dQa[r]);
+    if (g < 2) *reinterpret_cast<f4*>(Qp[buf] + w * 128 + c * 8 + 4 * g) = dq;
+    if (it + 1 < nqt) commit(buf ^ 1);
+    kw = kwn;
+    __syncthreads();
+  }
+  dq_reduce(16 * (nqt - 1), (nqt - 1) & 1);
+  // dK, dV: rows f + rows f + 8
+  const float uk = ldexpf(a.scale / a.scale_log2, -14 - s), uv = ldexpf(1.f, -14 - s - cs);
+#pragma unroll
+  for (int tt = 0; tt < BKT; ++tt) {
+    if (tt < ntile) {
+      f4 v, k_;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = xsum32(dV[tt][r]) * uv;
+        k_[r] = xsum32(dK[tt][r]) * uk;
+      }
+      const int key = key0 + 16 * tt + c;
+      if (g < 2 && key < a.Lk) {
+        *reinterpret_cast<float4*>(a.dv + (int64_t)b * a.dv_bs + (int64_t)key * a.dv_ls + h * 8 + 4 * g) =
+            make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(a.dk + (int64_t)b * a.dk_bs + (int64_t)key * a.dk_ls + h * 8 + 4 * g) =
+            make_float4(k_[0], k_[1], k_[2], k_[3]);
+      }
+    }
+  }
+}
+
+// out[b, q, h*8 + f] = sum over the nkb key blocks' partials (fixed order)
+__global__ void sf16_dq_sum_kernel(const float* __restrict__ ws, int64_t ss, int n, int B, int Lq,
+                                   int E, float* __restrict__ dq, int64_t bs, int64_t ls) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)B * Lq * E) return;
+  const int e = (int)(t % E);
+  const int64_t bl = t / E;
+  const int q = (int)(bl % Lq), b = (int)(bl / Lq);
+  float v = 0.f;
+  for (int i = 0; i < n; ++i) v += ws[i * ss + t];
+  dq[(int64_t)b * bs + (int64_t)q * ls + e] = v;
+}
+
+int fwd_waves(int Lq) { return Lq <= 64 ? 1 : (Lq <= 128 ? 2 : 4); }
+int bwd_waves(int Lk) { return std::min(BNW_MAX, (Lk + 127) / 128); }
+int bwd_blocks(int Lk) {
+  const int nw = bwd_waves(Lk);
+  return (Lk + 128 * nw - 1) / (128 * nw);
+}
+int lq_pad(int Lq) { return (Lq + 15) & ~15; }
+int nt8(int Lk) { return (Lk + 127) / 128; }
+
+}  // namespace
+
+bool sf16_path(int dh, int64_t bh, int Lq, int Lk) {
+  return dh == 8 && bh > 0 && Lq > 16 && Lq <= BLQ_MAX && Lk >= 1;
+}
+
+int64_t sf16_bits_bytes(int B, int H, int Lq, int Lk) {
+  return (int64_t)B * H * nt8(Lk) * 4 * lq_pad(Lq) * (int64_t)sizeof(uint32_t);
+}
+
+int64_t sf16_bwd_ws_floats(int B, int H, int Lq, int Lk) {
+  const int nkb = bwd_blocks(Lk);
+  return nkb > 1 ? (int64_t)nkb * B * Lq * H * 8 : 0;
+}
+
+int sf16_fwd(const AttnArgs& a, float p_drop, hipStream_t s) {
+  const int nw = fwd_waves(a.Lq);
+  const int64_t bh = (int64_t)a.B * a.H;
+  const dim3 grid((unsigned)(bh * ((a.Lq + 64 * nw - 1) / (64 * nw))));
+  if (p_drop > 0.f)
+    hipLaunchKernelGGL(attn_fwd_sf16_kernel<true>, grid, dim3(64 * nw), 0, s, a, nt8(a.Lk), lq_pad(a.Lq));
+  else
+    hipLaunchKernelGGL(attn_fwd_sf16_kernel<false>, grid, dim3(64 * nw), 0, s, a, nt8(a.Lk), lq_pad(a.Lq));
+  VAESNE_CHECK_LAUNCH();
+  return 0;
+}
+
+int sf16_bwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s) {
+  const int nw = bwd_waves(a.Lk), nkb = bwd_blocks(a.Lk);
+  const int64_t bh = (int64_t)a.B * a.H;
+  const int E = a.H * 8;
+  AttnArgs c = a;
+  if (nkb > 1) {
+    if (!ws) return (int)hipErrorInvalidValue;
+    c.dq = ws;
+    c.dq_bs = (int64_t)a.Lq * E;
+    c.dq_ls = E;
+    c.dq_ss = (int64_t)a.B * a.Lq * E;
+  }
+  const dim3 grid((unsigned)(bh * nkb));
+  if (p_drop > 0.f)
+    hipLaunchKernelGGL(attn_bwd_sf16_kernel<true>, grid, dim3(64 * nw), 0, s, c, nkb, nt8(a.Lk), lq_pad(a.Lq));
+  else
+    hipLaunchKernelGGL(attn_bwd_sf16_kernel<false>, grid, dim3(64 * nw), 0, s, c, nkb, nt8(a.Lk), lq_pad(a.Lq));
+  VAESNE_CHECK_LAUNCH();
+  if (nkb > 1) {
+    const int64_t n = (int64_t)a.B * a.Lq * E;
+    hipLaunchKernelGGL(sf16_dq_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ws,
+                       c.dq_ss, nkb, a.B, a.Lq, E, a.dq, a.dq_bs, a.dq_ls);
+    VAESNE_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+}  // namespace vaesne
