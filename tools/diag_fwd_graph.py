@@ -52,6 +52,12 @@ if os.environ.get("NO_SIDE") == "1":
 if os.environ.get("NO_CTX") == "1":
     from VAESNe import util_layers
     util_layers._ctx_stream = lambda t, i=0: None
+if os.environ.get("NO_PREP"):
+    # no latent-independent decoder prefix on the side stream: each decoder runs whole
+    from VAESNe import SpectraVAE as _S, PhotometricVAE as _P
+    for cls in [c for m in (_S, _P) for c in vars(m).values() if isinstance(c, type)]:
+        if "decode_prepare" in vars(cls):
+            delattr(cls, "decode_prepare")
 if os.environ.get("SIDE_ONLY"):
     from VAESNe import mmVAE
     _B = mmVAE._Branches

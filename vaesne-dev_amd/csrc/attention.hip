@@ -65,104 +65,47 @@ __device__ __forceinline__ void lrow(const float* s, float (&r)[DH]) {
   }
 }
 
-// broadcast-operand packed FMA: c + a * {r_d, r_d} with r_d one half of an LDS
-// row held as register pairs.  The op_sel / op_sel_hi forms read the scalar
-// straight out of the pair (the compiler otherwise copies it into a fresh pair
-// with up to two v_mov per use: ~30 % extra VALU in the inner loops).
-// Tied (in-place accumulator) forms for the forward / dQ kernels, where they
-// keep the register count down (forward 161 vs 189 VGPRs untied); untied forms
-// (_u) for the dK/dV kernel, whose accumulators start from live values.
+// broadcast-operand packed FMA: c + a * {r_d, r_d} with r_d one half of an LDS row held as
+// register pairs.
+//
+// gfx950 erratum (measured: tools/probe/mfma_interference.py, DESIGN.md "A packed-FP32
+// erratum"): a v_pk_{fma,mul,add}_f32 whose op_sel makes the LOW lane read the HIGH half
+// of a source (op_sel:[0,1,0] and friends) returns wrong values while another wave on the
+// CU runs v_mfma_f32_16x16x32_{f16,bf16} -- which the split-f16 attention kernels do,
+// beside these kernels, on the other streams of the training step.  op_sel_hi (the HIGH
+// lane reading the LOW half) is unaffected.  So the low half of a pair is broadcast by
+// one v_pk_fma_f32 with op_sel_hi (fma2_lo), the high half by two scalar FMAs (fma2_hi);
+// no kernel of this library contains the affected form (tests/test_isa_erratum.py).
 __device__ __forceinline__ f2 fma2_lo(f2 a, f2 b, f2 c) {
   asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(c) : "v"(a), "v"(b));
   return c;
 }
 __device__ __forceinline__ f2 fma2_hi(f2 a, f2 b, f2 c) {
-  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(c) : "v"(a), "v"(b));
-  return c;
+  return (f2){__builtin_fmaf(a.x, b.y, c.x), __builtin_fmaf(a.y, b.y, c.y)};
 }
 __device__ __forceinline__ f2 fma2_lo_u(f2 a, f2 b, f2 c) {
   f2 r;
   asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
-__device__ __forceinline__ f2 fma2_hi_u(f2 a, f2 b, f2 c) {
-  f2 r;
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
-      : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
+__device__ __forceinline__ f2 fma2_hi_u(f2 a, f2 b, f2 c) { return fma2_hi(a, b, c); }
 __device__ __forceinline__ f2 mul2_lo(f2 a, f2 b) {
   f2 r;
   asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
-__device__ __forceinline__ f2 mul2_hi(f2 a, f2 b) {
-  f2 r;
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
+__device__ __forceinline__ f2 mul2_hi(f2 a, f2 b) { return (f2){a.x * b.y, a.y * b.y}; }
 // the first FMA of a score chain: a * {b.x, b.x} + {c_H, c_H}, c = a pair of key biases
-// (H = 0: its first key, 1: its second) read straight out of the pair -- no register
-// copies to broadcast the bias into a fresh accumulator pair
+// (H = 0: its first key, read with op_sel_hi; 1: its second, two scalar FMAs)
 template <int H>
 __device__ __forceinline__ f2 fma2_bias(f2 a, f2 b, f2 c) {
-  f2 r;
-  if (H == 0)
+  if (H == 0) {
+    f2 r;
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  else
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]"
-        : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+    return r;
+  }
+  return (f2){__builtin_fmaf(a.x, b.x, c.y), __builtin_fmaf(a.y, b.x, c.y)};
 }
-// Two dh-8 score chains (bias + q . k, the first FMA reading its key bias out of the pair,
-// as fma2_bias) interleaved in ONE asm statement.  Consecutive dependent v_pk_fma_f32 need
-// one wait state on gfx950, and hipcc pads every asm-to-asm dependence it cannot see
-// through (it counts an asm statement as zero wait states): as one statement per FMA the
-// forward's 8-key trip carried 39 `s_nop 0` (4 cycles each).  Interleaved, each chain's
-// next FMA is two instructions after its last, which is the wait state; the statement
-// boundary costs at most one pad.
-#define VAESNE_QK_BIAS0(o, q, k, kb) "v_pk_fma_f32 %" #o ", %" #q ", %" #k ", %" #kb " op_sel_hi:[1,0,0]\n"
-#define VAESNE_QK_BIAS1(o, q, k, kb) \
-  "v_pk_fma_f32 %" #o ", %" #q ", %" #k ", %" #kb " op_sel:[0,0,1] op_sel_hi:[1,0,1]\n"
-#define VAESNE_QK_TAIL                                                 \
-  "v_pk_fma_f32 %0, %3, %18, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"   \
-  "v_pk_fma_f32 %1, %11, %22, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"  \
-  "v_pk_fma_f32 %0, %4, %19, %0 op_sel_hi:[1,0,1]\n"                  \
-  "v_pk_fma_f32 %1, %12, %23, %1 op_sel_hi:[1,0,1]\n"                 \
-  "v_pk_fma_f32 %0, %5, %19, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"   \
-  "v_pk_fma_f32 %1, %13, %23, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"  \
-  "v_pk_fma_f32 %0, %6, %20, %0 op_sel_hi:[1,0,1]\n"                  \
-  "v_pk_fma_f32 %1, %14, %24, %1 op_sel_hi:[1,0,1]\n"                 \
-  "v_pk_fma_f32 %0, %7, %20, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"   \
-  "v_pk_fma_f32 %1, %15, %24, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"  \
-  "v_pk_fma_f32 %0, %8, %21, %0 op_sel_hi:[1,0,1]\n"                  \
-  "v_pk_fma_f32 %1, %16, %25, %1 op_sel_hi:[1,0,1]\n"                 \
-  "v_pk_fma_f32 %0, %9, %21, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"   \
-  "v_pk_fma_f32 %1, %17, %25, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
-#define VAESNE_QK_OPERANDS                                                                    \
-  : "=&v"(sa), "=&v"(sb)                                                                      \
-  : "v"(qa[0]), "v"(qa[1]), "v"(qa[2]), "v"(qa[3]), "v"(qa[4]), "v"(qa[5]), "v"(qa[6]),       \
-    "v"(qa[7]), "v"(qb[0]), "v"(qb[1]), "v"(qb[2]), "v"(qb[3]), "v"(qb[4]), "v"(qb[5]),       \
-    "v"(qb[6]), "v"(qb[7]), "v"(kra[0]), "v"(kra[1]), "v"(kra[2]), "v"(kra[3]),               \
-    "v"(krb[0]), "v"(krb[1]), "v"(krb[2]), "v"(krb[3]), "v"(kba), "v"(kbb)
-template <int HA, int HB>
-__device__ __forceinline__ void qk_chains2(const f2 (&qa)[8], const f2 (&kra)[4], f2 kba,
-                                           const f2 (&qb)[8], const f2 (&krb)[4], f2 kbb,
-                                           f2& sa, f2& sb) {
-  if constexpr (HA == 0 && HB == 0)
-    asm(VAESNE_QK_BIAS0(0, 2, 18, 26) VAESNE_QK_BIAS0(1, 10, 22, 27) VAESNE_QK_TAIL VAESNE_QK_OPERANDS);
-  else if constexpr (HA == 0)
-    asm(VAESNE_QK_BIAS0(0, 2, 18, 26) VAESNE_QK_BIAS1(1, 10, 22, 27) VAESNE_QK_TAIL VAESNE_QK_OPERANDS);
-  else if constexpr (HB == 0)
-    asm(VAESNE_QK_BIAS1(0, 2, 18, 26) VAESNE_QK_BIAS0(1, 10, 22, 27) VAESNE_QK_TAIL VAESNE_QK_OPERANDS);
-  else
-    asm(VAESNE_QK_BIAS1(0, 2, 18, 26) VAESNE_QK_BIAS1(1, 10, 22, 27) VAESNE_QK_TAIL VAESNE_QK_OPERANDS);
-}
-#undef VAESNE_QK_BIAS0
-#undef VAESNE_QK_BIAS1
-#undef VAESNE_QK_TAIL
-#undef VAESNE_QK_OPERANDS
-
 template <int DH>
 __device__ __forceinline__ f2 fma2r(f2 a, const f2 (&r)[DH / 2], int d, f2 c) {
   return (d & 1) ? fma2_hi(a, r[d >> 1], c) : fma2_lo(a, r[d >> 1], c);
@@ -170,6 +113,20 @@ __device__ __forceinline__ f2 fma2r(f2 a, const f2 (&r)[DH / 2], int d, f2 c) {
 template <int DH>
 __device__ __forceinline__ f2 fma2ru(f2 a, const f2 (&r)[DH / 2], int d, f2 c) {
   return (d & 1) ? fma2_hi_u(a, r[d >> 1], c) : fma2_lo_u(a, r[d >> 1], c);
+}
+// Two dh-8 score chains (bias + q . k) of one or two query pairs, interleaved so each
+// chain's next FMA is not right behind its last (hipcc pads what remains)
+template <int HA, int HB>
+__device__ __forceinline__ void qk_chains2(const f2 (&qa)[8], const f2 (&kra)[4], f2 kba,
+                                           const f2 (&qb)[8], const f2 (&krb)[4], f2 kbb,
+                                           f2& sa, f2& sb) {
+  sa = fma2_bias<HA>(qa[0], kra[0], kba);
+  sb = fma2_bias<HB>(qb[0], krb[0], kbb);
+#pragma unroll
+  for (int d = 1; d < 8; ++d) {
+    sa = fma2r<8>(qa[d], kra, d, sa);
+    sb = fma2r<8>(qb[d], krb, d, sb);
+  }
 }
 // broadcast read of one LDS row as register pairs
 template <int DH>
@@ -183,111 +140,42 @@ __device__ __forceinline__ void lrow2(const float* s, f2 (&r)[DH / 2]) {
 }
 
 // The fused backward's two chains of one (query, key pair): s = kbias + k . q (scores,
-// log2 domain) and g = v . dO, interleaved in ONE asm statement (see qk_chains2: as
-// separate statements hipcc padded each step, 30 `s_nop 0` per two-query trip).
-// %0 s, %1 g, %2-%9 k[0..7], %10-%17 v[0..7], %18-%21 q row, %22-%25 dO row, %26 kbias
+// log2 domain) and g = v . dO
 __device__ __forceinline__ void sg_chains(const f2 (&k)[8], const f2 (&v)[8], const f2 (&qr)[4],
                                           const f2 (&dr)[4], f2 kb, f2& s, f2& g) {
-  asm("v_pk_fma_f32 %0, %2, %18, %26 op_sel_hi:[1,0,1]\n"
-      "v_pk_mul_f32 %1, %10, %22 op_sel_hi:[1,0]\n"
-      "v_pk_fma_f32 %0, %3, %18, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %1, %11, %22, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %0, %4, %19, %0 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %1, %12, %23, %1 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %0, %5, %19, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %1, %13, %23, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %0, %6, %20, %0 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %1, %14, %24, %1 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %0, %7, %20, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %1, %15, %24, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %0, %8, %21, %0 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %1, %16, %25, %1 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %0, %9, %21, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %1, %17, %25, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
-      : "=&v"(s), "=&v"(g)
-      : "v"(k[0]), "v"(k[1]), "v"(k[2]), "v"(k[3]), "v"(k[4]), "v"(k[5]), "v"(k[6]), "v"(k[7]),
-        "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
-        "v"(qr[0]), "v"(qr[1]), "v"(qr[2]), "v"(qr[3]), "v"(dr[0]), "v"(dr[1]), "v"(dr[2]),
-        "v"(dr[3]), "v"(kb));
+  s = fma2_lo_u(k[0], qr[0], kb);
+  g = mul2_lo(v[0], dr[0]);
+#pragma unroll
+  for (int d = 1; d < 8; ++d) {
+    s = fma2r<8>(k[d], qr, d, s);
+    g = fma2r<8>(v[d], dr, d, g);
+  }
 }
 
 // The fused backward's accumulator updates of one (query, key pair): dV += aP dO and
-// dK += dS q over the 8 features, one statement (no pads between the 16 FMAs).
-// %0-%7 dv, %8-%15 dk, %16 aP, %17 dS, %18-%21 dO row, %22-%25 q row
+// dK += dS q over the 8 features
 __device__ __forceinline__ void dvdk_update(f2 (&dv)[8], f2 (&dk)[8], f2 aP, f2 dS,
                                             const f2 (&dr)[4], const f2 (&qr)[4]) {
-  asm(
-      "v_pk_fma_f32 %0, %16, %18, %0 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %8, %17, %22, %8 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %1, %16, %18, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %9, %17, %22, %9 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %2, %16, %19, %2 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %10, %17, %23, %10 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %3, %16, %19, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %11, %17, %23, %11 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %4, %16, %20, %4 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %12, %17, %24, %12 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %5, %16, %20, %5 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %13, %17, %24, %13 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %6, %16, %21, %6 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %14, %17, %25, %14 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %7, %16, %21, %7 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %15, %17, %25, %15 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
-      : "+v"(dv[0]), "+v"(dv[1]), "+v"(dv[2]), "+v"(dv[3]), "+v"(dv[4]), "+v"(dv[5]), "+v"(dv[6]),
-        "+v"(dv[7]), "+v"(dk[0]), "+v"(dk[1]), "+v"(dk[2]), "+v"(dk[3]), "+v"(dk[4]), "+v"(dk[5]),
-        "+v"(dk[6]), "+v"(dk[7])
-      : "v"(aP), "v"(dS), "v"(dr[0]), "v"(dr[1]), "v"(dr[2]), "v"(dr[3]), "v"(qr[0]), "v"(qr[1]),
-        "v"(qr[2]), "v"(qr[3]));
+#pragma unroll
+  for (int d = 0; d < 8; ++d) {
+    dv[d] = fma2r<8>(aP, dr, d, dv[d]);
+    dk[d] = fma2r<8>(dS, qr, d, dk[d]);
+  }
 }
 
 // The fused dQ's per-feature key sums of two queries over the lane's two key pairs (NP 2):
-// F[d] = sx0 k0[d].x + sy0 k0[d].y + sx1 k1[d].x + sy1 k1[d].y, as one statement whose four
-// passes over d keep each F[d]'s dependent FMAs eight instructions apart.
-// %0-%7 F, %8 sx0, %9 sy0, %10 sx1, %11 sy1, %12-%19 k0[0..7], %20-%27 k1[0..7]
-#define VAESNE_DQ_PASS(op, mod, s, kb)                                                       \
-  op " %0, %" #s ", %" #kb "0" mod "\n" op " %1, %" #s ", %" #kb "1" mod "\n"                \
-  op " %2, %" #s ", %" #kb "2" mod "\n" op " %3, %" #s ", %" #kb "3" mod "\n"
+// F[d] = sx0 k0[d].x + sy0 k0[d].y + sx1 k1[d].x + sy1 k1[d].y
 __device__ __forceinline__ void dq_sums(f2 sx0, f2 sy0, f2 sx1, f2 sy1, const f2 (&k0)[8],
                                         const f2 (&k1)[8], f2 (&F)[8]) {
-  asm("v_pk_mul_f32 %0, %8, %12 op_sel_hi:[1,0]\n"
-      "v_pk_mul_f32 %1, %8, %13 op_sel_hi:[1,0]\n"
-      "v_pk_mul_f32 %2, %8, %14 op_sel_hi:[1,0]\n"
-      "v_pk_mul_f32 %3, %8, %15 op_sel_hi:[1,0]\n"
-      "v_pk_mul_f32 %4, %8, %16 op_sel_hi:[1,0]\n"
-      "v_pk_mul_f32 %5, %8, %17 op_sel_hi:[1,0]\n"
-      "v_pk_mul_f32 %6, %8, %18 op_sel_hi:[1,0]\n"
-      "v_pk_mul_f32 %7, %8, %19 op_sel_hi:[1,0]\n"
-      "v_pk_fma_f32 %0, %9, %12, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %1, %9, %13, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %2, %9, %14, %2 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %3, %9, %15, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %4, %9, %16, %4 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %5, %9, %17, %5 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %6, %9, %18, %6 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %7, %9, %19, %7 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %0, %10, %20, %0 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %1, %10, %21, %1 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %2, %10, %22, %2 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %3, %10, %23, %3 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %4, %10, %24, %4 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %5, %10, %25, %5 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %6, %10, %26, %6 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %7, %10, %27, %7 op_sel_hi:[1,0,1]\n"
-      "v_pk_fma_f32 %0, %11, %20, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %1, %11, %21, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %2, %11, %22, %2 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %3, %11, %23, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %4, %11, %24, %4 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %5, %11, %25, %5 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %6, %11, %26, %6 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n"
-      "v_pk_fma_f32 %7, %11, %27, %7 op_sel:[0,1,0] op_sel_hi:[1,1,1]"
-      : "=&v"(F[0]), "=&v"(F[1]), "=&v"(F[2]), "=&v"(F[3]), "=&v"(F[4]), "=&v"(F[5]),
-        "=&v"(F[6]), "=&v"(F[7])
-      : "v"(sx0), "v"(sy0), "v"(sx1), "v"(sy1), "v"(k0[0]), "v"(k0[1]), "v"(k0[2]), "v"(k0[3]),
-        "v"(k0[4]), "v"(k0[5]), "v"(k0[6]), "v"(k0[7]), "v"(k1[0]), "v"(k1[1]), "v"(k1[2]),
-        "v"(k1[3]), "v"(k1[4]), "v"(k1[5]), "v"(k1[6]), "v"(k1[7]));
+#pragma unroll
+  for (int d = 0; d < 8; ++d) F[d] = mul2_lo(sx0, k0[d]);
+#pragma unroll
+  for (int d = 0; d < 8; ++d) F[d] = fma2_hi(sy0, k0[d], F[d]);
+#pragma unroll
+  for (int d = 0; d < 8; ++d) F[d] = fma2_lo(sx1, k1[d], F[d]);
+#pragma unroll
+  for (int d = 0; d < 8; ++d) F[d] = fma2_hi(sy1, k1[d], F[d]);
 }
-#undef VAESNE_DQ_PASS
 
 // s[p][u] = kb[u] + q[p] . k[u] for the 8 keys of a group, x[p] = max(x[p], s[p][.]).
 // dh 8: two chains per asm statement (qk_chains2): the two query pairs of one key (NP 2),
@@ -1808,19 +1696,14 @@ void launch_sum_chunks(const float* ws, int64_t ss, int n, int B, int L, int E, 
 
 // the split-f16 matrix-core kernels (attention_sf16.hip) for head_dim 8 unless a test forces
 // a packed-VALU geometry
-bool use_sf16(int dh, int64_t bh, int Lq, int Lk, bool bwd) {
-  static const int dbg_only = [] { const char* e = getenv("SF16_DBG_ONLY_L"); return e ? atoi(e) : 0; }();
-  static const int dbg_f = [] { const char* e = getenv("SF16_DBG_FWD"); return e ? atoi(e) : 1; }();
-  static const int dbg_b = [] { const char* e = getenv("SF16_DBG_BWD"); return e ? atoi(e) : 1; }();
-  if (dbg_only && Lq != dbg_only) return false;
-  if (bwd ? !dbg_b : !dbg_f) return false;
+bool use_sf16(int dh, int64_t bh, int Lq, int Lk) {
   return g_forced.nt == 0 && sf16_path(dh, bh, Lq, Lk);
 }
 
 // workspace of a split launch (bytes; 0 = no split for this shape)
 int64_t fwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sp) {
   sp = {1, Lk};
-  if (Lq <= 2 * SQ || use_sf16(dh, (int64_t)B * H, Lq, Lk, false)) return 0;
+  if (Lq <= 2 * SQ || use_sf16(dh, (int64_t)B * H, Lq, Lk)) return 0;
   sp = pick_split(waves_of((int64_t)B * H, Lq), Lk);
   if (sp.n <= 1) return 0;
   return (int64_t)sp.n * B * Lq * H * dh + (int64_t)sp.n * B * H * Lq * 2;
@@ -1843,7 +1726,7 @@ int64_t bwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sq, Split& sk
   sq = {1, Lk};   // dQ: key chunks
   sk = {1, Lq};   // dK/dV: query chunks
   if (Lq <= 2 * SQ) return 0;
-  if (use_sf16(dh, (int64_t)B * H, Lq, Lk, true)) return sf16_bwd_ws_floats(B, H, Lq, Lk);
+  if (use_sf16(dh, (int64_t)B * H, Lq, Lk)) return sf16_bwd_ws_floats(B, H, Lq, Lk);
   sq = pick_split(waves_of((int64_t)B * H, Lq), Lk);
   sk = pick_split(waves_of((int64_t)B * H, Lk), Lq);
   return bwd_dq_floats(B, H, Lq, Lk, dh, sq) +
@@ -1878,7 +1761,7 @@ int launch_fwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s) {
     VAESNE_CHECK_LAUNCH();
     return 0;
   }
-  if (use_sf16(DHV, (int64_t)a.B * a.H, a.Lq, a.Lk, false)) return sf16_fwd(a, p_drop, s);
+  if (use_sf16(DHV, (int64_t)a.B * a.H, a.Lq, a.Lk)) return sf16_fwd(a, p_drop, s);
   Split sp;
   const int64_t wsf = fwd_ws_floats(a.B, a.H, a.Lq, a.Lk, DHV, sp);
   AttnArgs c = a;
@@ -1924,7 +1807,7 @@ int launch_bwd(const AttnArgs& a, float p_drop, int part, float* ws, hipStream_t
     return 0;
   }
   // the split-f16 backward is one fused kernel: every part runs it whole
-  if (use_sf16(DHV, (int64_t)a.B * a.H, a.Lq, a.Lk, true)) return sf16_bwd(a, p_drop, ws, s);
+  if (use_sf16(DHV, (int64_t)a.B * a.H, a.Lq, a.Lk)) return sf16_bwd(a, p_drop, ws, s);
   Split sq, sk;
   const int64_t wsf = bwd_ws_floats(a.B, a.H, a.Lq, a.Lk, DHV, sq, sk);
   if (wsf == 0 || !ws) { sq = {1, a.Lk}; sk = {1, a.Lq}; }
