@@ -381,7 +381,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
 #pragma unroll
   for (int tt = 0; tt < BKT; ++tt) {
     Kop[tt] = (u4){0u, 0u, 0u, 0u};
-    if (tt < ntile) {
+    {   // every tile, past-Lk keys too (zero K / V, bias -inf): no per-tile branch
       const int key = key0 + 16 * tt + c;
       const bool ok = key < a.Lk;
       const int64_t kc = min(key, a.Lk - 1);
@@ -457,7 +457,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
 #pragma unroll
   for (int tt = 0; tt < BKT; ++tt) {
     Vop[tt] = (u4){0u, 0u, 0u, 0u};
-    if (tt < ntile) {
+    {   // every tile, past-Lk keys too (zero K / V, bias -inf): no per-tile branch
       const int key = key0 + 16 * tt + c;
       const bool ok = key < a.Lk;
       const int64_t kc = min(key, a.Lk - 1);
@@ -572,7 +572,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
       const f4 CD = *reinterpret_cast<const f4*>(Cd_l + q0 + 4 * g);
 #pragma unroll
       for (int tt = 0; tt < BKT; ++tt) {
-        if (tt < ntile) {
+        {   // every tile, past-Lk keys too (zero K / V, bias -inf): no per-tile branch
           const f4 S = mma(QA, Kop[tt], CS);
           const f4 dP = mma(DA, Vop[tt], CD);
           float P[4], Pd[4], dS[4];
@@ -582,7 +582,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
             if (DROP) {
               const uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe((int)kw[r], 4 * tt + (c & 3), 1);
               Pd[r] = __uint_as_float(as_u(P[r]) & mk);
-              const float tq = __uint_as_float((as_u(dP[r]) & mk) | (as_u(CD[r]) & ~mk));
+              const float tq = __uint_as_float(as_u(CD[r]) ^ ((as_u(CD[r]) ^ as_u(dP[r])) & mk));
               dS[r] = P[r] * tq;
             } else {
               Pd[r] = P[r];
@@ -605,8 +605,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
           const int R = 4 * (c >> 1) + (c & 1);
           *reinterpret_cast<uint2*>(sc + R * 8 + 2 * g) = make_uint2(Bk[0], Bk[2]);
           *reinterpret_cast<uint2*>(sc + (R + 2) * 8 + 2 * g) = make_uint2(Bk[1], Bk[3]);
-          // the other lanes' rows must have landed before the transposed reads gather them
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          // (the wave's LDS operations complete in order: the transposed reads see these rows)
           // B[slot 8g + j][query c] = row 8g + j: two 4-row transposed reads
           const int rq = (c >> 2), cp = (c & 3);
           const s4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
