@@ -323,6 +323,15 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_sf16_kernel(AttnArgs a, int N
 constexpr int BNW_MAX = 8;
 constexpr int BKT = 8;             // key tiles per wave
 constexpr int BLQ_MAX = 2048;      // queries of the prologue arrays
+// dS'' transpose image: 32 rows of 4 eight-byte chunks (16 queries as f16); chunk j of row r
+// at dword sc_at(r, j).  Rows padded 16 dwords per 4 and chunks XOR-swizzled per 8 rows:
+// the writes (ds_write_b64, 16-lane groups, 32 banks) and the transposed reads
+// (ds_read_b64_tr_b16, 32-lane halves, 64 banks) are both conflict-free (plain 8-dword rows
+// were 8-way / 2-way: SQ_LDS_BANK_CONFLICT 27 % of the wave cycles)
+constexpr int SC_WORDS = 368;
+__device__ __forceinline__ int sc_at(int r, int j) {
+  return r * 8 + 2 * (j ^ ((r >> 3) & 3)) + 16 * (r >> 2);
+}
 
 template <bool DROP>
 __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int nkb, int NT8, int Lqp) {
@@ -335,7 +344,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
   __shared__ __attribute__((aligned(16))) uint32_t Da[2][16 * 12];
   __shared__ __attribute__((aligned(16))) uint32_t QT[2][256];
   __shared__ __attribute__((aligned(16))) uint32_t DT[2][256];
-  __shared__ __attribute__((aligned(16))) uint32_t Sc[BNW_MAX][2][256];    // dS'' transposes
+  __shared__ __attribute__((aligned(16))) uint32_t Sc[BNW_MAX][2][SC_WORDS];   // dS'' transposes
   __shared__ __attribute__((aligned(16))) float Qp[2][BNW_MAX * 128];      // dQ partials
   __shared__ float Red[3][BNW_MAX];
   const int NW = blockDim.x >> 6, KB = 128 * NW;
@@ -603,15 +612,15 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
           // dS'' through LDS: row R = 4 (c/2) + 2 prec + c%2 holds queries 0..15 (32 B)
           uint32_t* sc = Sc[w][tt & 1];
           const int R = 4 * (c >> 1) + (c & 1);
-          *reinterpret_cast<uint2*>(sc + R * 8 + 2 * g) = make_uint2(Bk[0], Bk[2]);
-          *reinterpret_cast<uint2*>(sc + (R + 2) * 8 + 2 * g) = make_uint2(Bk[1], Bk[3]);
+          *reinterpret_cast<uint2*>(sc + sc_at(R, g)) = make_uint2(Bk[0], Bk[2]);
+          *reinterpret_cast<uint2*>(sc + sc_at(R + 2, g)) = make_uint2(Bk[1], Bk[3]);
           // (the wave's LDS operations complete in order: the transposed reads see these rows)
           // B[slot 8g + j][query c] = row 8g + j: two 4-row transposed reads
           const int rq = (c >> 2), cp = (c & 3);
           const s4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s4*)(sc + (8 * g + rq) * 8 + 2 * cp));
+              (__attribute__((address_space(3))) s4*)(sc + sc_at(8 * g + rq, cp)));
           const s4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s4*)(sc + (8 * g + 4 + rq) * 8 + 2 * cp));
+              (__attribute__((address_space(3))) s4*)(sc + sc_at(8 * g + 4 + rq, cp)));
           const u4 Bq = {__builtin_bit_cast(uint2, r0).x, __builtin_bit_cast(uint2, r0).y,
                          __builtin_bit_cast(uint2, r1).x, __builtin_bit_cast(uint2, r1).y};
           const u4 KA = ldu4(KTi + (w * BKT + tt) * 256 + c * 16 + 4 * g);
