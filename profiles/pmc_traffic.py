@@ -11,7 +11,8 @@ import os
 import re
 import sys
 
-KERNELS = ("attn_fwd_kernel", "attn_bwd_kv_kernel", "attn_fwd_mfma_kernel", "attn_bwd_mfma_kernel")
+KERNELS = ("attn_fwd_kernel", "attn_bwd_kv_kernel", "attn_fwd_mfma_kernel", "attn_bwd_mfma_kernel",
+           "attn_fwd_sf16_kernel", "attn_bwd_sf16_kernel")
 
 
 def per_kernel(path, counter):
@@ -19,9 +20,11 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = re.sub(r"^void ", "", r["Kernel_Name"].replace("(anonymous namespace)::", ""))
+        name = re.sub(r"^void ", "", r["Kernel_Name"].replace("(anonymous namespace)::", "")
+                      .replace("vaesne::", ""))
         name = name.split("(")[0]
-        if name.startswith(KERNELS) and ("<8, 256, 2, true" in name or "_mfma_kernel<true" in name):
+        if name.startswith(KERNELS) and ("<8, 256, 2, true" in name or "_mfma_kernel<true" in name
+                                         or "_sf16_kernel<true>" in name):
             vals[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 

@@ -18,6 +18,10 @@ KERNELS = {
     "attn_fwd_kernel": ("attn_fwd_kernel<8, 256, 2, true, false>", N * H * 256),
     "attn_fwd_mfma_kernel": ("attn_fwd_mfma_kernel<true, 4, false>", N * H * 4 * 256),
     "attn_bwd_mfma_kernel": ("attn_bwd_mfma_kernel<true, 4, 0>", N * H * 4 * 256),
+    # the split-f16 kernels (r05): backward one 512-thread block (8 waves x 128 keys) per
+    # (sequence, head); forward one 256-thread block per 256 queries of it
+    "attn_bwd_sf16_kernel": ("attn_bwd_sf16_kernel<true>", N * H * 512),
+    "attn_fwd_sf16_kernel": ("attn_fwd_sf16_kernel<true>", N * H * 4 * 256),
 }
 
 
