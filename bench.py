@@ -427,10 +427,46 @@ def roofline(device, B, in_step=None):
                     "launch_ms = in-step HIP events (headline), launch_ms_isolated = the same "
                     "launch alone on a stream, ms_rocprof = the committed kernel-trace "
                     "average inside the captured step" % scores)
+    sp = softmax_peak(device, pd > 0)
+    if sp is not None:
+        f = res["fwd"]
+        ach = scores / (f.get("ms_in_step", f["ms"]) * 1e-3) / 1e9
+        out["softmax_frac"] = round(ach / sp, 4)
+        out["softmax"] = dict(kernel=f["kernel"], achieved=round(ach, 1), peak=round(sp, 1),
+                              unit="Gscores/s", frac=round(ach / sp, 4),
+                              peak_source="tools/probe/softmax_peak.hip: the forward's key loop "
+                                          "with every operand in registers (MFMAs, max test, "
+                                          "exp2, sums, dropout hash and keep bits, f16 split), "
+                                          "no LDS / HBM; achieved = scores per launch / the "
+                                          "forward's in-step launch time")
     if "ms_rocprof" in r:
         out["launch_ms_rocprof"] = round(r["ms_rocprof"], 4)
         out["frac_rocprof"] = round(r["tflops_rocprof"] / FP32_PEAK_TFLOPS, 4)
     return out
+
+
+def softmax_peak(device, drop, iters=1500):
+    """Score-processing peak (Gscores/s) of the split-f16 forward's key loop with its
+    operands in registers (tools/probe/softmax_peak.hip; SURVEY.md §8(d)'s softmax
+    roofline), or None when the microbench library is absent (build_lib.build_probes)."""
+    import ctypes
+    path = os.path.join(ROOT, "tools", "probe", "libsoftmax_peak.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.softmax_peak_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                        ctypes.c_void_p]
+    grid = 256 * 3 * 4            # 4 rounds of 3 workgroups (12 waves) per CU
+    out = torch.empty(grid * 256, device=device)
+
+    def fn():
+        rc = lib.softmax_peak_launch(grid, iters, int(drop), out.data_ptr(),
+                                     torch.cuda.current_stream(device).cuda_stream)
+        assert rc == 0, rc
+
+    t = time_kernel(fn, 5, device)
+    assert torch.isfinite(out).all()
+    return grid * 4 * iters * 2048 / t / 1e9
 
 
 def attn_bwd_algorithmic_bytes(N, H, L, dh, p):

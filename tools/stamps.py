@@ -3,7 +3,7 @@
 node at each phase boundary, replayed, and the stamps of the last replay are printed
 in microseconds from the step's first stamp.  rocprofv3's kernel trace stretches the
 latency-bound encoder phases with its per-dispatch cost; these nodes cost ~2 us each.
-    VAESNE_STAMPS=1 python tools/stamps.py [--steps N]"""
+    VAESNE_STAMPS=1 python tools/stamps.py [--steps N] [--batch B]"""
 import argparse
 import os
 import sys
@@ -19,12 +19,13 @@ import bench  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=16, help="SN pairs per step (2: the DP script's per-GPU batch at 8 GPUs)")
     args = ap.parse_args()
     from VAESNe import _stamps
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     model = bench.make_model(dev, bench.CFG["dropout"])
-    x = bench.synthetic_batch(16, 1234, dev)
+    x = bench.synthetic_batch(args.batch, 1234, dev)
     st = bench.Step(model, x, dev, 1, True)
     st.capture()
     runs = []

@@ -122,5 +122,28 @@ def build_variant(out, src_name, defines):
     return out
 
 
+PROBE_DIR = os.path.join(ROOT, "tools", "probe")
+# measurement microbenches bench.py loads (not the product): source -> library
+PROBES = {"softmax_peak.hip": "libsoftmax_peak.so"}
+
+
+def build_probes(verbose=True):
+    """The measurement microbenches (tools/probe/softmax_peak.hip: the forward's
+    score-processing peak, bench.py's softmax_frac), built like attention_sf16.hip."""
+    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + [os.path.abspath(__file__)]
+    for src, lib in PROBES.items():
+        src, lib = os.path.join(PROBE_DIR, src), os.path.join(PROBE_DIR, lib)
+        if os.path.exists(lib) and os.path.getmtime(lib) >= max(os.path.getmtime(p) for p in [src] + hdrs):
+            continue
+        cmd = [HIPCC, "-shared", *CFLAGS, *NO_PACKED_FP32, "-o", lib + ".tmp", src]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+        os.replace(lib + ".tmp", lib)
+        if verbose:
+            print(f"[vaesne] built {lib}")
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_probes()
