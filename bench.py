@@ -884,7 +884,7 @@ def config_cpu_baselines():
 ALLREDUCE_MS_ASSUMED = 0.06   # 0.88 MB ring all-reduce over 8 GPUs' xGMI: latency-bound
 
 
-def training_step_script(device, batches=8):
+def training_step_script(device, batches=32):
     """What the script runs, literally (cannon/ZTF_photospect.py:76,119-128):
     training_step(model, torch.optim.AdamW, DataLoader(multimodalDataset(...), 16),
     m_iwae K=8, multimodal=True) with HOST-resident batches (H2D copies, the loss read

@@ -154,7 +154,7 @@ class TorchAdamWUpdater(Updater):
             return
         groups = self.opt.param_groups
         ps, gs, ms, vs, ns, sets = [], [], [], [], [], []
-        coefs, set_of, stepped = [], {}, []
+        coefs, set_of, stepped, steps = [], {}, [], []
         for gi, p, g in batch:
             st = self.opt.state[p]
             created = len(st) == 0
@@ -162,9 +162,14 @@ class TorchAdamWUpdater(Updater):
                 st["step"] = torch.tensor(0.0, dtype=torch.float32)
                 st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-            st["step"] += 1
+            steps.append(st["step"])
             stepped.append((p, created))
-            step = float(st["step"])
+        # every step count += 1 and read back in three host ops, not two per parameter (the
+        # per-tensor add and item() were most of the loop's host time at small batches)
+        torch._foreach_add_(steps, 1.0)
+        step_vals = torch.stack(steps).tolist()
+        for (gi, p, g), step in zip(batch, step_vals):
+            st = self.opt.state[p]
             key = (gi, step)
             k = set_of.get(key)
             if k is None:

@@ -674,9 +674,17 @@ __global__ void sf16_dq_sum_kernel(const float* __restrict__ ws, int64_t ss, int
 }
 
 int fwd_waves(int Lq) { return Lq <= 64 ? 1 : (Lq <= 128 ? 2 : 4); }
-int bwd_waves(int Lk) { return std::min(BNW_MAX, (Lk + 127) / 128); }
-int bwd_blocks(int Lk) {
-  const int nw = bwd_waves(Lk);
+// waves (128 keys each) per backward workgroup: the whole key axis in one workgroup of up
+// to 8 waves, unless (sequence, head) pairs are too few to give every CU a workgroup -- small
+// batches (B = 2: 128 decoder pairs) and the encoders' context attention (64 pairs) -- then
+// halved (down to 2) until they do, the key blocks' dQ partials summed after the launch
+int bwd_waves(int Lk, int64_t bh) {
+  int nw = std::min(BNW_MAX, (Lk + 127) / 128);
+  while (nw > 2 && bh * ((Lk + 128 * nw - 1) / (128 * nw)) < 256) nw = (nw + 1) / 2;
+  return nw;
+}
+int bwd_blocks(int Lk, int64_t bh) {
+  const int nw = bwd_waves(Lk, bh);
   return (Lk + 128 * nw - 1) / (128 * nw);
 }
 int lq_pad(int Lq) { return (Lq + 15) & ~15; }
@@ -693,7 +701,7 @@ int64_t sf16_bits_bytes(int B, int H, int Lq, int Lk) {
 }
 
 int64_t sf16_bwd_ws_floats(int B, int H, int Lq, int Lk) {
-  const int nkb = bwd_blocks(Lk);
+  const int nkb = bwd_blocks(Lk, (int64_t)B * H);
   return nkb > 1 ? (int64_t)nkb * B * Lq * H * 8 : 0;
 }
 
@@ -710,8 +718,8 @@ int sf16_fwd(const AttnArgs& a, float p_drop, hipStream_t s) {
 }
 
 int sf16_bwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s) {
-  const int nw = bwd_waves(a.Lk), nkb = bwd_blocks(a.Lk);
   const int64_t bh = (int64_t)a.B * a.H;
+  const int nw = bwd_waves(a.Lk, bh), nkb = bwd_blocks(a.Lk, bh);
   const int E = a.H * 8;
   AttnArgs c = a;
   if (nkb > 1) {

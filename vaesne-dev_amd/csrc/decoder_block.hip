@@ -1639,10 +1639,24 @@ int dispatch_fused(const Tail& a, int grid, hipStream_t s) {
 // long sequences take the fused backward (vaesne_dec_tail_force_path(2): the two-kernel
 // path; force_path(1): fused always)
 int g_tail_path = 0;
-bool use_fused(int L) {
+bool use_fused(int L, int nseq) {
   if (g_tail_path == 1) return true;
   if (g_tail_path == 2) return false;
-  return L >= 256;
+  // one workgroup per sequence: only when the sequences alone fill half the chip (the
+  // fused kernel runs a whole 982-token sequence serially: 0.22 ms at any batch); small
+  // batches take the two-kernel path over chunks (tail_chunk)
+  return L >= 256 && nseq >= 128;
+}
+
+// tokens per workgroup of the two-kernel path and the forward: short sequences whole
+// (rounded to 128); long ones in 512-token chunks, halved down to 128 while the grid
+// would stay under one workgroup per CU (small batches: B = 2 -> 32 sequences x 8 chunks)
+int tail_chunk(int M, int L) {
+  if (L <= 256) return ((L + 127) / 128) * 128;
+  const int64_t nseq = M / L;
+  for (int c = 512; c > 128; c >>= 1)
+    if (nseq * ((L + c - 1) / c) >= 256) return c;
+  return 128;
 }
 
 template <bool FWD>
@@ -1669,7 +1683,7 @@ Tail make(const float* x, const float* O, const float* ctx, int M, int L, int Lc
   a.p_drop = p_drop; a.thr = drop_thr16(p_drop);
   a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   a.rng = rng; a.call_id = call_id;
-  a.chunk = L <= 256 ? ((L + 127) / 128) * 128 : 512;
+  a.chunk = tail_chunk(M, L);
   return a;
 }
 
@@ -1688,7 +1702,7 @@ int64_t ctx_grad_floats(int M, int L, int Lc) {
 
 VAESNE_API int64_t vaesne_dec_tail_workspace(int M, int L, int Lc) {
   if (!shapes_ok(M, L, Lc)) return 0;
-  const int chunk = L <= 256 ? ((L + 127) / 128) * 128 : 512;
+  const int chunk = tail_chunk(M, L);
   const int chunks = (L + chunk - 1) / chunk;
   const int64_t G = (int64_t)(M / L) * chunks;
   return (G * WPART + (int64_t)NVEC * M * E + ctx_grad_floats(M, L, Lc)) * (int64_t)sizeof(float);
@@ -1724,7 +1738,7 @@ VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* 
   if (a.Wn && !dqkv) return (int)hipErrorInvalidValue;
   a.y = const_cast<float*>(y);
   a.dctx = dctx;
-  if (use_fused(L)) {   // one workgroup per sequence, no scratch
+  if (use_fused(L, M / L)) {   // one workgroup per sequence, no scratch
     const int nseq = M / L;
     a.wpart = workspace;
     int rc = dispatch_fused(a, nseq, s);
