@@ -337,17 +337,21 @@ template <bool DROP>
 __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int nkb, int NT8, int Lqp) {
   __shared__ __attribute__((aligned(16))) float Cs_l[BLQ_MAX];     // 14 - lse (-inf past Lq)
   __shared__ __attribute__((aligned(16))) float Cd_l[BLQ_MAX];     // D, then -2^s D
-  __shared__ __attribute__((aligned(16))) uint32_t KTi[BNW_MAX * BKT * 256];   // K^T A operands
+  // sized by the launch's wave count (bwd_lds_bytes): K^T A operands [NW][BKT][256], the
+  // dS'' transpose images [NW][2][SC_WORDS], the dQ partials [2][NW * 128] -- a key-split
+  // launch of 2 or 4 waves then leaves room for more workgroups per CU
+  extern __shared__ __attribute__((aligned(16))) uint32_t bwd_dyn[];
   // staged query tile: Q A operand [16][hi | lo | ones], dO' [16][hi | lo | 0], Q^T and
   // dO'^T A operands [16 rows][32 slots]
   __shared__ __attribute__((aligned(16))) uint32_t Qa[2][16 * 12];
   __shared__ __attribute__((aligned(16))) uint32_t Da[2][16 * 12];
   __shared__ __attribute__((aligned(16))) uint32_t QT[2][256];
   __shared__ __attribute__((aligned(16))) uint32_t DT[2][256];
-  __shared__ __attribute__((aligned(16))) uint32_t Sc[BNW_MAX][2][SC_WORDS];   // dS'' transposes
-  __shared__ __attribute__((aligned(16))) float Qp[2][BNW_MAX * 128];      // dQ partials
   __shared__ float Red[3][BNW_MAX];
   const int NW = blockDim.x >> 6, KB = 128 * NW;
+  uint32_t* const KTi = bwd_dyn;
+  uint32_t* const Sc = bwd_dyn + NW * BKT * 256;
+  float* const Qp = reinterpret_cast<float*>(Sc + NW * 2 * SC_WORDS);
   const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, c = l & 15;
   const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
   const int kb = wg % nkb, bh = wg / nkb;
@@ -557,7 +561,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
     for (int i0 = t; i0 < 128; i0 += blockDim.x) {
       const int qq = i0 >> 3, f = i0 & 7;
       float acc = 0.f;
-      for (int i = 0; i < NW; ++i) acc += Qp[buf][i * 128 + qq * 8 + f];
+      for (int i = 0; i < NW; ++i) acc += Qp[buf * NW * 128 + i * 128 + qq * 8 + f];
       if (q0 + qq < a.Lq) dqb[(int64_t)(q0 + qq) * a.dq_ls + f] = acc * uq;
     }
   };
@@ -610,7 +614,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
           dV[tt] = mma(DTA, Bv, dV[tt]);
           dK[tt] = mma(QTA, Bk, dK[tt]);
           // dS'' through LDS: row R = 4 (c/2) + 2 prec + c%2 holds queries 0..15 (32 B)
-          uint32_t* sc = Sc[w][tt & 1];
+          uint32_t* sc = Sc + (w * 2 + (tt & 1)) * SC_WORDS;
           const int R = 4 * (c >> 1) + (c & 1);
           *reinterpret_cast<uint2*>(sc + sc_at(R, g)) = make_uint2(Bk[0], Bk[2]);
           *reinterpret_cast<uint2*>(sc + sc_at(R + 2, g)) = make_uint2(Bk[1], Bk[3]);
@@ -632,7 +636,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
     f4 dq;
 #pragma unroll
     for (int r = 0; r < 4; ++r) dq[r] = xsum32(dQa[r]);
-    if (g < 2) *reinterpret_cast<f4*>(Qp[buf] + w * 128 + c * 8 + 4 * g) = dq;
+    if (g < 2) *reinterpret_cast<f4*>(Qp + buf * NW * 128 + w * 128 + c * 8 + 4 * g) = dq;
     if (it + 1 < nqt) commit(buf ^ 1);
     kw = kwn;
     __syncthreads();
@@ -688,6 +692,9 @@ int bwd_blocks(int Lk, int64_t bh) {
   return (Lk + 128 * nw - 1) / (128 * nw);
 }
 int lq_pad(int Lq) { return (Lq + 15) & ~15; }
+size_t bwd_lds_bytes(int nw) {
+  return (size_t)nw * (BKT * 256 + 2 * SC_WORDS + 2 * 128) * sizeof(uint32_t);
+}
 int nt8(int Lk) { return (Lk + 127) / 128; }
 
 }  // namespace
@@ -730,10 +737,20 @@ int sf16_bwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s) {
     c.dq_ss = (int64_t)a.B * a.Lq * E;
   }
   const dim3 grid((unsigned)(bh * nkb));
+  static const bool lds_ok = [] {     // dynamic LDS beyond 64 KB (8 waves: 95 KB)
+    const int mx = (int)bwd_lds_bytes(BNW_MAX);
+    return hipFuncSetAttribute((const void*)attn_bwd_sf16_kernel<true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, mx) == hipSuccess &&
+           hipFuncSetAttribute((const void*)attn_bwd_sf16_kernel<false>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, mx) == hipSuccess;
+  }();
+  if (!lds_ok) return (int)hipErrorInvalidConfiguration;
   if (p_drop > 0.f)
-    hipLaunchKernelGGL(attn_bwd_sf16_kernel<true>, grid, dim3(64 * nw), 0, s, c, nkb, nt8(a.Lk), lq_pad(a.Lq));
+    hipLaunchKernelGGL(attn_bwd_sf16_kernel<true>, grid, dim3(64 * nw), bwd_lds_bytes(nw), s, c, nkb,
+                       nt8(a.Lk), lq_pad(a.Lq));
   else
-    hipLaunchKernelGGL(attn_bwd_sf16_kernel<false>, grid, dim3(64 * nw), 0, s, c, nkb, nt8(a.Lk), lq_pad(a.Lq));
+    hipLaunchKernelGGL(attn_bwd_sf16_kernel<false>, grid, dim3(64 * nw), bwd_lds_bytes(nw), s, c, nkb,
+                       nt8(a.Lk), lq_pad(a.Lq));
   VAESNE_CHECK_LAUNCH();
   if (nkb > 1) {
     const int64_t n = (int64_t)a.B * a.Lq * E;
