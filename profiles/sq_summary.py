@@ -1,33 +1,43 @@
-"""Per-kernel SQ counter summary of profiles/sq_pass.sh / pmc_step.sh output:
-    python profiles/sq_summary.py [-k substr,substr] run_counter_collection.csv [...]"""
+"""Per-kernel SQ counter summary of the two roofline passes of profiles/sq_pass.sh
+(bench.py --roofline-only: the decoder-shape attention launches), the first section of a
+profile set's sq_counters.txt:
+    python profiles/sq_summary.py gpurun_out/pmc_sq1/run_counter_collection.csv \
+        gpurun_out/pmc_sq2/run_counter_collection.csv"""
 import collections
 import csv
 import sys
 
-agg = collections.defaultdict(lambda: collections.defaultdict(list))
-dur = collections.defaultdict(list)
-args = sys.argv[1:]
-keys = ("attn_fwd", "attn_bwd", "keep_bits")
-if args and args[0] == "-k":
-    keys = tuple(args[1].split(","))
-    args = args[2:]
-for path in args:
-    for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
-        agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-        dur[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-for name, cs in agg.items():
-    if not any(k in name for k in keys):
-        continue
-    avg = {k: sum(v) / len(v) for k, v in cs.items()}
-    print(f"{name}: {sum(dur[name]) / len(dur[name]):.1f} us avg over {len(dur[name])} rows")
-    for k in sorted(avg):
-        print(f"   {k:24s} {avg[k]:.4g}")
-    if "SQ_WAVE_CYCLES" in avg:
-        wc = avg["SQ_WAVE_CYCLES"]
-        for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_LDS",
+KERNELS = ("attn_fwd_sf16_kernel<true>", "attn_bwd_sf16_kernel<true>",
+           "attn_rep_fwd_kernel<8, 256, 1, 2, true>", "attn_rep_bwd_kernel<256, 1, 16>")
+
+
+def main(paths):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    rows = collections.Counter()
+    dur = collections.defaultdict(float)
+    for p in paths:
+        for r in csv.DictReader(open(p)):
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+            if not any(name.endswith(k) for k in KERNELS):
+                continue
+            agg[name][r["Counter_Name"]] += float(r["Counter_Value"])
+            if p == paths[0]:
+                rows[name] += 1
+                dur[name] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
+    print("# SQ counters, bench.py --roofline-only (decoder-shape launches), profiles/sq_pass.sh")
+    for k in sorted(agg, key=lambda k: KERNELS.index(next(x for x in KERNELS if k.endswith(x)))):
+        c = agg[k]
+        print(f"{k}: {dur[k] / max(rows[k], 1):.1f} us avg over {rows[k]} rows")
+        for n in sorted(c):
+            print(f"   {n:24s} {c[n]:.4g}")
+        wc = max(c["SQ_WAVE_CYCLES"], 1)
+        for n in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_LDS",
                   "SQ_ACTIVE_INST_VALU"):
-            if k in avg:
-                print(f"   {k} / WAVE_CYCLES = {avg[k] / wc:.3f}")
-    if "SQ_INSTS_VALU" in avg and "SQ_WAVES" in avg:
-        print(f"   VALU insts per wave = {avg['SQ_INSTS_VALU'] / avg['SQ_WAVES']:.0f}")
+            if n in c:
+                print(f"   {n} / WAVE_CYCLES = {c[n] / wc:.3f}")
+        if c.get("SQ_WAVES"):
+            print(f"   VALU insts per wave = {c['SQ_INSTS_VALU'] / c['SQ_WAVES']:.0f}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
