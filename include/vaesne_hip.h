@@ -126,7 +126,10 @@ int vaesne_reduce_partials(const float* partial, int G, int F, float* out0, floa
  * lse [B,H,Lq] (log2 domain) is saved for the backward.  dh in {8, 16}.
  * Dropout (p_drop > 0): the forward draws the keep mask from the counter RNG
  * and stores it in keep_bits (1 bit per score, vaesne_attn_keep_bits_size
- * bytes); the backward of the same shape reads it.
+ * bytes); the backward of the same shape reads it.  The bitmap is opaque: its
+ * word layout depends on the kernel family the shape takes (dh 8 with Lq > 16:
+ * the split-f16 matrix-core kernels; otherwise the packed-VALU ones),
+ * the keep decisions themselves do not.
  * workspace (may be null): vaesne_attn_workspace(..., bwd) bytes.  Shapes whose
  * grid cannot fill the chip (the encoder's 983-token context self-attention,
  * B*H = 64) then run as key / query chunks with a fixed-order combine. */
