@@ -3,7 +3,9 @@
 kernels on the expanded input (the reference computes every copy separately:
 SpectraVAE.py:189-192 expands z and the decoder embeds the expanded grid).
 
-* forward, same geometry: o, lse and the dropout keep bitmap bit for bit;
+* forward, same geometry: o, lse and the dropout keep bitmap bit for bit (here the
+  packed-VALU kernels under a forced geometry; the default split-f16 kernels in
+  tests/test_gpu_rep_sf16.py);
 * backward: d(qkv) equals the plain backward's gradients summed over the copies
   (summation order differs: max-abs-relative 1e-5), with and without dropout, for
   every kernel configuration, ragged copy batches (R % RC != 0), masked keys and
@@ -97,9 +99,12 @@ def test_rep_forward_bitwise_equals_plain_forward(fnp, frc, Bd, R, L, pm, p):
                                          (2, 19, 37, 0.0, 0.1), (2, 16, 300, 0.3, 0.0),
                                          (1, 3, 983, 0.05, 0.1)])
 def test_rep_backward_equals_summed_plain_backward(cfg, Bd, R, L, pm, p):
+    """the packed-VALU kernels (a forced geometry selects them on both paths; the default
+    split-f16 ones: tests/test_gpu_rep_sf16.py)"""
     from VAESNe import _lib, _ops, rng
     lib = _lib.lib
     assert lib.attn_rep_config(*cfg) == 0
+    assert lib.attn_force_geometry(256, 1) == 0
     try:
         qkv, kb, kb_full, qkv_full = _inputs(Bd, R, L, pm, 7 * L + R + cfg[1])
         g = torch.Generator(device=DEV).manual_seed(L + 3)
@@ -118,6 +123,7 @@ def test_rep_backward_equals_summed_plain_backward(cfg, Bd, R, L, pm, p):
         torch.cuda.synchronize()
     finally:
         lib.attn_rep_config(-1, 0, 0, 0, 0, 0, 0)
+        lib.attn_force_geometry(0, 0)
     (o0, d0), (o1, d1) = res
     assert _rel(o1, o0) < 1e-5     # plain launch may split the key axis (chunk combine)
     for sl in (slice(0, E), slice(E, 2 * E), slice(2 * E, 3 * E)):     # dQ, dK, dV

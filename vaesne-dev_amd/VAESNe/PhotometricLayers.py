@@ -93,7 +93,7 @@ class photometricTransformerEncoder(nn.Module):
         """forward as a generator (VAESNe._chain.drive): yields the fused latent chain's
         work item so several encoders' chains can share one launch."""
         if self.concat:
-            tok = self.LCfc(torch.cat([self.fluxfc(flux[:, :, None]),
+            tok = self.LCfc(_ops.cat([self.fluxfc(flux[:, :, None]),
                                        self.time_embd(time),
                                        _ops.embedding(band, self.bandembd.weight)], dim=-1))
         else:

@@ -40,7 +40,7 @@ class spectraTransformerDecoder(nn.Module):
         if prepared is None:
             prepared = self.prepare(wavelength, phase, mask, repeat, bottleneck.shape[1] + 1)
         x_res, x_qkv, x_out, rep, phase_embd, first = prepared
-        bottleneck = torch.cat([self.contextfc(bottleneck), phase_embd], dim=1)
+        bottleneck = _ops.cat([self.contextfc(bottleneck), phase_embd], dim=1)
         h = decoder_stack(self.transformerblocks, x_res, bottleneck, mask, x_qkv=x_qkv,
                           rep=rep, first=first)
         return self.get_flux(x_out, h).squeeze(-1)   # get_flux(x + h)
@@ -90,16 +90,16 @@ class spectraTransformerEncoder(nn.Module):
     def steps(self, wavelength, flux, phase, mask=None):
         """forward as a generator (VAESNe._chain.drive), see photometricTransformerEncoder."""
         if self.concat:
-            flux_embd = self.spectrafc(torch.cat([self.flux_embd(flux[:, :, None]),
+            flux_embd = self.spectrafc(_ops.cat([self.flux_embd(flux[:, :, None]),
                                                   self.wavelength_embd_layer(wavelength)], dim=-1))
         else:
             flux_embd = self.flux_embd(flux[:, :, None],
                                        base=self.wavelength_embd_layer(wavelength))
         phase_embd = self.phase_embd_layer(phase[:, None])
-        context = torch.cat([flux_embd, phase_embd], dim=1)
+        context = _ops.cat([flux_embd, phase_embd], dim=1)
         if mask is not None:
             # the phase token is never masked (SpectraLayers.py:129-131)
-            mask = torch.cat([mask, torch.zeros(mask.shape[0], 1, dtype=mask.dtype,
+            mask = _ops.cat([mask, torch.zeros(mask.shape[0], 1, dtype=mask.dtype,
                                                 device=mask.device)], dim=1)
         x = _ops.repeat_batch(self.initbottleneck, context.shape[0])
         x_res, x_qkv, x_out = _ops.fanout(x, 3)

@@ -68,6 +68,7 @@ SIGNATURES = {
     "vaesne_attn_rep_bwd": (I32, [P, I64, I64, P, I64, P, I64, I64, P, P, P, I32, I32, I32, I32, I32,
                                   F32, P, U32, P, P, P]),
     "vaesne_attn_rep_config": (I32, [I32, I32, I32, I32, I32, I32, I32]),
+    "vaesne_attn_rep_sf16_config": (I32, [I32, I32]),
     "vaesne_enc_block_fwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P]),
     "vaesne_enc_block_bwd": (I32, [I32, P, P, I32, PP, F32, P, U32, P, P, P, P, P, P, P, P, P,
                                    P]),
@@ -114,6 +115,7 @@ SIGNATURES = {
     "vaesne_stamp": (I32, [P, I32, P]),
     "vaesne_loss_stat": (I32, [P, F32, P, P, P]),
     "vaesne_pack": (I32, [PP, C.POINTER(I64), C.POINTER(I64), I32, P, I32, P]),
+    "vaesne_cat": (I32, [PP, C.POINTER(I64), I32, I64, P, P]),
 }
 
 # int-returning entry points whose result is a value, not a hipError_t

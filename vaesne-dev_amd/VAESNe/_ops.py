@@ -894,6 +894,57 @@ def posterior_rsample(loc, scale, K):
     return RsampleFn.apply(loc, scale, u, False), loc, scale
 
 
+def _cat_launch(xs, dim):
+    """torch.cat(xs, dim) of contiguous device tensors through vaesne_cat (aten's
+    concatenation kernels carry the packed-FP32 erratum form)."""
+    x0 = xs[0]
+    d = dim % x0.dim()
+    shape = list(x0.shape)
+    shape[d] = sum(x.shape[d] for x in xs)
+    out = torch.empty(shape, dtype=x0.dtype, device=x0.device)
+    outer = math.prod(x0.shape[:d])
+    es = x0.element_size()
+    widths = [math.prod(x.shape[d:]) * es for x in xs]
+    if out.numel():
+        rc = lib.cat(_lib.ptr_array(xs), (C.c_int64 * len(xs))(*widths), len(xs), outer,
+                     out.data_ptr(), stream())
+        if rc != 0:
+            raise RuntimeError(f"vaesne_cat failed ({rc})")
+    return out
+
+
+class CatFn(torch.autograd.Function):
+    """cat(xs, dim) on the HIP kernel; the backward hands each input its slice (a view,
+    as aten's cat backward)."""
+
+    @staticmethod
+    def forward(ctx, dim, *xs):
+        ctx.dim = dim
+        ctx.sizes = [x.shape[dim] for x in xs]
+        return _cat_launch(xs, dim)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (None, *g.split(ctx.sizes, dim=ctx.dim))
+
+
+def cat(xs, dim=0):
+    """torch.cat for the step's device tensors (same dtype, device and trailing shapes, at
+    most 4 of them); anything else goes to torch.cat."""
+    xs = list(xs)
+    ok = (1 <= len(xs) <= 4 and all(x.is_cuda for x in xs)
+          and all(x.dtype == xs[0].dtype and x.dim() == xs[0].dim() for x in xs))
+    if ok:
+        d = dim % xs[0].dim()
+        ok = all(x.shape[:d] == xs[0].shape[:d] and x.shape[d + 1:] == xs[0].shape[d + 1:] for x in xs)
+    if not ok:
+        return torch.cat(xs, dim)
+    xs = [x.contiguous() for x in xs]
+    if torch.is_grad_enabled() and any(x.requires_grad for x in xs):
+        return CatFn.apply(d, *xs)
+    return _cat_launch(xs, d)
+
+
 class LatentCatFn(torch.autograd.Function):
     """zcat = cat(zs, dim 1) for `readers` consumers (one alias each) plus aliases of the
     zs themselves (the loss reads them): the backward sums every reader's gradient slice
@@ -905,7 +956,7 @@ class LatentCatFn(torch.autograd.Function):
         _lib.require_device(*zs)
         ctx.G, ctx.readers = len(zs), readers
         ctx.shape = zs[0].shape
-        zcat = torch.cat(zs, dim=1)
+        zcat = _cat_launch([z.contiguous() for z in zs], 1)
         return (*(zcat.view_as(zcat) for _ in range(readers)), *(z.view_as(z) for z in zs))
 
     @staticmethod
@@ -928,7 +979,7 @@ def latent_cat(zs, readers):
     """(zcat aliases x readers, z aliases): cat(zs, dim 1) for `readers` decoders and the
     zs for the loss, their gradients summed by one kernel (LatentCatFn)."""
     if not (torch.is_grad_enabled() and any(z.requires_grad for z in zs)):
-        zcat = torch.cat(zs, dim=1)
+        zcat = cat(zs, dim=1)
         return (zcat,) * readers, tuple(zs)
     out = LatentCatFn.apply(int(readers), *zs)
     return out[:readers], out[readers:]

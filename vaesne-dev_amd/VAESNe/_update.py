@@ -155,49 +155,54 @@ class TorchAdamWUpdater(Updater):
         groups = self.opt.param_groups
         ps, gs, ms, vs, ns, sets = [], [], [], [], [], []
         coefs, set_of, stepped, steps = [], {}, [], []
-        for gi, p, g in batch:
-            st = self.opt.state[p]
-            created = len(st) == 0
-            if created:       # torch's lazy state (torch/optim/adam.py _init_group)
-                st["step"] = torch.tensor(0.0, dtype=torch.float32)
-                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-            steps.append(st["step"])
-            stepped.append((p, created))
-        # every step count += 1 and read back in three host ops, not two per parameter (the
-        # per-tensor add and item() were most of the loop's host time at small batches)
-        torch._foreach_add_(steps, 1.0)
-        step_vals = torch.stack(steps).tolist()
-        for (gi, p, g), step in zip(batch, step_vals):
-            st = self.opt.state[p]
-            key = (gi, step)
-            k = set_of.get(key)
-            if k is None:
-                grp = groups[gi]
-                lr, wd, eps = grp["lr"], grp["weight_decay"], grp["eps"]
-                b1, b2 = grp["betas"]
-                bc1 = 1 - b1 ** step
-                bc2 = 1 - b2 ** step
-                k = set_of[key] = len(set_of)
-                coefs += [1 - lr * wd, 1 - b1, b2, 1 - b2, bc2 ** 0.5, eps, (lr / bc1) * -1, 0.0]
-            ps.append(p)
-            gs.append(g)
-            ms.append(st["exp_avg"])
-            vs.append(st["exp_avg_sq"])
-            ns.append(p.numel())
-            sets.append(k)
-        n = len(ps)
+        added = False
         try:
+            for gi, p, g in batch:
+                st = self.opt.state[p]
+                created = len(st) == 0
+                if created:       # torch's lazy state (torch/optim/adam.py _init_group)
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                steps.append(st["step"])
+                stepped.append((p, created))
+            # every step count += 1 and read back in three host ops, not two per parameter (the
+            # per-tensor add and item() were most of the loop's host time at small batches)
+            torch._foreach_add_(steps, 1.0)
+            added = True
+            step_vals = torch.stack(steps).tolist()
+            for (gi, p, g), step in zip(batch, step_vals):
+                st = self.opt.state[p]
+                key = (gi, step)
+                k = set_of.get(key)
+                if k is None:
+                    grp = groups[gi]
+                    lr, wd, eps = grp["lr"], grp["weight_decay"], grp["eps"]
+                    b1, b2 = grp["betas"]
+                    bc1 = 1 - b1 ** step
+                    bc2 = 1 - b2 ** step
+                    k = set_of[key] = len(set_of)
+                    coefs += [1 - lr * wd, 1 - b1, b2, 1 - b2, bc2 ** 0.5, eps, (lr / bc1) * -1, 0.0]
+                ps.append(p)
+                gs.append(g)
+                ms.append(st["exp_avg"])
+                vs.append(st["exp_avg_sq"])
+                ns.append(p.numel())
+                sets.append(k)
+            n = len(ps)
             _lib.lib.adamw_list(_lib.ptr_array(ps), _lib.ptr_array(gs), _lib.ptr_array(ms),
                                 _lib.ptr_array(vs), (C.c_int64 * n)(*ns),
                                 (C.c_int32 * n)(*sets), (C.c_float * len(coefs))(*coefs), n,
                                 skip, TORCH_FMA, _lib.stream())
         except BaseException:
-            # a failed enqueue (a checked hipError partway): undo this update's host
-            # bookkeeping, so the step counts never run ahead of launched updates
+            # anything failing between the lazy state creation and a completed enqueue (a
+            # stack of step tensors on different devices, a missing group key, a checked
+            # hipError partway): undo this update's host bookkeeping, so the step counts
+            # never run ahead of launched updates
             for p, created in stepped:
                 st = self.opt.state[p]
-                st["step"] -= 1
+                if added:
+                    st["step"] -= 1
                 if created:
                     del self.opt.state[p]
             raise

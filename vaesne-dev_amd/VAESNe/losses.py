@@ -114,7 +114,7 @@ def m_iwae(model, x, K=1):
     for i in range(n_chunk):
         split_i = tuple(tuple(tensor.split(S)[i] for tensor in tensor_tuple) for tensor_tuple in x)
         lw.append(_m_iwae(model, split_i, K))
-    lw = lw[0] if len(lw) == 1 else torch.cat(lw, 1)
+    lw = lw[0] if len(lw) == 1 else _ops.cat(lw, 1)
     return _ops.LmeSumFn.apply(lw)
 
 

@@ -22,6 +22,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
 
 #include "attn_common.h"
 
@@ -1699,6 +1701,32 @@ void launch_sum_chunks(const float* ws, int64_t ss, int n, int B, int L, int E, 
 bool use_sf16(int dh, int64_t bh, int Lq, int Lk) {
   return g_forced.nt == 0 && sf16_path(dh, bh, Lq, Lk);
 }
+// the repeated-sequence kernels: split-f16 unless a packed-VALU geometry is forced (the plain
+// path's rule, so a forced geometry selects the VALU kernels on both paths)
+bool use_rep_sf16(int L, int R) { return g_forced.nt == 0 && sf16_rep_path(L, R); }
+
+// Keep-bitmap layout guard: each forward records which kernel family (layout) and shape wrote
+// a bitmap; a backward that would read it with the other family -- a geometry override
+// flipped between the two calls -- fails with hipErrorInvalidValue instead of reading the
+// wrong bits.  Host side only (a captured graph replays both as captured).
+enum BitsFamily { kBitsValu = 1, kBitsSf16 = 2 };
+struct BitsTag { int fam, B, H, Lq, Lk; };
+std::mutex g_bits_mu;
+std::unordered_map<const void*, BitsTag> g_bits;
+void bits_record(const void* bits, int fam, int B, int H, int Lq, int Lk) {
+  if (!bits) return;
+  std::lock_guard<std::mutex> lk(g_bits_mu);
+  if (g_bits.size() > 65536) g_bits.clear();
+  g_bits[bits] = {fam, B, H, Lq, Lk};
+}
+bool bits_check(const void* bits, int fam, int B, int H, int Lq, int Lk) {
+  if (!bits) return true;
+  std::lock_guard<std::mutex> lk(g_bits_mu);
+  const auto it = g_bits.find(bits);
+  if (it == g_bits.end()) return true;   // written elsewhere (the caller's own bitmap)
+  const BitsTag& t = it->second;
+  return t.fam == fam && t.B == B && t.H == H && t.Lq == Lq && t.Lk == Lk;
+}
 
 // workspace of a split launch (bytes; 0 = no split for this shape)
 int64_t fwd_ws_floats(int B, int H, int Lq, int Lk, int dh, Split& sp) {
@@ -1925,6 +1953,10 @@ RepPlan rep_bwd_plan(int Bd, int R, int H, int L, float p_drop) {
     pl.std_floats = bwd_ws_floats(Bd, H, L, L, 8, sq, sk);
     return pl;
   }
+  if (use_rep_sf16(L, R)) {   // query-chunk partials of dK / dV only (dQ complete)
+    pl.dkv_floats = sf16_rep_bwd_ws_floats(Bd, H, L);
+    return pl;
+  }
   const int KB = 2 * g_rep.bnp * g_rep.bnt;
   pl.nkb = (L + KB - 1) / KB;
   pl.CB = (R + g_rep.brc - 1) / g_rep.brc;
@@ -1941,6 +1973,7 @@ RepPlan rep_bwd_plan(int Bd, int R, int H, int L, float p_drop) {
 
 // query blocks [p0 * nqb / np_, p1 * nqb / np_) of the launch geometry
 int launch_rep_fwd(const AttnArgs& a, int R, float p_drop, int p0, int p1, int np_, hipStream_t s) {
+  if (use_rep_sf16(a.Lq, R)) return sf16_rep_fwd(a, R, p_drop, p0, p1, np_, s);
   const bool drop = p_drop > 0.f;
   const int rc = drop ? g_rep.frc : 1;
   const int cb = drop ? (R + rc - 1) / rc : 1;
@@ -1977,6 +2010,7 @@ int launch_rep_bwd(const AttnArgs& a, int R, float p_drop, float* ws, hipStream_
     c.dout = dsum; c.do_bs = (int64_t)a.Lq * E; c.do_ls = E;
     return launch_bwd<8>(c, 0.f, 3, pl.std_floats > 0 ? ws + pl.dsum_floats : nullptr, s);
   }
+  if (use_rep_sf16(a.Lq, R)) return sf16_rep_bwd(a, R, ws, s);
   AttnArgs c = a;
   c.qchunk = pl.chunk;
   float* wdkv = ws;
@@ -2029,6 +2063,8 @@ VAESNE_API int vaesne_attn_rep_config(int fnt, int frc, int bnt, int bnp, int br
   return 0;
 }
 
+VAESNE_API int vaesne_attn_rep_sf16_config(int frc, int bwgs) { return sf16_rep_config(frc, bwgs); }
+
 VAESNE_API int64_t vaesne_attn_rep_workspace(int Bd, int R, int H, int L, int dh, float p_drop) {
   if (Bd <= 0 || R <= 0 || L <= 2 * SQ || dh != 8) return 0;
   const RepPlan pl = rep_bwd_plan(Bd, R, H, L, p_drop);
@@ -2066,6 +2102,7 @@ VAESNE_API int vaesne_attn_rep_fwd_part(const float* qkv, int64_t qkv_bs, int64_
   a.o = o; a.o_out = o; a.o_bs = o_bs; a.o_ls = o_ls;
   a.lse = lse;
   a.bits = keep_bits;
+  if (p_drop > 0.f) bits_record(keep_bits, use_rep_sf16(L, R) ? kBitsSf16 : kBitsValu, R * Bd, H, L, L);
   return launch_rep_fwd(a, R, p_drop, p0, p1, nparts, (hipStream_t)stream);
 }
 
@@ -2087,6 +2124,8 @@ VAESNE_API int vaesne_attn_rep_bwd(const float* qkv, int64_t qkv_bs, int64_t qkv
   if (Bd <= 0 || R <= 0 || L <= 0) return 0;
   if (dh != 8 || L <= 2 * SQ || !rep_cfg_ok(g_rep)) return (int)hipErrorInvalidValue;
   if (p_drop > 0.f && !keep_bits) return (int)hipErrorInvalidValue;
+  if (p_drop > 0.f && !bits_check(keep_bits, use_rep_sf16(L, R) ? kBitsSf16 : kBitsValu, R * Bd, H, L, L))
+    return (int)hipErrorInvalidValue;
   if (vaesne_attn_rep_workspace(Bd, R, H, L, dh, p_drop) > 0 && !workspace)
     return (int)hipErrorInvalidValue;
   const int E = H * dh;
@@ -2153,6 +2192,8 @@ VAESNE_API int vaesne_attn_fwd(const float* q, int64_t q_bs, int64_t q_ls, const
   a.lse = lse;
   a.bits = keep_bits;
   fill_common(a, B, H, Lq, Lk, dh, p_drop, rng_state, call_id);
+  if (p_drop > 0.f && Lq > 2 * SQ)
+    bits_record(keep_bits, use_sf16(dh, (int64_t)B * H, Lq, Lk) ? kBitsSf16 : kBitsValu, B, H, Lq, Lk);
   hipStream_t s = (hipStream_t)stream;
   if (dh == 8) return launch_fwd<8>(a, p_drop, workspace, s);
   return launch_fwd<16>(a, p_drop, workspace, s);
@@ -2175,6 +2216,14 @@ int attn_bwd_impl(const float* q, int64_t q_bs, int64_t q_ls, const float* k, in
   if (!aligned16(q, q_ls) || !aligned16(k, k_ls) || !aligned16(v, v_ls) || !aligned16(o, o_ls) ||
       !aligned16(dout, do_ls) || !aligned16(dq, dq_ls) || !aligned16(dk, dk_ls) ||
       !aligned16(dv, dv_ls))
+    return (int)hipErrorInvalidValue;
+  // one fused kernel (the few-query path, the split-f16 path) writes dq, dk and dv whichever
+  // part is asked for: all three must be given
+  if ((Lq <= 2 * SQ || use_sf16(dh, (int64_t)B * H, Lq, Lk)) && (!dq || !dk || !dv))
+    return (int)hipErrorInvalidValue;
+  // the bitmap must come from the kernel family this backward reads it with
+  if (p_drop > 0.f && Lq > 2 * SQ &&
+      !bits_check(keep_bits, use_sf16(dh, (int64_t)B * H, Lq, Lk) ? kBitsSf16 : kBitsValu, B, H, Lq, Lk))
     return (int)hipErrorInvalidValue;
   AttnArgs a{};
   a.q = q; a.q_bs = q_bs; a.q_ls = q_ls;

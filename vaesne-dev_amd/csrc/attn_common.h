@@ -63,5 +63,12 @@ int64_t sf16_bits_bytes(int B, int H, int Lq, int Lk);
 int64_t sf16_bwd_ws_floats(int B, int H, int Lq, int Lk);
 int sf16_fwd(const AttnArgs& a, float p_drop, hipStream_t s);
 int sf16_bwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s);
+// the decoders' first block: R copies of each of a.B distinct sequences (vaesne_attn_rep_*),
+// taken for L in (16, 1024] unless a geometry is forced
+bool sf16_rep_path(int L, int R);
+int64_t sf16_rep_bwd_ws_floats(int Bd, int H, int L);
+int sf16_rep_fwd(const AttnArgs& a, int R, float p_drop, int p0, int p1, int np, hipStream_t s);
+int sf16_rep_bwd(const AttnArgs& a, int R, float* ws, hipStream_t s);
+int sf16_rep_config(int frc, int bwgs);
 
 }  // namespace vaesne
