@@ -117,10 +117,32 @@ class TorchAdamWUpdater(Updater):
     def __init__(self, optimizer):
         super().__init__(optimizer)
         self.hist = collections.deque(maxlen=8)
+        self._bkey = None      # identity key of the last validated batch (_batch)
+        self._bval = None
+        self._arrays = None    # (identity key, ctypes arrays) of the last launch (update)
 
     def _batch(self):
         """(params, grads, states) of the tensors torch would update now, or None if
-        one of them is outside the supported configuration."""
+        one of them is outside the supported configuration.  A batch of the same tensors
+        as the previous one (the captured step's gradients, the same state tensors) is
+        not re-validated."""
+        st_of = self.opt.state
+        key = []
+        for group in self.opt.param_groups:
+            for p in group["params"]:
+                g = p.grad
+                if g is not None:
+                    st = st_of.get(p)
+                    key.append((id(p), id(g), id(st["exp_avg"]) if st else 0, p.data_ptr(),
+                                g.data_ptr()))
+        key = tuple(key)
+        if key == self._bkey:
+            return list(self._bval)
+        out = self._batch_full()
+        self._bkey, self._bval = (key, tuple(out)) if out is not None else (None, None)
+        return out
+
+    def _batch_full(self):
         out = []
         for gi, group in enumerate(self.opt.param_groups):
             for p in group["params"]:
@@ -190,9 +212,15 @@ class TorchAdamWUpdater(Updater):
                 ns.append(p.numel())
                 sets.append(k)
             n = len(ps)
-            _lib.lib.adamw_list(_lib.ptr_array(ps), _lib.ptr_array(gs), _lib.ptr_array(ms),
-                                _lib.ptr_array(vs), (C.c_int64 * n)(*ns),
-                                (C.c_int32 * n)(*sets), (C.c_float * len(coefs))(*coefs), n,
+            # the arrays hold device addresses: keyed by the addresses themselves
+            akey = (tuple(t.data_ptr() for t in ps), tuple(t.data_ptr() for t in gs),
+                    tuple(t.data_ptr() for t in ms), tuple(t.data_ptr() for t in vs), tuple(ns),
+                    tuple(sets))
+            if self._arrays is None or self._arrays[0] != akey:
+                self._arrays = (akey, (_lib.ptr_array(ps), _lib.ptr_array(gs), _lib.ptr_array(ms),
+                                       _lib.ptr_array(vs), (C.c_int64 * n)(*ns), (C.c_int32 * n)(*sets)))
+            pa, ga, ma, va, na, sa = self._arrays[1]
+            _lib.lib.adamw_list(pa, ga, ma, va, na, sa, (C.c_float * len(coefs))(*coefs), n,
                                 skip, TORCH_FMA, _lib.stream())
         except BaseException:
             # anything failing between the lazy state creation and a completed enqueue (a

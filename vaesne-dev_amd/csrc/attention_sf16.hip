@@ -725,9 +725,12 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
 // of dO'' and v'' (maxima in [2^6, 2^7): normal f16 lo parts).
 constexpr int RB_NW_MAX = 8;
 constexpr int RB_RG = 16;            // copies per staged group
-constexpr int RB_QCH_MAX = 1024;     // queries of a chunk (prologue arrays)
+constexpr int RB_QCH_MAX = 512;      // queries of a chunk (prologue arrays)
+constexpr int RB_LMAX = 1024;        // sequence length of the path (8 waves x 128 keys)
+// dS'' transpose image: ONE per wave (a wave's LDS operations complete in order, so the next
+// tile's writes never overtake this tile's transposed reads)
 size_t rep_bwd_lds_bytes(int nw) {
-  return (size_t)nw * (BKT * 256 + 2 * SC_WORDS + 2 * 128) * sizeof(uint32_t);
+  return (size_t)nw * (BKT * 256 + SC_WORDS + 2 * 128) * sizeof(uint32_t);
 }
 
 template <bool DROP>
@@ -738,15 +741,17 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
   // image [RG][256]; during the prologue the per-copy D_c [RG][chunk] scratch
   __shared__ __attribute__((aligned(16))) uint32_t Ca[RB_RG * 16 * 12];
   __shared__ __attribute__((aligned(16))) uint32_t Ct[RB_RG * 256];
-  // K^T A operands [NW][BKT][256], dS'' transpose images [NW][2][SC_WORDS], dQ partials [2][NW * 128]
+  // K^T A operands [NW][BKT][256], dS'' transpose images [NW][SC_WORDS], dQ partials [2][NW * 128]
   extern __shared__ __attribute__((aligned(16))) uint32_t bwd_dyn[];
   __shared__ __attribute__((aligned(16))) uint32_t Qa[16 * 12];
   __shared__ __attribute__((aligned(16))) uint32_t QT[256];
+  // the staged step's keep words: [wave][copy][key group (key % 16) / 4][16 queries]
+  __shared__ __attribute__((aligned(16))) uint32_t Kw[RB_NW_MAX * RB_RG * 64];
   __shared__ float Red[3][RB_NW_MAX];
   const int NW = blockDim.x >> 6;
   uint32_t* const KTi = bwd_dyn;
   uint32_t* const Sc = bwd_dyn + NW * BKT * 256;
-  float* const Qp = reinterpret_cast<float*>(Sc + NW * 2 * SC_WORDS);
+  float* const Qp = reinterpret_cast<float*>(Sc + NW * SC_WORDS);
   const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, c = l & 15;
   const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
   const int qs = wg % QS, bh = wg / QS;
@@ -916,6 +921,24 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
   const int ngrp = (R + RB_RG - 1) / RB_RG;
   const int sq_i = (t >> 1) & 15, shf = t & 1, src = t >> 5;
   float4 rQ = make_float4(0.f, 0.f, 0.f, 0.f), rD = rQ;
+  // this wave's keep words of step (it, gi) straight into its own LDS region (LDS-DMA: no
+  // registers; a wave reads only its own region, so it may refill it once its copy loops are
+  // done): 4 loads of 1 KB, lane l of load j = copy 4j + l / 16, key group (l / 4) % 4, queries
+  // 4 (l % 4) .. + 3 of the tile
+  auto keep_dma = [&](int it, int gi) {
+    if (!DROP || ntile == 0) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int rc = 4 * j + (l >> 4), G = (l >> 2) & 3, r = gi * RB_RG + rc;
+      if (r < R) {
+        const int64_t nh = seq(r) * a.H + h;
+        const uint32_t* src = a.bits + ((nh * NT8 + w) * 4 + G) * Lqp + qbeg + 16 * it + 4 * (l & 3);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(Kw + (w * RB_RG * 64 + j * 256)),
+                                         16, 0, 0);
+      }
+    }
+  };
   auto issue = [&](int it, int gi) {
     const int q = qbeg + 16 * it + sq_i;
     if (t < 32 && gi == 0)
@@ -970,12 +993,9 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
       }
     }
   };
-  // keep words of copy r for this lane: 4 queries (q + 4g + i), key residue c, the wave's 128 keys
-  auto words = [&](int r, int q0) -> u4 {
-    if (!DROP || ntile == 0) return (u4){0u, 0u, 0u, 0u};
-    const int64_t nh = seq(r) * a.H + h;
-    return *reinterpret_cast<const u4*>(a.bits + ((nh * NT8 + w) * 4 + (c >> 2)) * Lqp + q0 + 4 * g);
-  };
+  // keep words of staged copy rc for this lane: 4 queries (q0 + 4g + i), key group c / 4, the
+  // wave's 128 keys
+  auto words = [&](int rc) -> u4 { return ldu4(Kw + ((w * RB_RG + rc) * 4 + (c >> 2)) * 16 + 4 * g); };
   const float uq = ldexpf(a.scale, -14 - s);
   float* dqb = a.dq + (int64_t)b * a.dq_bs + h * 8;
   auto dq_reduce = [&](int q0, int buf) {
@@ -988,6 +1008,7 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
   };
 
   const int nsteps = nqt * ngrp;
+  keep_dma(0, 0);
   issue(0, 0);
   __syncthreads();      // the prologue's scratch (Ca) is free
   commit(0);
@@ -1026,8 +1047,9 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
           Pw[u][3] = pk_lo(P[2], P[3], Pw[u][2]);
           acc[u] = splat(0.f);
         }
+        if (DROP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's keep-word DMA
         for (int rc = 0; rc < ng; ++rc) {
-          const u4 kw = words(rg0 + rc, q0);
+          const u4 kw = words(rc);
           const u4 DA = ldu4(Ca + (rc * 16 + c) * 12 + dtoff);
           const u4 DT = ldu4(Ct + rc * 256 + c * 16 + 4 * g);
 #pragma unroll
@@ -1053,6 +1075,7 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
           }
         }
         if (!issued && (hh == 1 || 4 >= ntile) && st + 1 < nsteps) {
+          keep_dma((st + 1) / ngrp, (st + 1) % ngrp);
           issue((st + 1) / ngrp, (st + 1) % ngrp);
           issued = true;
         }
@@ -1078,7 +1101,7 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
           Bk[1] = pk_lo(dS[0], dS[1], Bk[0]);
           Bk[3] = pk_lo(dS[2], dS[3], Bk[2]);
           dK[tt] = mma(QTA, Bk, dK[tt]);
-          uint32_t* sc = Sc + (w * 2 + (tt & 1)) * SC_WORDS;
+          uint32_t* sc = Sc + w * SC_WORDS;
           const int Rw = 4 * (c >> 1) + (c & 1);
           *reinterpret_cast<uint2*>(sc + sc_at(Rw, g)) = make_uint2(Bk[0], Bk[2]);
           *reinterpret_cast<uint2*>(sc + sc_at(Rw + 2, g)) = make_uint2(Bk[1], Bk[3]);
@@ -1181,6 +1204,7 @@ RepBwdPlan rep_bwd_plan_sf16(int Bd, int H, int L) {
   const int64_t bh = (int64_t)Bd * H;
   int qs = (int)std::max<int64_t>(1, (g_rs.bwgs + bh / 2) / bh);
   qs = std::min(qs, tiles);
+  qs = std::max(qs, (tiles + RB_QCH_MAX / 16 - 1) / (RB_QCH_MAX / 16));   // chunk <= RB_QCH_MAX
   RepBwdPlan pl;
   pl.qchunk = (tiles + qs - 1) / qs * 16;
   pl.QS = (L + pl.qchunk - 1) / pl.qchunk;
@@ -1199,7 +1223,7 @@ void launch_fwd_k(const AttnArgs& a, int R, int nw, int qb0, int nqbs, int cy, h
 bool sf16_path(int dh, int64_t bh, int Lq, int Lk) {
   return dh == 8 && bh > 0 && Lq > 16 && Lq <= BLQ_MAX && Lk >= 1;
 }
-bool sf16_rep_path(int L, int R) { return L > 16 && L <= 128 * RB_NW_MAX && L <= RB_QCH_MAX && R >= 1; }
+bool sf16_rep_path(int L, int R) { return L > 16 && L <= RB_LMAX && R >= 1; }
 
 int64_t sf16_bits_bytes(int B, int H, int Lq, int Lk) {
   return (int64_t)B * H * nt8(Lk) * 4 * lq_pad(Lq) * (int64_t)sizeof(uint32_t);
