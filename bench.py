@@ -292,6 +292,32 @@ def _rocprof_avg_ms(kernel_prefix):
     return None, None
 
 
+def _sq_valu(kernel, scores):
+    """VALU issue model of a roofline kernel from the committed SQ counter passes
+    (profiles/<LATEST>/sq_counters.json, written by profiles/sq_json.py from
+    profiles/r06/sq.sh): lane-ops per score = SQ_INSTS_VALU * 64 / scores; issue cycles per
+    SIMD = (2 * (VALU - MFMA) + 2 * TRANS + 8 * MFMA) / 1024 SIMDs (each VALU op issues in
+    2 cycles on a 64-wide wave, transcendentals take 2 more, a 16x16x32 f16 MFMA 8);
+    frac = issue cycles / active cycles (GRBM_GUI_ACTIVE / 8 XCDs); issue-bound ms =
+    frac * the profiled launch duration.  None without the file."""
+    try:
+        d = open(os.path.join(ROOT, "profiles", "LATEST")).read().strip()
+        path = os.path.join(ROOT, "profiles", d, "sq_counters.json")
+        k = json.load(open(path))["kernels"][kernel]
+    except (OSError, KeyError, ValueError):
+        return None
+    c = k["per_launch"]
+    valu, mfma = c["SQ_INSTS_VALU"], c.get("SQ_INSTS_MFMA", 0.0)
+    trans = c.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
+    cyc = (2 * (valu - mfma) + 2 * trans + 8 * mfma) / 1024
+    frac = cyc * 8 / c["GRBM_GUI_ACTIVE"]
+    return dict(valu_ops_per_score=round(valu * 64 / scores, 2),
+                valu_issue_frac=round(frac, 3),
+                valu_issue_bound_ms=round(frac * k["launch_us_pass1"] * 1e-3, 4),
+                sq_launch_ms=round(k["launch_us_pass1"] * 1e-3, 4),
+                sq_source=f"profiles/{d}/sq_counters.json")
+
+
 def roofline(device, B, in_step=None):
     """Spectra-decoder masked self-attention at its step shape (N = 2*K*B
     sequences x 982 tokens: the decoder runs once over both modalities'
@@ -377,11 +403,18 @@ def roofline(device, B, in_step=None):
                          st.data_ptr(), 9, bits.data_ptr(), wsr.data_ptr(), _lib.stream())
 
     rep_fwd()
-    for name, kern, fn, fl in [("rep_fwd", "attn_rep_fwd_kernel", rep_fwd, 4 * dh),
-                               ("rep_bwd", "attn_rep_bwd_kernel", rep_bwd, 8 * dh)]:
+    for name, kern, fn, fl in [("rep_fwd", "attn_fwd_sf16_kernel<1, 16, true>", rep_fwd, 4 * dh),
+                               ("rep_bwd", "attn_rep_bwd_sf16_kernel", rep_bwd, 8 * dh)]:
         t = time_kernel(fn, 20, device)
         res[name] = dict(kernel=kern, ms=t * 1e3, equiv_tflops=scores * fl / t / 1e12,
                          note=f"{R} copies x {Bd} sequences (decoder block 1)")
+    for name, sqk in (("fwd", "attn_fwd_sf16_kernel<4, 1, true>"),
+                      ("bwd", "attn_bwd_sf16_kernel<true>"),
+                      ("rep_fwd", "attn_fwd_sf16_kernel<1, 16, true>"),
+                      ("rep_bwd", "attn_rep_bwd_sf16_kernel<true>")):
+        v = _sq_valu(sqk, scores) if pd > 0 else None   # the counters are of the dropout launch
+        if v is not None:
+            res[name].update(v)
     for name, key, fl in (("fwd", "attn_fwd", 4 * dh), ("bwd", "attn_bwd", 8 * dh)):
         if in_step and key in in_step:
             ms, n = in_step[key]

@@ -19,10 +19,12 @@
 // contraction sums over slots, and A's slot (g, j) meets B's slot (g, j) whichever k the
 // hardware gives it, so the term layout needs only that A and B share one slot map.
 // Contractions over the 16 rows of an accumulator tile (P V, dV = P^T dO, dK = dS^T Q,
-// dQ = dS K) pack each value pair (x_a, x_b) as a hi pair and a lo pair in adjacent slots;
-// the other operand supplies [y_hi(a), y_hi(b), y_hi(a), y_hi(b)] for the hi rows of its
-// tile and [y_lo(a), y_lo(b), 0, 0] for its lo rows (rows f and f + 8 of the result summed
-// at the end: the same three terms).
+// dQ = dS K) carry the values as hi pair words and lo pair words (f16x2 of two values of the
+// same precision); the other operand supplies the matching y_hi in the slots of both for its
+// hi rows and y_lo / 0 for its lo rows (rows f and f + 8 of the result summed at the end: the
+// same three terms).  A dword of either operand never mixes a hi and a lo part: the matrix
+// core adds a dword's two products first, and a (hi, lo) dword of one value measurably loses
+// the lo product ("Split-f16 operand pairing").
 //
 // Range.  Softmax probabilities enter scaled, P' = 2^c P (c = 7 forward with the lazy
 // running max, 14 backward), so they sit in f16's normal range; the gradient operands of the
@@ -67,6 +69,19 @@ __device__ __forceinline__ uint32_t pk_lo(float a, float b, uint32_t hi) {
   const f2v h = __builtin_convertvector(__builtin_bit_cast(h2v, hi), f2v);
   return pk_hi(a - h.x, b - h.y);
 }
+// pk_lo through v_fma_mix_f32 (a * one - f16 hi half, one rounding: the same bits as a - hi,
+// which is exact): one instruction per value instead of a conversion and a subtract.  `one`
+// is 1.0 from opaque_one(), which the compiler cannot fold (a * 1 would become the plain
+// subtract again)
+__device__ __forceinline__ uint32_t pk_lo1(float a, float b, uint32_t hi, float one) {
+  const h2v h = __builtin_bit_cast(h2v, hi);
+  return pk_hi(fmaf(a, one, -(float)h.x), fmaf(b, one, -(float)h.y));
+}
+__device__ __forceinline__ float opaque_one() {
+  float x;
+  asm volatile("v_mov_b32 %0, 1.0" : "=v"(x));
+  return x;
+}
 __device__ __forceinline__ _Float16 f16_hi(float x) { return (_Float16)x; }
 __device__ __forceinline__ _Float16 f16_lo(float x) {
   return isfinite(x) ? (_Float16)(x - (float)(_Float16)x) : (_Float16)0.f;
@@ -75,6 +90,11 @@ __device__ __forceinline__ uint32_t pack2(_Float16 a, _Float16 b) {
   return __builtin_bit_cast(uint32_t, (h2v){a, b});
 }
 __device__ __forceinline__ float max4(f4 v) { return fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])); }
+__device__ __forceinline__ int imax8(f4 a, f4 b) {
+  const int m0 = max(max(__float_as_int(a[0]), __float_as_int(a[1])), __float_as_int(a[2]));
+  const int m1 = max(max(__float_as_int(a[3]), __float_as_int(b[0])), __float_as_int(b[1]));
+  return max(max(m0, m1), max(__float_as_int(b[2]), __float_as_int(b[3])));
+}
 __device__ __forceinline__ f4 splat(float x) { return (f4){x, x, x, x}; }
 __device__ __forceinline__ u4 ldu4(const uint32_t* p) { return *reinterpret_cast<const u4*>(p); }
 __device__ __forceinline__ uint32_t as_u(float x) { return __float_as_uint(x); }
@@ -127,6 +147,7 @@ __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(At
   const float* vg = a.v + (int64_t)b * a.v_bs + h * 8;
   const float* kbg = a.kbias ? a.kbias + (int64_t)b * a.kb_bs : nullptr;
   const uint32_t skey = DROP ? key_of(a.rng_state, a.call_id) : 0u;
+  const float one = opaque_one();
   // the output sequence of copy rc: copies past R (R % RC != 0) run as copy R - 1, not stored
   auto seq_of = [&](int rc) { return (int64_t)min(r0 + rc, R - 1) * Bd + b; };
 
@@ -227,8 +248,10 @@ __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(At
       const int T0 = ks / 16 + 2 * p;
 #pragma unroll
       for (int n = 0; n < NQT; ++n) {
-        // lazy origin: p' <= 2^15 while no score passes m by more than 8
-        if (__builtin_amdgcn_ballot_w64(fmaxf(max4(S0[n]), max4(S1[n])) > 15.f)) {
+        // lazy origin: p' <= 2^15 while no score passes m by more than 8.  Tested on the bit
+        // patterns (scores are never NaN; a negative one is a negative integer): an integer
+        // max needs no NaN canonicalisation (v_max3_i32)
+        if (__builtin_amdgcn_ballot_w64(imax8(S0[n], S1[n]) > (int)0x41700000)) {   // > 15.f
           const f4 z = splat(0.f);
           const f4 R0 = mma(A0, Qop[n], z), R1 = mma(A1, Qop[n], z);
           float x = fmaxf(max4(R0), max4(R1));
@@ -281,10 +304,10 @@ __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(At
         Bh[1] = pk_hi(S0[n][2], S0[n][3]);
         Bh[2] = pk_hi(S1[n][0], S1[n][1]);
         Bh[3] = pk_hi(S1[n][2], S1[n][3]);
-        Bl[0] = pk_lo(S0[n][0], S0[n][1], Bh[0]);
-        Bl[1] = pk_lo(S0[n][2], S0[n][3], Bh[1]);
-        Bl[2] = pk_lo(S1[n][0], S1[n][1], Bh[2]);
-        Bl[3] = pk_lo(S1[n][2], S1[n][3], Bh[3]);
+        Bl[0] = pk_lo1(S0[n][0], S0[n][1], Bh[0], one);
+        Bl[1] = pk_lo1(S0[n][2], S0[n][3], Bh[1], one);
+        Bl[2] = pk_lo1(S1[n][0], S1[n][1], Bh[2], one);
+        Bl[3] = pk_lo1(S1[n][2], S1[n][3], Bh[3], one);
         if (DROP && RC > 1) {    // copies: the split is shared, each copy masks the words
           const int q = qb * QB + 16 * (NQT * w + n) + c;
 #pragma unroll
@@ -397,6 +420,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
   const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, c = l & 15;
   const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
   const int kb = wg % nkb, bh = wg / nkb;
+  const float one = opaque_one();
   const int b = bh / a.H, h = bh - b * a.H;
   const int key0 = kb * KB + 128 * w;
   const int ntile = key0 < a.Lk ? min(BKT, (a.Lk - key0 + 15) / 16) : 0;   // wave-uniform
@@ -573,19 +597,19 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
       A_[10] = 0u;
       A_[11] = 0u;
     }
-    // transposed A operand: rows f / f + 8, slots 8 gs + j of query qi = 4 gs + i:
-    // j = 4 (i/2) + i%2 (precision 0) and + 2 (precision 1)
+    // transposed A operand: rows f / f + 8, slots 8 gs + i (precision 0) and 8 gs + 4 + i
+    // (precision 1) of query qi = 4 gs + i (B: [hi(q0, q1) | hi(q2, q3) | lo(q0, q1) | lo(q2, q3)])
     _Float16* T_ = reinterpret_cast<_Float16*>(isq ? QT[buf] : DT[buf]);
-    const int gs = qi >> 2, i = qi & 3, j0 = 4 * (i >> 1) + (i & 1);
+    const int gs = qi >> 2, j0 = qi & 3;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int f = f0 + e;
       const _Float16 xh = f16_hi(x[e]), xl = f16_lo(x[e]);
       _Float16* row = T_ + f * 32 + 8 * gs + j0;
       row[0] = xh;
-      row[2] = xh;
+      row[4] = xh;
       row[8 * 32] = xl;
-      row[8 * 32 + 2] = (_Float16)0.f;
+      row[8 * 32 + 4] = (_Float16)0.f;
     }
   };
   // keep words of this lane: 4 queries (q0 + 4g + r), key residue c, the wave's 128 keys
@@ -629,7 +653,9 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
       for (int tt = 0; tt < BKT; ++tt) {
         {   // every tile, past-Lk keys too (zero K / V, bias -inf): no per-tile branch
           const f4 S = mma(QA, Kop[tt], CS);
-          const f4 dP = mma(DA, Vop[tt], CD);
+          // with dropout dP' without the row constant: dS'' = p' keep dP' + p' (-D') = fma(Pd,
+          // dP', p' C) (the keep select folded into the masked p' the dV product needs anyway)
+          const f4 dP = mma(DA, Vop[tt], DROP ? splat(0.f) : CD);
           float P[4], Pd[4], dS[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -637,8 +663,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
             if (DROP) {
               const uint32_t mk = (uint32_t)__builtin_amdgcn_sbfe((int)kw[r], 4 * tt + (c & 3), 1);
               Pd[r] = __uint_as_float(as_u(P[r]) & mk);
-              const float tq = __uint_as_float(as_u(CD[r]) ^ ((as_u(CD[r]) ^ as_u(dP[r])) & mk));
-              dS[r] = P[r] * tq;
+              dS[r] = fmaf(Pd[r], dP[r], P[r] * CD[r]);
             } else {
               Pd[r] = P[r];
               dS[r] = P[r] * dP[r];
@@ -646,20 +671,20 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
           }
           u4 Bv, Bk;
           Bv[0] = pk_hi(Pd[0], Pd[1]);
-          Bv[2] = pk_hi(Pd[2], Pd[3]);
-          Bv[1] = pk_lo(Pd[0], Pd[1], Bv[0]);
-          Bv[3] = pk_lo(Pd[2], Pd[3], Bv[2]);
+          Bv[1] = pk_hi(Pd[2], Pd[3]);
+          Bv[2] = pk_lo1(Pd[0], Pd[1], Bv[0], one);
+          Bv[3] = pk_lo1(Pd[2], Pd[3], Bv[1], one);
           Bk[0] = pk_hi(dS[0], dS[1]);
-          Bk[2] = pk_hi(dS[2], dS[3]);
-          Bk[1] = pk_lo(dS[0], dS[1], Bk[0]);
-          Bk[3] = pk_lo(dS[2], dS[3], Bk[2]);
+          Bk[1] = pk_hi(dS[2], dS[3]);
+          Bk[2] = pk_lo1(dS[0], dS[1], Bk[0], one);
+          Bk[3] = pk_lo1(dS[2], dS[3], Bk[1], one);
           dV[tt] = mma(DTA, Bv, dV[tt]);
           dK[tt] = mma(QTA, Bk, dK[tt]);
           // dS'' through LDS: row R = 4 (c/2) + 2 prec + c%2 holds queries 0..15 (32 B)
           uint32_t* sc = Sc + (w * 2 + (tt & 1)) * SC_WORDS;
           const int R = 4 * (c >> 1) + (c & 1);
-          *reinterpret_cast<uint2*>(sc + sc_at(R, g)) = make_uint2(Bk[0], Bk[2]);
-          *reinterpret_cast<uint2*>(sc + sc_at(R + 2, g)) = make_uint2(Bk[1], Bk[3]);
+          *reinterpret_cast<uint2*>(sc + sc_at(R, g)) = make_uint2(Bk[0], Bk[1]);
+          *reinterpret_cast<uint2*>(sc + sc_at(R + 2, g)) = make_uint2(Bk[2], Bk[3]);
           // (the wave's LDS operations complete in order: the transposed reads see these rows)
           // B[slot 8g + j][query c] = row 8g + j: two 4-row transposed reads
           const int rq = (c >> 2), cp = (c & 3);
@@ -755,6 +780,7 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
   const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, c = l & 15;
   const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
   const int qs = wg % QS, bh = wg / QS;
+  const float one = opaque_one();
   const int b = bh / a.H, h = bh - b * a.H;
   const int Bd = a.B;
   const int key0 = 128 * w;
@@ -958,16 +984,16 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
       *reinterpret_cast<uint2*>(A_ + 4 + 2 * shf) = make_uint2(pk_lo(x[0], x[1], h0), pk_lo(x[2], x[3], h1));
       *reinterpret_cast<uint2*>(A_ + 8 + 2 * shf) = make_uint2(shf == 0 ? ONES_F16X2 : 0u, 0u);
       _Float16* T_ = reinterpret_cast<_Float16*>(QT);
-      const int gs = sq_i >> 2, i = sq_i & 3, j0 = 4 * (i >> 1) + (i & 1);
+      const int gs = sq_i >> 2, j0 = sq_i & 3;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int f = 4 * shf + e;
         const _Float16 xh = f16_hi(x[e]), xl = f16_lo(x[e]);
         _Float16* row = T_ + f * 32 + 8 * gs + j0;
         row[0] = xh;
-        row[2] = xh;
+        row[4] = xh;
         row[8 * 32] = xl;
-        row[8 * 32 + 2] = (_Float16)0.f;
+        row[8 * 32 + 4] = (_Float16)0.f;
       }
     }
     if (src < RB_RG) {   // dO'_c: A operand [hi | lo | 0] (the dP' product) and the dO'^T image
@@ -979,16 +1005,16 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
       *reinterpret_cast<uint2*>(A_ + 8 + 2 * shf) = make_uint2(0u, 0u);
       {   // the transposed A operand, rows f / f + 8, as the Q^T image
         _Float16* T_ = reinterpret_cast<_Float16*>(Ct + src * 256);
-        const int gs = sq_i >> 2, i = sq_i & 3, j0 = 4 * (i >> 1) + (i & 1);
+        const int gs = sq_i >> 2, j0 = sq_i & 3;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int f = 4 * shf + e;
           const _Float16 xh = f16_hi(x[e]), xl = f16_lo(x[e]);
           _Float16* row = T_ + f * 32 + 8 * gs + j0;
           row[0] = xh;
-          row[2] = xh;
+          row[4] = xh;
           row[8 * 32] = xl;
-          row[8 * 32 + 2] = (_Float16)0.f;
+          row[8 * 32 + 4] = (_Float16)0.f;
         }
       }
     }
@@ -1032,7 +1058,7 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
       for (int hh = 0; hh < 2; ++hh) {
         if (4 * hh >= ntile) break;
         f4 acc[4];
-        u4 Pw[4];     // p' as hi / lo pair words [hi(0,1) | lo(0,1) | hi(2,3) | lo(2,3)]
+        u4 Pw[4];     // p' as hi / lo pair words [hi(0,1) | hi(2,3) | lo(0,1) | lo(2,3)]
         const u4 QA = ldu4(Qa + c * 12 + dtoff);
         const f4 CS = *reinterpret_cast<const f4*>(Cs_l + ql + 4 * g);
 #pragma unroll
@@ -1042,9 +1068,9 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
 #pragma unroll
           for (int r = 0; r < 4; ++r) P[r] = ex2(S[r]);
           Pw[u][0] = pk_hi(P[0], P[1]);
-          Pw[u][2] = pk_hi(P[2], P[3]);
-          Pw[u][1] = pk_lo(P[0], P[1], Pw[u][0]);
-          Pw[u][3] = pk_lo(P[2], P[3], Pw[u][2]);
+          Pw[u][1] = pk_hi(P[2], P[3]);
+          Pw[u][2] = pk_lo1(P[0], P[1], Pw[u][0], one);
+          Pw[u][3] = pk_lo1(P[2], P[3], Pw[u][1], one);
           acc[u] = splat(0.f);
         }
         if (DROP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's keep-word DMA
@@ -1068,8 +1094,8 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
                 acc[u][r] = __uint_as_float((as_u(x[r]) & mk[i]) | (as_u(acc[u][r]) & ~mk[i]));
               }
               const uint32_t mm = (mk[0] & 0xFFFFu) | (mk[1] & 0xFFFF0000u);
-              Bv[2 * r2] = Pw[u][2 * r2] & mm;
-              Bv[2 * r2 + 1] = Pw[u][2 * r2 + 1] & mm;
+              Bv[r2] = Pw[u][r2] & mm;
+              Bv[2 + r2] = Pw[u][2 + r2] & mm;
             }
             dV[tt] = mma(DT, Bv, dV[tt]);
           }
@@ -1089,7 +1115,7 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
           for (int r = 0; r < 4; ++r) {
             // p' = hi + lo again, each half converted on its own (hipcc 7.2 miscompiled the
             // vector conversion of a u4 element here, converting element 0's word for all r)
-            const uint32_t wh = Pw[u][(r >> 1) * 2], wl = Pw[u][(r >> 1) * 2 + 1];
+            const uint32_t wh = Pw[u][r >> 1], wl = Pw[u][2 + (r >> 1)];
             const int sh = 16 * (r & 1);
             const float ph = (float)__builtin_bit_cast(_Float16, (uint16_t)((wh >> sh) & 0xffffu));
             const float pl = (float)__builtin_bit_cast(_Float16, (uint16_t)((wl >> sh) & 0xffffu));
@@ -1097,14 +1123,14 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
           }
           u4 Bk;
           Bk[0] = pk_hi(dS[0], dS[1]);
-          Bk[2] = pk_hi(dS[2], dS[3]);
-          Bk[1] = pk_lo(dS[0], dS[1], Bk[0]);
-          Bk[3] = pk_lo(dS[2], dS[3], Bk[2]);
+          Bk[1] = pk_hi(dS[2], dS[3]);
+          Bk[2] = pk_lo1(dS[0], dS[1], Bk[0], one);
+          Bk[3] = pk_lo1(dS[2], dS[3], Bk[1], one);
           dK[tt] = mma(QTA, Bk, dK[tt]);
           uint32_t* sc = Sc + w * SC_WORDS;
           const int Rw = 4 * (c >> 1) + (c & 1);
-          *reinterpret_cast<uint2*>(sc + sc_at(Rw, g)) = make_uint2(Bk[0], Bk[2]);
-          *reinterpret_cast<uint2*>(sc + sc_at(Rw + 2, g)) = make_uint2(Bk[1], Bk[3]);
+          *reinterpret_cast<uint2*>(sc + sc_at(Rw, g)) = make_uint2(Bk[0], Bk[1]);
+          *reinterpret_cast<uint2*>(sc + sc_at(Rw + 2, g)) = make_uint2(Bk[2], Bk[3]);
           const int rq = (c >> 2), cp = (c & 3);
           const s4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (__attribute__((address_space(3))) s4*)(sc + sc_at(8 * g + rq, cp)));
