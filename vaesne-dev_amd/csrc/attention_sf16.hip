@@ -132,10 +132,12 @@ template <int NQT, int RC, bool DROP>
 __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(AttnArgs a, int NT8, int Lqp,
                                                                             int R, int qb0, int nqbs) {
   // per staged key: [hi 4 u32 | lo 4 | bias (hi, lo), 0 ...]; V^T per 32-key pair: 16 rows
-  // x 32 f16; key-pair mixes for the dropout hash
+  // x 32 f16 at a 24-word row stride (conflict-free staging stores and operand reads);
+  // key-pair mixes for the dropout hash
   __shared__ __attribute__((aligned(16))) uint32_t Ki[2][FKC_MAX * 12];
-  __shared__ __attribute__((aligned(16))) uint32_t Vi[2][FKC_MAX * 8];
+  __shared__ __attribute__((aligned(16))) uint32_t Vi[2][FKC_MAX * 12];
   __shared__ __attribute__((aligned(16))) uint32_t Kp[2][FKC_MAX / 2];
+  __shared__ uint32_t Red[3][FNW_MAX];
   const int NW = blockDim.x >> 6, KC = 32 * NW, QB = 16 * NQT * NW;
   const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, c = l & 15;
   const int wg = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -151,6 +153,85 @@ __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(At
   // the output sequence of copy rc: copies past R (R % RC != 0) run as copy R - 1, not stored
   auto seq_of = [&](int rc) { return (int64_t)min(r0 + rc, R - 1) * Bd + b; };
 
+  // operand ranges: powers of two for the f16 splits.  v' = v 2^ev with max |v'| over the
+  // (sequence, head) in [2^14, 2^15) (o unscaled once at the end: relative precision for any
+  // |v|); q' = q 2^-ek, k' = k 2^ek balanced around sqrt(max|q| max|k|), max |q| over the
+  // aligned group of 256 queries holding this workgroup's (whatever the kernel's query block:
+  // the plain and the copies' kernels agree bit for bit), max |k| over the keys (the product,
+  // hence S, unchanged; f16 range for |q|, |k| up to ~2^15 either side of the balance).
+  // Maxima on bit patterns (an unsigned max of |x| is the float max)
+  float xq[NQT][8];
+  uint32_t mq_ = 0u, mk_ = 0u, mv_ = 0u;
+  const uint32_t am = 0x7fffffffu;
+#pragma unroll
+  for (int n = 0; n < NQT; ++n) {
+    const int qc = min(qb * QB + 16 * (NQT * w + n) + c, a.Lq - 1);
+    const float* qp = a.q + (int64_t)b * a.q_bs + (int64_t)qc * a.q_ls + h * 8;
+    const float4 x0 = *reinterpret_cast<const float4*>(qp);
+    const float4 x1 = *reinterpret_cast<const float4*>(qp + 4);
+    const float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+    for (int f = 0; f < 8; ++f) xq[n][f] = x[f];
+  }
+  for (int i = (qb * QB & ~255) + t; i < min((qb * QB & ~255) + 256, a.Lq); i += blockDim.x) {
+    const float* qp = a.q + (int64_t)b * a.q_bs + (int64_t)i * a.q_ls + h * 8;
+    const float4 x0 = *reinterpret_cast<const float4*>(qp), x1 = *reinterpret_cast<const float4*>(qp + 4);
+    mq_ = max(mq_, max(max(max(as_u(x0.x) & am, as_u(x0.y) & am), max(as_u(x0.z) & am, as_u(x0.w) & am)),
+                       max(max(as_u(x1.x) & am, as_u(x1.y) & am), max(as_u(x1.z) & am, as_u(x1.w) & am))));
+  }
+  for (int i0 = 0; i0 < a.Lk; i0 += 4 * (int)blockDim.x) {   // four rows a thread: one round trip
+    float4 kx[4][2], vx[4][2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = min(i0 + j * (int)blockDim.x + t, a.Lk - 1);   // (repeats: max unchanged)
+      kx[j][0] = *reinterpret_cast<const float4*>(kg + i * a.k_ls);
+      kx[j][1] = *reinterpret_cast<const float4*>(kg + i * a.k_ls + 4);
+      vx[j][0] = *reinterpret_cast<const float4*>(vg + i * a.v_ls);
+      vx[j][1] = *reinterpret_cast<const float4*>(vg + i * a.v_ls + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        mk_ = max(mk_, max(max(as_u(kx[j][u].x) & am, as_u(kx[j][u].y) & am),
+                           max(as_u(kx[j][u].z) & am, as_u(kx[j][u].w) & am)));
+        mv_ = max(mv_, max(max(as_u(vx[j][u].x) & am, as_u(vx[j][u].y) & am),
+                           max(as_u(vx[j][u].z) & am, as_u(vx[j][u].w) & am)));
+      }
+  }
+  {
+    const float mq0 = wave_max(__uint_as_float(mq_)), mk0 = wave_max(__uint_as_float(mk_)),
+                mv0 = wave_max(__uint_as_float(mv_));
+    if (l == 0) {
+      Red[0][w] = as_u(mq0);
+      Red[1][w] = as_u(mk0);
+      Red[2][w] = as_u(mv0);
+    }
+  }
+  __syncthreads();
+  int ev = 0, ek = 0;
+  {
+    float mq = 0.f, mk = 0.f, mv = 0.f;
+    for (int i = 0; i < NW; ++i) {
+      mq = fmaxf(mq, __uint_as_float(Red[0][i]));
+      mk = fmaxf(mk, __uint_as_float(Red[1][i]));
+      mv = fmaxf(mv, __uint_as_float(Red[2][i]));
+    }
+    int e;
+    if (mv > 0.f && isfinite(mv)) {
+      frexpf(mv, &e);                                   // mv = m 2^e, m in [0.5, 1)
+      ev = max(-100, min(100, 15 - e));
+    }
+    mq *= fabsf(a.scale_log2);
+    if (mq > 0.f && mk > 0.f && isfinite(mq) && isfinite(mk)) {
+      int eq;
+      frexpf(mq, &eq);
+      frexpf(mk, &e);
+      ek = max(-60, min(60, (eq - e) / 2));
+    }
+  }
+  const float fk = ldexpf(1.f, ek), fv = ldexpf(1.f, ev);
+
   // resident Q operands (term g of lane group g), running state
   u4 Qop[NQT];
   f4 Cm[NQT], O[NQT][RC];
@@ -160,12 +241,10 @@ __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(At
   for (int n = 0; n < NQT; ++n) {
     const int q = qb * QB + 16 * (NQT * w + n) + c;
     const int qc = min(q, a.Lq - 1);
-    const float* qp = a.q + (int64_t)b * a.q_bs + (int64_t)qc * a.q_ls + h * 8;
-    const float4 x0 = *reinterpret_cast<const float4*>(qp);
-    const float4 x1 = *reinterpret_cast<const float4*>(qp + 4);
-    const float s = a.scale_log2;
-    const float x[8] = {x0.x * s, x0.y * s, x0.z * s, x0.w * s,
-                        x1.x * s, x1.y * s, x1.z * s, x1.w * s};
+    const float s = ldexpf(a.scale_log2, -ek);
+    float x[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) x[f] = xq[n][f] * s;
     u4 hi, lo;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -184,37 +263,47 @@ __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(At
       rk[n][rc] = DROP ? attn_row_key(skey, (uint32_t)((seq_of(rc) * a.H + h) * a.Lq + qc)) : 0u;
     }
   }
-  // K image term of lane group g: hi, hi, lo, bias
-  const int toff = g == 2 ? 4 : (g == 3 ? 8 : 0);
+  // K image term of lane group g: hi, hi, lo, bias (lo / bias swapped for keys 4..11 of a
+  // tile: the upper lane groups' reads conflict-free)
+  const int ksw = ((c + 4) >> 3) & 1;
+  const int toff = g == 2 ? 4 + 4 * ksw : (g == 3 ? 8 - 4 * ksw : 0);
 
-  // staging item: key kk_i of the chunk, features 4 hf .. 4 hf + 3
-  const int kk_i = t >> 1, hf = t & 1;
-  float4 rK = make_float4(0.f, 0.f, 0.f, 0.f), rV = rK;
+  // staging items: K of key kk_i of the chunk, features 4 hf .. 4 hf + 3; V of keys
+  // 32 w + 2 vp + {0, 1}, features 2 vf, 2 vf + 1 (one pair word per V^T row written)
+  const int kk_i = t >> 1, hf = t & 1, vp = l & 15, vf = l >> 4;
+  float4 rK = make_float4(0.f, 0.f, 0.f, 0.f);
+  float2 rV0 = make_float2(0.f, 0.f), rV1 = rV0;
   float rB = 0.f;
   auto issue = [&](int ks) {
     const int key = ks + kk_i;
     const bool ok = key < a.Lk;
     const int64_t kc = min(key, a.Lk - 1);
     rK = ok ? *reinterpret_cast<const float4*>(kg + kc * a.k_ls + 4 * hf) : make_float4(0.f, 0.f, 0.f, 0.f);
-    rV = ok ? *reinterpret_cast<const float4*>(vg + kc * a.v_ls + 4 * hf) : make_float4(0.f, 0.f, 0.f, 0.f);
     rB = ok ? (kbg ? kbg[key] : 0.f) : -INFINITY;
+    const int v0 = ks + 32 * w + 2 * vp;
+    const int64_t vc0 = min(v0, a.Lk - 1), vc1 = min(v0 + 1, a.Lk - 1);
+    rV0 = v0 < a.Lk ? *reinterpret_cast<const float2*>(vg + vc0 * a.v_ls + 2 * vf) : make_float2(0.f, 0.f);
+    rV1 = v0 + 1 < a.Lk ? *reinterpret_cast<const float2*>(vg + vc1 * a.v_ls + 2 * vf) : make_float2(0.f, 0.f);
+    rK = make_float4(rK.x * fk, rK.y * fk, rK.z * fk, rK.w * fk);
+    rV0 = make_float2(rV0.x * fv, rV0.y * fv);
+    rV1 = make_float2(rV1.x * fv, rV1.y * fv);
   };
   auto commit = [&](int ks, int buf) {
     uint32_t* K_ = Ki[buf] + kk_i * 12;
     const uint32_t h0 = pk_hi(rK.x, rK.y), h1 = pk_hi(rK.z, rK.w);
     *reinterpret_cast<uint2*>(K_ + 2 * hf) = make_uint2(h0, h1);
-    *reinterpret_cast<uint2*>(K_ + 4 + 2 * hf) = make_uint2(pk_lo(rK.x, rK.y, h0), pk_lo(rK.z, rK.w, h1));
-    *reinterpret_cast<uint2*>(K_ + 8 + 2 * hf) = make_uint2(hf == 0 ? pack2(f16_hi(rB), f16_lo(rB)) : 0u, 0u);
-    // V^T: pair pp, slot of key kq in it: 8 gg + 4 tt + jj (kq = 16 tt + 4 gg + jj)
-    const int pp = kk_i >> 5, kq = kk_i & 31;
-    const int slot = 8 * ((kq & 15) >> 2) + 4 * (kq >> 4) + (kq & 3);
-    _Float16* V_ = reinterpret_cast<_Float16*>(Vi[buf]) + pp * 512 + slot;
-    const float v4[4] = {rV.x, rV.y, rV.z, rV.w};
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      V_[(4 * hf + f) * 32] = f16_hi(v4[f]);
-      V_[(8 + 4 * hf + f) * 32] = f16_lo(v4[f]);
-    }
+    const int kx = 4 * (((kk_i + 4) >> 3) & 1);
+    *reinterpret_cast<uint2*>(K_ + 4 + kx + 2 * hf) = make_uint2(pk_lo(rK.x, rK.y, h0), pk_lo(rK.z, rK.w, h1));
+    *reinterpret_cast<uint2*>(K_ + 8 - kx + 2 * hf) = make_uint2(hf == 0 ? pack2(f16_hi(rB), f16_lo(rB)) : 0u, 0u);
+    // V^T of pair w: slot of key kq in it 8 gg + 4 tt + jj (kq = 16 tt + 4 gg + jj); keys
+    // 2 vp, 2 vp + 1 are neighbouring slots: one word per row (hi rows 2 vf, 2 vf + 1, lo + 8)
+    const int kq = 2 * vp;
+    uint32_t* V_ = Vi[buf] + w * 384 + (8 * ((kq & 15) >> 2) + 4 * (kq >> 4) + (kq & 3)) / 2;
+    const uint32_t v0 = pk_hi(rV0.x, rV1.x), v1 = pk_hi(rV0.y, rV1.y);
+    V_[(2 * vf) * 24] = v0;
+    V_[(2 * vf + 1) * 24] = v1;
+    V_[(8 + 2 * vf) * 24] = pk_lo(rV0.x, rV1.x, v0);
+    V_[(9 + 2 * vf) * 24] = pk_lo(rV0.y, rV1.y, v1);
     if (DROP && hf == 0 && (kk_i & 1) == 0)
       Kp[buf][kk_i >> 1] = attn_keypair_mix(skey, (uint32_t)((ks + kk_i) >> 1));
   };
@@ -233,7 +322,7 @@ __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(At
       if (ks + 32 * p >= a.Lk) break;
       const u4 A0 = ldu4(K_ + (32 * p + c) * 12 + toff);
       const u4 A1 = ldu4(K_ + (32 * p + 16 + c) * 12 + toff);
-      const u4 VT = ldu4(V_ + p * 256 + c * 16 + g * 4);
+      const u4 VT = ldu4(V_ + p * 384 + c * 24 + g * 4);
       f4 S0[NQT], S1[NQT];
 #pragma unroll
       for (int n = 0; n < NQT; ++n) {
@@ -346,7 +435,7 @@ __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(At
     __syncthreads();
   }
   // rows f (lane groups 0, 1) + rows f + 8 (groups 2, 3); l over the column's four groups
-  const float ik = DROP ? a.inv_keep : 1.f;
+  const float ik = ldexpf(DROP ? a.inv_keep : 1.f, -ev);     // and v' = v 2^ev back
 #pragma unroll
   for (int n = 0; n < NQT; ++n) {
     const float lt = xsum16(xsum32(lsum[n]));
@@ -397,6 +486,12 @@ constexpr int SC_WORDS = 368;
 __device__ __forceinline__ int sc_at(int r, int j) {
   return r * 8 + 2 * (j ^ ((r >> 3) & 3)) + 16 * (r >> 2);
 }
+
+// Transposed A-operand images (K^T, Q^T, dO'^T: 16 rows of 32 f16, 16 dwords): the 4-dword
+// chunk g of row r sits at chunk g ^ tsw(r), so the operand reads (ds_read_b128, 16-lane
+// groups over 64 banks: rows c, c + 4 of one chunk collide at the plain 16-dword stride) are
+// conflict-free
+__device__ __forceinline__ int tsw(int r) { return (r >> 1) & 2; }
 
 template <bool DROP>
 __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int nkb, int NT8, int Lqp) {
@@ -495,7 +590,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
       for (int e = 0; e < 2; ++e) {
         const int f = 2 * g + e;
         const _Float16 kh = f16_hi(kr[f]), kl = f16_lo(kr[f]);
-        _Float16* row = KT_ + tt * 512 + f * 32 + 8 * gs + jb;
+        _Float16* row = KT_ + tt * 512 + f * 32 + 8 * (gs ^ tsw(f)) + jb;
         row[0] = kh;                 // (hi row, prec 0)
         row[2] = kh;                 // (hi row, prec 1)
         row[8 * 32] = kl;            // (lo row, prec 0)
@@ -605,7 +700,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
     for (int e = 0; e < 4; ++e) {
       const int f = f0 + e;
       const _Float16 xh = f16_hi(x[e]), xl = f16_lo(x[e]);
-      _Float16* row = T_ + f * 32 + 8 * gs + j0;
+      _Float16* row = T_ + f * 32 + 8 * (gs ^ tsw(f)) + j0;
       row[0] = xh;
       row[4] = xh;
       row[8 * 32] = xl;
@@ -645,8 +740,8 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
     if (ntile > 0) {
       const u4 QA = ldu4(Qa[buf] + c * 12 + (g == 2 ? 4 : (g == 3 ? 8 : 0)));
       const u4 DA = ldu4(Da[buf] + c * 12 + (g == 2 ? 4 : (g == 3 ? 8 : 0)));
-      const u4 QTA = ldu4(QT[buf] + c * 16 + 4 * g);
-      const u4 DTA = ldu4(DT[buf] + c * 16 + 4 * g);
+      const u4 QTA = ldu4(QT[buf] + c * 16 + 4 * (g ^ tsw(c)));
+      const u4 DTA = ldu4(DT[buf] + c * 16 + 4 * (g ^ tsw(c)));
       const f4 CS = *reinterpret_cast<const f4*>(Cs_l + q0 + 4 * g);
       const f4 CD = *reinterpret_cast<const f4*>(Cd_l + q0 + 4 * g);
 #pragma unroll
@@ -694,7 +789,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
               (__attribute__((address_space(3))) s4*)(sc + sc_at(8 * g + 4 + rq, cp)));
           const u4 Bq = {__builtin_bit_cast(uint2, r0).x, __builtin_bit_cast(uint2, r0).y,
                          __builtin_bit_cast(uint2, r1).x, __builtin_bit_cast(uint2, r1).y};
-          const u4 KA = ldu4(KTi + (w * BKT + tt) * 256 + c * 16 + 4 * g);
+          const u4 KA = ldu4(KTi + (w * BKT + tt) * 256 + c * 16 + 4 * (g ^ tsw(c)));
           dQa = mma(KA, Bq, dQa);
         }
       }
@@ -870,7 +965,7 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
     for (int e = 0; e < 2; ++e) {
       const int f = 2 * g + e;
       const _Float16 kh = f16_hi(kr[f]), kl = f16_lo(kr[f]);
-      _Float16* row = KT_ + tt * 512 + f * 32 + 8 * gs + jb;
+      _Float16* row = KT_ + tt * 512 + f * 32 + 8 * (gs ^ tsw(f)) + jb;
       row[0] = kh;
       row[2] = kh;
       row[8 * 32] = kl;
@@ -989,7 +1084,7 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
       for (int e = 0; e < 4; ++e) {
         const int f = 4 * shf + e;
         const _Float16 xh = f16_hi(x[e]), xl = f16_lo(x[e]);
-        _Float16* row = T_ + f * 32 + 8 * gs + j0;
+        _Float16* row = T_ + f * 32 + 8 * (gs ^ tsw(f)) + j0;
         row[0] = xh;
         row[4] = xh;
         row[8 * 32] = xl;
@@ -1010,7 +1105,7 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
         for (int e = 0; e < 4; ++e) {
           const int f = 4 * shf + e;
           const _Float16 xh = f16_hi(x[e]), xl = f16_lo(x[e]);
-          _Float16* row = T_ + f * 32 + 8 * gs + j0;
+          _Float16* row = T_ + f * 32 + 8 * (gs ^ tsw(f)) + j0;
           row[0] = xh;
           row[4] = xh;
           row[8 * 32] = xl;
@@ -1077,7 +1172,7 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
         for (int rc = 0; rc < ng; ++rc) {
           const u4 kw = words(rc);
           const u4 DA = ldu4(Ca + (rc * 16 + c) * 12 + dtoff);
-          const u4 DT = ldu4(Ct + rc * 256 + c * 16 + 4 * g);
+          const u4 DT = ldu4(Ct + rc * 256 + c * 16 + 4 * (g ^ tsw(c)));
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int tt = 4 * hh + u;
@@ -1105,7 +1200,7 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
           issue((st + 1) / ngrp, (st + 1) % ngrp);
           issued = true;
         }
-        const u4 QTA = ldu4(QT + c * 16 + 4 * g);
+        const u4 QTA = ldu4(QT + c * 16 + 4 * (g ^ tsw(c)));
         const f4 CD = gi == 0 ? *reinterpret_cast<const f4*>(Cd_l + ql + 4 * g) : splat(0.f);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -1138,7 +1233,7 @@ __global__ __launch_bounds__(512, 2) void attn_rep_bwd_sf16_kernel(AttnArgs a, i
               (__attribute__((address_space(3))) s4*)(sc + sc_at(8 * g + 4 + rq, cp)));
           const u4 Bq = {__builtin_bit_cast(uint2, x0).x, __builtin_bit_cast(uint2, x0).y,
                          __builtin_bit_cast(uint2, x1).x, __builtin_bit_cast(uint2, x1).y};
-          const u4 KA = ldu4(KTi + (w * BKT + tt) * 256 + c * 16 + 4 * g);
+          const u4 KA = ldu4(KTi + (w * BKT + tt) * 256 + c * 16 + 4 * (g ^ tsw(c)));
           dQa = mma(KA, Bq, dQa);
         }
       }
