@@ -295,7 +295,8 @@ def _rocprof_avg_ms(kernel_prefix):
 def _sq_valu(kernel, scores):
     """VALU issue model of a roofline kernel from the committed SQ counter passes
     (profiles/<LATEST>/sq_counters.json, written by profiles/sq_json.py from
-    profiles/r06/sq.sh): lane-ops per score = SQ_INSTS_VALU * 64 / scores; issue cycles per
+    profiles/r06/sq.sh): VALU lane-ops per score = (SQ_INSTS_VALU - SQ_INSTS_MFMA) * 64 /
+    scores (SQ_INSTS_VALU counts the MFMAs too: reported apart, per score); issue cycles per
     SIMD = (2 * (VALU - MFMA) + 2 * TRANS + 8 * MFMA) / 1024 SIMDs (each VALU op issues in
     2 cycles on a 64-wide wave, transcendentals take 2 more, a 16x16x32 f16 MFMA 8);
     frac = issue cycles / active cycles (GRBM_GUI_ACTIVE / 8 XCDs); issue-bound ms =
@@ -311,7 +312,8 @@ def _sq_valu(kernel, scores):
     trans = c.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
     cyc = (2 * (valu - mfma) + 2 * trans + 8 * mfma) / 1024
     frac = cyc * 8 / c["GRBM_GUI_ACTIVE"]
-    return dict(valu_ops_per_score=round(valu * 64 / scores, 2),
+    return dict(valu_ops_per_score=round((valu - mfma) * 64 / scores, 2),
+                mfma_insts_per_256_scores=round(mfma * 256 / scores, 3),
                 valu_issue_frac=round(frac, 3),
                 valu_issue_bound_ms=round(frac * k["launch_us_pass1"] * 1e-3, 4),
                 sq_launch_ms=round(k["launch_us_pass1"] * 1e-3, 4),
