@@ -21,7 +21,12 @@ KERNELS = {
     # the split-f16 kernels (r05): backward one 512-thread block (8 waves x 128 keys) per
     # (sequence, head); forward one 256-thread block per 256 queries of it
     "attn_bwd_sf16_kernel": ("attn_bwd_sf16_kernel<true>", N * H * 512),
-    "attn_fwd_sf16_kernel": ("attn_fwd_sf16_kernel<true>", N * H * 4 * 256),
+    # r06: the forward is templated on query tiles per wave and copies per workgroup
+    "attn_fwd_sf16_kernel": ("attn_fwd_sf16_kernel<4, 1, true>", N * H * 4 * 256),
+    # the decoders' block 1 on the matrix cores (r06): the launch shape with the most
+    # time in the trace (the spectra decoder's 982 tokens)
+    "attn_rep_fwd_sf16": ("attn_fwd_sf16_kernel<1, 16, true>", None),
+    "attn_rep_bwd_sf16": ("attn_rep_bwd_sf16_kernel<true>", None),
 }
 
 
@@ -47,9 +52,20 @@ def main(path, out):
     res = {}
     rows = replayed_step_rows(list(csv.DictReader(open(path))))
     for key, (inst, gx) in KERNELS.items():
-        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in rows
-                if inst in r["Kernel_Name"] and int(r["Grid_Size_X"]) == gx
-                and int(r.get("Grid_Size_Y", 1) or 1) == 1]
+        if gx is None:
+            by = {}
+            for r in rows:
+                if inst in r["Kernel_Name"]:
+                    by.setdefault(int(r["Grid_Size_X"]), []).append(
+                        (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+            if not by:
+                continue
+            gx = max(by, key=lambda g: sum(by[g]))
+            durs = by[gx]
+        else:
+            durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in rows
+                    if inst in r["Kernel_Name"] and int(r["Grid_Size_X"]) == gx
+                    and int(r.get("Grid_Size_Y", 1) or 1) == 1]
         if durs:
             res[key] = {"instance": inst, "grid": f"{gx}x1", "launches": len(durs),
                         "avg_ms": round(sum(durs) / len(durs), 4)}

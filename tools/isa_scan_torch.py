@@ -9,6 +9,10 @@ v_pk_{fma,mul,add}_f32 with an op_sel bit on a VGPR source.  With --trace <kerne
 it intersects that list with the kernels a rocprofv3 trace of the step ran.
 
     python tools/isa_scan_torch.py [--trace profiles/r05_v2/kernel_stats.csv] [--out f.json]
+    python tools/isa_scan_torch.py --from-json profiles/r06/isa_scan_torch.json --trace T.csv
+(the second form re-matches a trace against a committed scan without rescanning).  Trace
+names match scanned symbols exactly, up to whitespace and a leading "void" (the trace and
+llvm-objdump -C print template closers as "> >" and ">>").
 """
 import argparse
 import concurrent.futures as cf
@@ -91,13 +95,44 @@ def trace_kernels(path):
         return [row["Name"] for row in csv.DictReader(f)]
 
 
+def norm_name(n):
+    n = n.strip()
+    if n.startswith("void "):
+        n = n[5:]
+    return "".join(n.split())
+
+
+def is_aten(n):
+    return "at::native" in n or n.startswith(("void at::", "at::"))
+
+
+def match_trace(bad, names):
+    """the trace's aten kernels and those of them the scan found the form in (exact names)"""
+    aten = [n for n in names if is_aten(n)]
+    idx = {norm_name(k): k for k in bad}
+    hit = {n: bad[idx[norm_name(n)]] for n in aten if norm_name(n) in idx}
+    return aten, hit
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", default=None)
     ap.add_argument("--trace", default=None, help="rocprofv3 kernel_stats.csv of the step")
     ap.add_argument("--out", default=None)
     ap.add_argument("--jobs", type=int, default=8)
+    ap.add_argument("--from-json", default=None, help="a committed scan: match only")
     args = ap.parse_args()
+    if args.from_json:
+        res = json.load(open(args.from_json))
+        if args.trace:
+            aten, hit = match_trace(res["kernels"], trace_kernels(args.trace))
+            res.update(trace=args.trace, trace_aten_kernels=aten, trace_aten_kernels_with_form=hit)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(json.dumps(res, indent=1))
+        print(json.dumps({k: v for k, v in res.items() if k not in ("kernels", "trace_aten_kernels")},
+                         indent=1)[:4000])
+        return
     lib = args.lib or torch_hip_lib()
     bundles = fatbin_bundles(lib)
     bad, nk = {}, 0
@@ -109,16 +144,7 @@ def main():
     res = {"lib": lib, "lib_size": os.path.getsize(lib), "bundles": len(bundles),
            "gfx950_symbols": nk, "kernels_with_form": len(bad)}
     if args.trace:
-        names = trace_kernels(args.trace)
-        aten = [n for n in names if n.startswith(("void at::", "at::", "void (anonymous namespace)::at"))
-                or "at::native" in n]
-        hit = {}
-        for n in aten:
-            core = n.split("(")[0].replace("void ", "").strip()
-            for k in bad:
-                if core and core in k:
-                    hit[n] = bad[k]
-                    break
+        aten, hit = match_trace(bad, trace_kernels(args.trace))
         res["trace"] = args.trace
         res["trace_aten_kernels"] = aten
         res["trace_aten_kernels_with_form"] = hit
