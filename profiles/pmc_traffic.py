@@ -24,7 +24,7 @@ def per_kernel(path, counter):
                       .replace("vaesne::", ""))
         name = name.split("(")[0]
         if name.startswith(KERNELS) and ("<8, 256, 2, true" in name or "_mfma_kernel<true" in name
-                                         or "_sf16_kernel<true>" in name):
+                                         or ("_sf16_kernel<" in name and name.endswith("true>"))):
             vals[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
@@ -39,6 +39,8 @@ def main(fetch, write, label):
            "kernels": {}}
     for inst in sorted(f):
         base = inst.split("<")[0]
+        if "sf16" in inst and inst.count(",") == 2:   # the templated forward: name the instance
+            base = inst.replace(" ", "")
         # the step's instances: the forward that hashes in-kernel (BITSIN = false), the
         # fused backward (DQ = true)
         if inst.startswith("attn_fwd_kernel") and not inst.endswith("false>"):
