@@ -153,9 +153,14 @@ __device__ __forceinline__ uint32_t attn_pair_bits(uint32_t row_key, uint32_t kp
 __device__ __forceinline__ uint32_t attn_keypair_mix(uint32_t key, uint32_t kp) {
   return mix32((key ^ 0x5bd1e995u) ^ (kp * 0x9e3779b9u));
 }
+// r06: the row key enters through the first multiply and the key-pair mix is ADDED after
+// it (one v_mad_u32_u24 instead of an xor and a multiply): 5 vector ops per (row, key pair).
+// Numpy restatement over 4096 rows x 1024 keys: keep rate 0.1001, max |r| 1.4e-3 over 128
+// key lags and 1.1e-3 over 64 row lags, 1.0e-3 for the (row, key) rectangle differences
+// (noise 4.9e-4 per lag; the r05 form: 1.6e-3 / 1.5e-3 / 1.2e-3).  The middle xorshift stays:
+// without it the four decisions of a (row, key) rectangle are additively related.
 __device__ __forceinline__ uint32_t attn_pair_bits_mixed(uint32_t row_key, uint32_t kp_mix) {
-  uint32_t x = row_key ^ kp_mix;
-  x = __umul24(x, 0x9e3779u);
+  uint32_t x = __umul24(row_key, 0x9e3779u) + kp_mix;
   x ^= x >> 13;
   x = __umul24(x, 0x68e31du);
   x ^= x >> 16;
