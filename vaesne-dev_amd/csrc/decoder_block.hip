@@ -1140,6 +1140,60 @@ __global__ __launch_bounds__(NT) void dec_tail_wgrad(Tail a, const float* __rest
   }
 }
 
+// The next block's in_proj gradient (dqkv^T y over the tokens: inputs only) beside the fused
+// backward: the three 32-row slices of one workgroup's tokens together, so each y row is read
+// once (dec_tail_wgrad's J_WN0..2 jobs read it three times); per slice the same tiles in the
+// same order as those jobs (the same sums).
+__global__ __launch_bounds__(NT) void dec_tail_wgrad_wn(Tail a) {
+  __shared__ float red[NW * 1024];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, c = lane & 31;
+  const int chunks = (a.L + a.chunk - 1) / a.chunk;
+  const int seq = blockIdx.x / chunks, ch = blockIdx.x % chunks;
+  const int t0 = ch * a.chunk, t1 = min(a.L, t0 + a.chunk);
+  const int64_t base = (int64_t)seq * a.L, rmax = base + t1;
+  float* out = a.wpart + (int64_t)blockIdx.x * WPART;
+  f16v acc[3] = {{}, {}, {}};
+  float cs[3] = {0.f, 0.f, 0.f};
+  for (int tt = t0 + wave * 32; tt < t1; tt += NW * 32) {   // 64 loads per lane in flight a tile
+    const int64_t r0 = base + tt;
+    float g[3][16], x[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int64_t t = min(r0 + 2 * s + h, rmax - 1);
+      x[s] = a.y[t * E + c];
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) g[cc][s] = a.dqkv[t * 3 * E + cc * E + c];
+    }
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const bool ok = r0 + 2 * s + h < rmax;
+        const float gg = ok ? g[cc][s] : 0.f;
+        cs[cc] += gg;
+        acc[cc] = mfma(gg, ok ? x[s] : 0.f, acc[cc]);
+      }
+  }
+#pragma unroll
+  for (int cc = 0; cc < 3; ++cc) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave * 1024 + F(r, h) * 32 + c] = acc[cc][r];
+    __syncthreads();
+    for (int i = threadIdx.x; i < 1024; i += NT)
+      out[OFF_WN + 1024 * cc + i] = ((red[i] + red[1024 + i]) + red[2048 + i]) + red[3072 + i];
+    __syncthreads();
+    red[threadIdx.x] = cs[cc];
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) sum += red[w * 64 + threadIdx.x] + red[w * 64 + 32 + threadIdx.x];
+      out[OFF_BN + 32 * cc + threadIdx.x] = sum;
+    }
+    __syncthreads();
+  }
+}
+
 // ======================= fused backward (long sequences) =====================
 // One workgroup per sequence runs dec_tail_bwd_data's chain per 32-token tile and
 // does every weight-gradient contraction in place, instead of writing 19
@@ -1750,8 +1804,7 @@ VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* 
     if (a.Wn) {
       Tail b = a;
       b.wpart = wn;
-      hipLaunchKernelGGL(dec_tail_wgrad, dim3(nseq * chunks, 3), dim3(NT), 0, s, b,
-                         (const float*)nullptr, (int)J_WN0);
+      hipLaunchKernelGGL(dec_tail_wgrad_wn, dim3(nseq * chunks), dim3(NT), 0, s, b);
       VAESNE_CHECK_LAUNCH();
     }
     // fused rows: everything but the in_proj-of-next regions
