@@ -82,7 +82,7 @@ def safelog10(x):
 class _Verdicts:
     """Each batch's [loss, posterior flag, loss flag], copied to pinned host memory
     behind the batch's work and read later: the host reads batch i's verdict while
-    batch i+1 runs (one wait per batch, the GPU never idles for it)."""
+    batch i+2 runs (one wait per batch, the GPU never idles for it)."""
 
     def __init__(self, device, slots=4):
         self.cuda = device.type == "cuda"
@@ -222,7 +222,10 @@ def training_step(network, optimizer, data_loader, loss_fn=elbo, multimodal=Fals
             upd.update(skip, flat)        # applied on the device unless a batch was flagged
             last_update[0] = index
             verdicts.push(stat, index)
-            settle(1)                     # the previous batch's verdict, read while this runs
+            # the verdict of the batch before the previous one: two batches stay queued
+            # on the device while the host prepares the next, so host jitter (a slow
+            # collate, a page-in) does not drain the queue at small batches
+            settle(2)
         else:
             verdicts.push(stat, index)
             settle(0)                     # the verdict first, then the optimizer's own step

@@ -519,14 +519,19 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
   const int b = bh / a.H, h = bh - b * a.H;
   const int key0 = kb * KB + 128 * w;
   const int ntile = key0 < a.Lk ? min(BKT, (a.Lk - key0 + 15) / 16) : 0;   // wave-uniform
-  const int nqt = (a.Lq + 15) / 16, Lq16 = 16 * nqt;
+  // query chunk blockIdx.y (a.qchunk > 0: few (sequence, head) pairs; dK / dV partials at
+  // + blockIdx.y * a.dk_ss, summed after the launch): query tiles [it0, it1)
+  const int qc0 = a.qchunk > 0 ? (int)blockIdx.y * a.qchunk : 0;
+  const int it0 = qc0 / 16;
+  const int it1 = a.qchunk > 0 ? min((a.Lq + 15) / 16, (qc0 + a.qchunk) / 16) : (a.Lq + 15) / 16;
+  const int Lq16 = 16 * it1;
   const float* qg = a.q + (int64_t)b * a.q_bs + h * 8;
   const float* dg = a.dout + (int64_t)b * a.do_bs + h * 8;
   const float* og = a.o + (int64_t)b * a.o_bs + h * 8;
 
   // ---- prologue: D, row constants, maxima ----
   float mdo = 0.f, md = 0.f, mv = 0.f;
-  for (int q = t; q < Lq16; q += blockDim.x) {
+  for (int q = 16 * it0 + t; q < Lq16; q += blockDim.x) {
     float D = 0.f, cs = -INFINITY;
     if (q < a.Lq) {
       const float* dp = dg + (int64_t)q * a.do_ls;
@@ -626,7 +631,7 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
   if (Mdo > 0.f && Mv > 0.f && isfinite(Mdo) && isfinite(Mv))
     cs = max(-30, min(30, (int)rintf(0.5f * (log2f(Mv) - log2f(Mdo * sd) - (float)s))));
   const float fdo = ldexpf(sd, s + cs), fv = ldexpf(1.f, -cs), fd = ldexpf(1.f, s);
-  for (int q = t; q < Lq16; q += blockDim.x) Cd_l[q] *= -fd;
+  for (int q = 16 * it0 + t; q < Lq16; q += blockDim.x) Cd_l[q] *= -fd;
   // resident V' operands
 #pragma unroll
   for (int tt = 0; tt < BKT; ++tt) {
@@ -727,15 +732,15 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
     }
   };
 
-  issue(0);
-  u4 kw = words(0);
+  issue(16 * it0);
+  u4 kw = words(16 * it0);
   commit(0);
   __syncthreads();
-  for (int it = 0; it < nqt; ++it) {
-    const int q0 = 16 * it, buf = it & 1;
-    if (it > 0) dq_reduce(q0 - 16, buf ^ 1);
-    if (it + 1 < nqt) issue(q0 + 16);
-    const u4 kwn = it + 1 < nqt ? words(q0 + 16) : (u4){0u, 0u, 0u, 0u};
+  for (int it = it0; it < it1; ++it) {
+    const int q0 = 16 * it, buf = (it - it0) & 1;
+    if (it > it0) dq_reduce(q0 - 16, buf ^ 1);
+    if (it + 1 < it1) issue(q0 + 16);
+    const u4 kwn = it + 1 < it1 ? words(q0 + 16) : (u4){0u, 0u, 0u, 0u};
     f4 dQa = splat(0.f);
     if (ntile > 0) {
       const u4 QA = ldu4(Qa[buf] + c * 12 + (g == 2 ? 4 : (g == 3 ? 8 : 0)));
@@ -799,11 +804,11 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
 #pragma unroll
     for (int r = 0; r < 4; ++r) dq[r] = xsum32(dQa[r]);
     if (g < 2) *reinterpret_cast<f4*>(Qp + buf * NW * 128 + w * 128 + c * 8 + 4 * g) = dq;
-    if (it + 1 < nqt) commit(buf ^ 1);
+    if (it + 1 < it1) commit(buf ^ 1);
     kw = kwn;
     __syncthreads();
   }
-  dq_reduce(16 * (nqt - 1), (nqt - 1) & 1);
+  dq_reduce(16 * (it1 - 1), (it1 - 1 - it0) & 1);
   // dK, dV: rows f + rows f + 8
   const float uk = ldexpf(a.scale / a.scale_log2, -14 - s), uv = ldexpf(1.f, -14 - s - cs);
 #pragma unroll
@@ -817,9 +822,10 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_sf16_kernel(AttnArgs a, int n
       }
       const int key = key0 + 16 * tt + c;
       if (g < 2 && key < a.Lk) {
-        *reinterpret_cast<float4*>(a.dv + (int64_t)b * a.dv_bs + (int64_t)key * a.dv_ls + h * 8 + 4 * g) =
+        const int64_t part = (int64_t)blockIdx.y * a.dk_ss;
+        *reinterpret_cast<float4*>(a.dv + part + (int64_t)b * a.dv_bs + (int64_t)key * a.dv_ls + h * 8 + 4 * g) =
             make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(a.dk + (int64_t)b * a.dk_bs + (int64_t)key * a.dk_ls + h * 8 + 4 * g) =
+        *reinterpret_cast<float4*>(a.dk + part + (int64_t)b * a.dk_bs + (int64_t)key * a.dk_ls + h * 8 + 4 * g) =
             make_float4(k_[0], k_[1], k_[2], k_[3]);
       }
     }
@@ -1305,6 +1311,17 @@ int bwd_blocks(int Lk, int64_t bh) {
   return (Lk + 128 * nw - 1) / (128 * nw);
 }
 int lq_pad(int Lq) { return (Lq + 15) & ~15; }
+// query chunks of a backward launch: while the workgroups' waves would leave SIMDs empty
+// (fewer than 2 per SIMD: 2048), the query axis is cut into chunks of >= 64 queries, each
+// chunk's dK / dV a partial summed after the launch (the encoders' context attention, 64
+// pairs; small batches).  Returns the chunk length (0: one chunk)
+int bwd_qchunk(int Lq, int Lk, int64_t bh) {
+  const int64_t waves = bh * bwd_blocks(Lk, bh) * bwd_waves(Lk, bh);
+  const int tiles = (Lq + 15) / 16;
+  int nqc = (int)std::min<int64_t>((2048 + waves - 1) / waves, tiles / 4);
+  if (nqc <= 1) return 0;
+  return (tiles + nqc - 1) / nqc * 16;
+}
 size_t bwd_lds_bytes(int nw) {
   return (size_t)nw * (BKT * 256 + 2 * SC_WORDS + 2 * 128) * sizeof(uint32_t);
 }
@@ -1351,8 +1368,11 @@ int64_t sf16_bits_bytes(int B, int H, int Lq, int Lk) {
 }
 
 int64_t sf16_bwd_ws_floats(int B, int H, int Lq, int Lk) {
-  const int nkb = bwd_blocks(Lk, (int64_t)B * H);
-  return nkb > 1 ? (int64_t)nkb * B * Lq * H * 8 : 0;
+  const int64_t bh = (int64_t)B * H;
+  const int nkb = bwd_blocks(Lk, bh), qch = bwd_qchunk(Lq, Lk, bh);
+  const int nqc = qch > 0 ? (Lq + qch - 1) / qch : 1;
+  return (nkb > 1 ? (int64_t)nkb * B * Lq * H * 8 : 0) +
+         (nqc > 1 ? 2 * (int64_t)nqc * B * Lk * H * 8 : 0);
 }
 
 int64_t sf16_rep_bwd_ws_floats(int Bd, int H, int L) {
@@ -1396,15 +1416,26 @@ int sf16_bwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s) {
   const int64_t bh = (int64_t)a.B * a.H;
   const int nw = bwd_waves(a.Lk, bh), nkb = bwd_blocks(a.Lk, bh);
   const int E = a.H * 8;
+  const int qch = bwd_qchunk(a.Lq, a.Lk, bh), nqc = qch > 0 ? (a.Lq + qch - 1) / qch : 1;
   AttnArgs c = a;
+  c.qchunk = qch;
+  c.dk_ss = 0;
+  float* wsk = ws;
   if (nkb > 1) {
     if (!ws) return (int)hipErrorInvalidValue;
     c.dq = ws;
     c.dq_bs = (int64_t)a.Lq * E;
     c.dq_ls = E;
     c.dq_ss = (int64_t)a.B * a.Lq * E;
+    wsk = ws + (int64_t)nkb * c.dq_ss;
   }
-  const dim3 grid((unsigned)(bh * nkb));
+  if (nqc > 1) {   // dK / dV partials per query chunk: [nqc][B][Lk][E] each
+    if (!ws) return (int)hipErrorInvalidValue;
+    c.dk_ss = (int64_t)a.B * a.Lk * E;
+    c.dk = wsk; c.dk_bs = (int64_t)a.Lk * E; c.dk_ls = E;
+    c.dv = wsk + (int64_t)nqc * c.dk_ss; c.dv_bs = c.dk_bs; c.dv_ls = E;
+  }
+  const dim3 grid((unsigned)(bh * nkb), (unsigned)nqc);
   static const bool lds_ok = [] {     // dynamic LDS beyond 64 KB (8 waves: 95 KB)
     const int mx = (int)bwd_lds_bytes(BNW_MAX);
     return hipFuncSetAttribute((const void*)attn_bwd_sf16_kernel<true>,
@@ -1424,6 +1455,16 @@ int sf16_bwd(const AttnArgs& a, float p_drop, float* ws, hipStream_t s) {
     const int64_t n = (int64_t)a.B * a.Lq * E;
     hipLaunchKernelGGL(sf16_dq_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ws,
                        c.dq_ss, nkb, a.B, a.Lq, E, a.dq, a.dq_bs, a.dq_ls);
+    VAESNE_CHECK_LAUNCH();
+  }
+  if (nqc > 1) {
+    const int64_t n = (int64_t)a.B * a.Lk * E;
+    const dim3 sg((unsigned)((n + 255) / 256));
+    hipLaunchKernelGGL(sf16_dq_sum_kernel, sg, dim3(256), 0, s, c.dk, c.dk_ss, nqc, a.B, a.Lk, E,
+                       a.dk, a.dk_bs, a.dk_ls);
+    VAESNE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(sf16_dq_sum_kernel, sg, dim3(256), 0, s, c.dv, c.dk_ss, nqc, a.B, a.Lk, E,
+                       a.dv, a.dv_bs, a.dv_ls);
     VAESNE_CHECK_LAUNCH();
   }
   return 0;
