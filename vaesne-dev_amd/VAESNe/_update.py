@@ -10,8 +10,8 @@ and guarded on the device instead:
   * the non-finite flag of VAESNe.guard is STICKY for the whole training_step call
     (cleared once at its start): from the first flagged batch on, every update kernel
     of the call is a no-op;
-  * the host reads each batch's (loss, flags) one batch late, while the next batch
-    runs, and raises there; the host-side bookkeeping of the updates that the device
+  * the host reads each batch's (loss, flags) two batches late, while the next two
+    run, and raises there; the host-side bookkeeping of the updates that the device
     skipped (torch.optim.AdamW's per-parameter `state['step']`) is rolled back, so
     the optimizer is exactly as it was before the flagged batch.
 

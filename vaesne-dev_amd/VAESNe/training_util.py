@@ -28,7 +28,7 @@ NaN / Inf loss on the device.  The flag is cleared once when training_step start
 and stays set from the first flagged batch on; the update is enqueued at once
 behind that device-side skip (VAESNe._update: FusedAdamW, and the scripts' own
 torch.optim.AdamW applied op for op by a HIP kernel on its own state), and the
-host reads each batch's (loss, flags) one batch late, while the next batch runs
+host reads each batch's (loss, flags) two batches late, while the next two run
 (the reference's `.item()`, training_util.py:46).  A flagged batch raises
 RuntimeError there, its update and any later one never applied (the reference
 stops before its update, PhotometricVAE.py:160-161) and the optimizer's host-side
