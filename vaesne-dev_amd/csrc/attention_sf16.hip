@@ -160,6 +160,26 @@ __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(At
   // the plain and the copies' kernels agree bit for bit), max |k| over the keys (the product,
   // hence S, unchanged; f16 range for |q|, |k| up to ~2^15 either side of the balance).
   // Maxima on bit patterns (an unsigned max of |x| is the float max)
+  // staging items: K of key kk_i of the chunk, features 4 hf .. 4 hf + 3; V of keys
+  // 32 w + 2 vp + {0, 1}, features 2 vf, 2 vf + 1 (one pair word per V^T row written).  The
+  // raw rows are loaded here (the first chunk's in flight with the range pass's loads) and
+  // scaled by 2^ek / 2^ev when committed
+  const int kk_i = t >> 1, hf = t & 1, vp = l & 15, vf = l >> 4;
+  float4 rK = make_float4(0.f, 0.f, 0.f, 0.f);
+  float2 rV0 = make_float2(0.f, 0.f), rV1 = rV0;
+  float rB = 0.f;
+  auto issue = [&](int ks) {
+    const int key = ks + kk_i;
+    const bool ok = key < a.Lk;
+    const int64_t kc = min(key, a.Lk - 1);
+    rK = ok ? *reinterpret_cast<const float4*>(kg + kc * a.k_ls + 4 * hf) : make_float4(0.f, 0.f, 0.f, 0.f);
+    rB = ok ? (kbg ? kbg[key] : 0.f) : -INFINITY;
+    const int v0 = ks + 32 * w + 2 * vp;
+    const int64_t vc0 = min(v0, a.Lk - 1), vc1 = min(v0 + 1, a.Lk - 1);
+    rV0 = v0 < a.Lk ? *reinterpret_cast<const float2*>(vg + vc0 * a.v_ls + 2 * vf) : make_float2(0.f, 0.f);
+    rV1 = v0 + 1 < a.Lk ? *reinterpret_cast<const float2*>(vg + vc1 * a.v_ls + 2 * vf) : make_float2(0.f, 0.f);
+  };
+  float fk = 1.f, fv = 1.f;
   float xq[NQT][8];
   uint32_t mq_ = 0u, mk_ = 0u, mv_ = 0u;
   const uint32_t am = 0x7fffffffu;
@@ -173,6 +193,7 @@ __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(At
 #pragma unroll
     for (int f = 0; f < 8; ++f) xq[n][f] = x[f];
   }
+  issue(0);
   for (int i = (qb * QB & ~255) + t; i < min((qb * QB & ~255) + 256, a.Lq); i += blockDim.x) {
     const float* qp = a.q + (int64_t)b * a.q_bs + (int64_t)i * a.q_ls + h * 8;
     const float4 x0 = *reinterpret_cast<const float4*>(qp), x1 = *reinterpret_cast<const float4*>(qp + 4);
@@ -230,7 +251,8 @@ __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(At
       ek = max(-60, min(60, (eq - e) / 2));
     }
   }
-  const float fk = ldexpf(1.f, ek), fv = ldexpf(1.f, ev);
+  fk = ldexpf(1.f, ek);
+  fv = ldexpf(1.f, ev);
 
   // resident Q operands (term g of lane group g), running state
   u4 Qop[NQT];
@@ -268,49 +290,30 @@ __global__ __launch_bounds__(256, fwd_occ(NQT, RC)) void attn_fwd_sf16_kernel(At
   const int ksw = ((c + 4) >> 3) & 1;
   const int toff = g == 2 ? 4 + 4 * ksw : (g == 3 ? 8 - 4 * ksw : 0);
 
-  // staging items: K of key kk_i of the chunk, features 4 hf .. 4 hf + 3; V of keys
-  // 32 w + 2 vp + {0, 1}, features 2 vf, 2 vf + 1 (one pair word per V^T row written)
-  const int kk_i = t >> 1, hf = t & 1, vp = l & 15, vf = l >> 4;
-  float4 rK = make_float4(0.f, 0.f, 0.f, 0.f);
-  float2 rV0 = make_float2(0.f, 0.f), rV1 = rV0;
-  float rB = 0.f;
-  auto issue = [&](int ks) {
-    const int key = ks + kk_i;
-    const bool ok = key < a.Lk;
-    const int64_t kc = min(key, a.Lk - 1);
-    rK = ok ? *reinterpret_cast<const float4*>(kg + kc * a.k_ls + 4 * hf) : make_float4(0.f, 0.f, 0.f, 0.f);
-    rB = ok ? (kbg ? kbg[key] : 0.f) : -INFINITY;
-    const int v0 = ks + 32 * w + 2 * vp;
-    const int64_t vc0 = min(v0, a.Lk - 1), vc1 = min(v0 + 1, a.Lk - 1);
-    rV0 = v0 < a.Lk ? *reinterpret_cast<const float2*>(vg + vc0 * a.v_ls + 2 * vf) : make_float2(0.f, 0.f);
-    rV1 = v0 + 1 < a.Lk ? *reinterpret_cast<const float2*>(vg + vc1 * a.v_ls + 2 * vf) : make_float2(0.f, 0.f);
-    rK = make_float4(rK.x * fk, rK.y * fk, rK.z * fk, rK.w * fk);
-    rV0 = make_float2(rV0.x * fv, rV0.y * fv);
-    rV1 = make_float2(rV1.x * fv, rV1.y * fv);
-  };
   auto commit = [&](int ks, int buf) {
     uint32_t* K_ = Ki[buf] + kk_i * 12;
-    const uint32_t h0 = pk_hi(rK.x, rK.y), h1 = pk_hi(rK.z, rK.w);
+    const float4 k4 = make_float4(rK.x * fk, rK.y * fk, rK.z * fk, rK.w * fk);
+    const float2 va = make_float2(rV0.x * fv, rV0.y * fv), vb = make_float2(rV1.x * fv, rV1.y * fv);
+    const uint32_t h0 = pk_hi(k4.x, k4.y), h1 = pk_hi(k4.z, k4.w);
     *reinterpret_cast<uint2*>(K_ + 2 * hf) = make_uint2(h0, h1);
     const int kx = 4 * (((kk_i + 4) >> 3) & 1);
-    *reinterpret_cast<uint2*>(K_ + 4 + kx + 2 * hf) = make_uint2(pk_lo(rK.x, rK.y, h0), pk_lo(rK.z, rK.w, h1));
+    *reinterpret_cast<uint2*>(K_ + 4 + kx + 2 * hf) = make_uint2(pk_lo(k4.x, k4.y, h0), pk_lo(k4.z, k4.w, h1));
     *reinterpret_cast<uint2*>(K_ + 8 - kx + 2 * hf) = make_uint2(hf == 0 ? pack2(f16_hi(rB), f16_lo(rB)) : 0u, 0u);
     // V^T of pair w: slot of key kq in it 8 gg + 4 tt + jj (kq = 16 tt + 4 gg + jj); keys
     // 2 vp, 2 vp + 1 are neighbouring slots: one word per row (hi rows 2 vf, 2 vf + 1, lo + 8)
     const int kq = 2 * vp;
     uint32_t* V_ = Vi[buf] + w * 384 + (8 * ((kq & 15) >> 2) + 4 * (kq >> 4) + (kq & 3)) / 2;
-    const uint32_t v0 = pk_hi(rV0.x, rV1.x), v1 = pk_hi(rV0.y, rV1.y);
+    const uint32_t v0 = pk_hi(va.x, vb.x), v1 = pk_hi(va.y, vb.y);
     V_[(2 * vf) * 24] = v0;
     V_[(2 * vf + 1) * 24] = v1;
-    V_[(8 + 2 * vf) * 24] = pk_lo(rV0.x, rV1.x, v0);
-    V_[(9 + 2 * vf) * 24] = pk_lo(rV0.y, rV1.y, v1);
+    V_[(8 + 2 * vf) * 24] = pk_lo(va.x, vb.x, v0);
+    V_[(9 + 2 * vf) * 24] = pk_lo(va.y, vb.y, v1);
     if (DROP && hf == 0 && (kk_i & 1) == 0)
       Kp[buf][kk_i >> 1] = attn_keypair_mix(skey, (uint32_t)((ks + kk_i) >> 1));
   };
 
   const int nch = (a.Lk + KC - 1) / KC;
   const int Tlast = 2 * ((a.Lk + 31) / 32) - 1;     // last 16-key tile processed (pairs)
-  issue(0);
   commit(0, 0);
   __syncthreads();
   for (int ch = 0; ch < nch; ++ch) {
