@@ -188,6 +188,55 @@ __device__ __forceinline__ void mv(const float* W, const float* b, const float (
 #pragma unroll
   for (int r = 0; r < 16; ++r) y[r] = acc[r];
 }
+// mv on the f16 matrix cores with split products (the attention kernels' scheme,
+// attention_sf16.hip): W and x carried as hi = f16(v), lo = f16(v - hi); y = b + Wh xh + Wl xh
+// + Wh xl with fp32 accumulation (2^-20 relative per product) in six v_mfma_f32_32x32x16_f16
+// instead of sixteen v_mfma_f32_32x32x2_f32 (3/16 of the matrix-core time).  For the decoder
+// tails' forward chain (and its recompute in the backward), whose operands are LayerNorm
+// outputs, attention / cross-attention outputs and GELU values: O(1), inside f16's range
+// (the encoder halves keep mv: the fused encoder chain is pinned to them bit for bit).
+// MFMA K = 16: lane half h carries its own 8 features F(8m + e, h), e = 0..7, of group m in
+// both operands (A: W[o][.], B: x_t[.]), so no cross-lane movement; each dword pairs two
+// features of ONE precision (a dword mixing a hi and a lo product of one value loses the lo)
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t pk_hi16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2v){a, b}, h2v));
+}
+__device__ __forceinline__ uint32_t pk_lo16(float a, float b, uint32_t hi) {
+  const f2v h = __builtin_convertvector(__builtin_bit_cast(h2v, hi), f2v);
+  return pk_hi16(a - h.x, b - h.y);
+}
+__device__ __forceinline__ f16v mfma16(u4v a, u4v b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b),
+                                                c, 0, 0, 0);
+}
+__device__ __forceinline__ void mv16(const float* W, const float* b, const float (&x)[16],
+                                     float (&y)[16], int lane) {
+  const int o = lane & 31, h = lane >> 5;
+  f16v acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = b ? b[F(r, h)] : 0.f;
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    u4v wh, wl, xh, xl;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float w0 = W[o * LP + F(8 * m + 2 * i, h)], w1 = W[o * LP + F(8 * m + 2 * i + 1, h)];
+      wh[i] = pk_hi16(w0, w1);
+      wl[i] = pk_lo16(w0, w1, wh[i]);
+      xh[i] = pk_hi16(x[8 * m + 2 * i], x[8 * m + 2 * i + 1]);
+      xl[i] = pk_lo16(x[8 * m + 2 * i], x[8 * m + 2 * i + 1], xh[i]);
+    }
+    acc = mfma16(wh, xh, acc);
+    acc = mfma16(wl, xh, acc);
+    acc = mfma16(wh, xl, acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) y[r] = acc[r];
+}
 // y (+)= W^T g   (backward data):  y[k] = sum_o W[o][k] g[o]
 __device__ __forceinline__ void mvt(const float* W, const float (&g)[16], f16v& acc, int lane) {
   const int i = lane & 31, h = lane >> 5;
@@ -381,7 +430,7 @@ __global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
     float xin[16], v[16], xh[16], rs;
 #pragma unroll
     for (int r = 0; r < 16; ++r) { v[r] = nO[r]; xin[r] = nX[r]; }
-    mv(S.Wo1, S.bo1, v, v, lane);                          // a1
+    mv16(S.Wo1, S.bo1, v, v, lane);                          // a1
     uint16_t* m16 = reinterpret_cast<uint16_t*>(a.masks) + row * 8 + h;
     const bool keep_masks = DROP && a.masks != nullptr && valid;
     if (DROP) {
@@ -399,9 +448,9 @@ __global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
     for (int r = 0; r < 16; ++r) xin[r] = fmaf(xh[r], S.g1[F(r, h)], S.be1[F(r, h)]);  // x1
     float q[16], c[16], p[H][LC];
     uint32_t km;
-    mv(S.Wq, S.bq, xin, q, lane);
+    mv16(S.Wq, S.bq, xin, q, lane);
     cross_fwd<LC>(S.kv, a.Lc, q, h, site_key(key, 3), row, DROP, a.thr, a.inv_keep, p, km, c);
-    mv(S.Wo2, S.bo2, c, v, lane);                           // a2
+    mv16(S.Wo2, S.bo2, c, v, lane);                           // a2
     if (DROP) {
       float sc[16];
       drop_res_pairs(site_key(key, 1), row, h, a.thr, a.inv_keep, sc);
@@ -415,10 +464,10 @@ __global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
     layernorm(v, rs, xh);
 #pragma unroll
     for (int r = 0; r < 16; ++r) xin[r] = fmaf(xh[r], S.g2[F(r, h)], S.be2[F(r, h)]);  // x2
-    mv(S.W1, S.b1, xin, v, lane);
+    mv16(S.W1, S.b1, xin, v, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = gelu(v[r]);
-    mv(S.W2, S.b2, v, v, lane);                             // f
+    mv16(S.W2, S.b2, v, v, lane);                             // f
     if (DROP) {
       float sc[16];
       drop_res_pairs(site_key(key, 2), row, h, a.thr, a.inv_keep, sc);
@@ -441,7 +490,7 @@ __global__ __launch_bounds__(NT) void dec_tail_fwd(Tail a) {
 #pragma unroll
       for (int cc = 0; cc < 3; ++cc) {
         float o[16];
-        mv(S.Wn + cc * E * LP, S.bn + cc * E, v, o, lane);
+        mv16(S.Wn + cc * E * LP, S.bn + cc * E, v, o, lane);
         if (valid) store_row(a.qkv, row, 3 * E, cc * E, h, o);
       }
     }
@@ -512,7 +561,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     {
       float v[16], t[16], q[16], c[16], p[H][LC];
       load_row(a.O, row, h, t);
-      mv(S.Wo1, S.bo1, t, v, lane);
+      mv16(S.Wo1, S.bo1, t, v, lane);
       load_row(a.x, row, h, t);
       if (DROP && have) {
 #pragma unroll
@@ -534,12 +583,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       // is register-bound)
       if (valid) store_row(SV(V_X1), row, E, 0, h, t);
       park(Pk[wave][0], xh1, lane);
-      mv(S.Wq, S.bq, t, q, lane);
+      mv16(S.Wq, S.bq, t, q, lane);
       if (valid) store_row(SV(V_Q), row, E, 0, h, q);
       cross_fwd<LC>(S.kv, a.Lc, q, h, site_key(key, 3), row, DROP, a.thr, a.inv_keep, p, km, c,
                     have);
       if (valid) store_row(SV(V_C), row, E, 0, h, c);
-      mv(S.Wo2, S.bo2, c, v, lane);
+      mv16(S.Wo2, S.bo2, c, v, lane);
       if (DROP && have) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] *= ((k1 >> r) & 1u) ? a.inv_keep : 0.f;
@@ -557,11 +606,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       for (int r = 0; r < 16; ++r) t[r] = fmaf(xh2[r], S.g2[F(r, h)], S.be2[F(r, h)]);   // x2
       if (valid) store_row(SV(V_X2), row, E, 0, h, t);
       park(Pk[wave][1], xh2, lane);
-      mv(S.W1, S.b1, t, f1, lane);
+      mv16(S.W1, S.b1, t, f1, lane);
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = gelu(f1[r]);
       if (valid) store_row(SV(V_GL), row, E, 0, h, v);
-      mv(S.W2, S.b2, v, v, lane);
+      mv16(S.W2, S.b2, v, v, lane);
       if (DROP && have) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] *= ((k2 >> r) & 1u) ? a.inv_keep : 0.f;
@@ -1288,7 +1337,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       load_row(a.O, row, h, t);
       load_row(a.x, row, h, xr);   // in flight with O's row (one HBM round trip)
       put_fl(tO, t, lane);    // read back at the tile's end (the dW_o1 operand): LDS, not HBM
-      mv(S.Wo1, S.bo1, t, v, lane);
+      mv16(S.Wo1, S.bo1, t, v, lane);
 #pragma unroll
       for (int r = 0; r < 16; ++r) t[r] = xr[r];
       if (DROP && have) {
@@ -1308,12 +1357,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
       for (int r = 0; r < 16; ++r) t[r] = fmaf(xh1[r], S.g1[F(r, h)], S.be1[F(r, h)]);   // x1
       put_fl(tX1, t, lane);
-      mv(S.Wq, S.bq, t, q, lane);
+      mv16(S.Wq, S.bq, t, q, lane);
       put_fl(tQ, q, lane);
       cross_fwd<LC>(S.kv, a.Lc, q, h, site_key(key, 3), row, DROP, a.thr, a.inv_keep, p, km, c,
                     have);
       put_fl(tC, c, lane);
-      mv(S.Wo2, S.bo2, c, v, lane);
+      mv16(S.Wo2, S.bo2, c, v, lane);
       if (DROP && have) {
         const uint32_t kk = opaque(k1);
 #pragma unroll
@@ -1331,11 +1380,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
       for (int r = 0; r < 16; ++r) t[r] = fmaf(xh2[r], S.g2[F(r, h)], S.be2[F(r, h)]);   // x2
       put_fl(tX2, t, lane);
-      mv(S.W1, S.b1, t, f1, lane);
+      mv16(S.W1, S.b1, t, f1, lane);
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = gelu(f1[r]);
       put_fl(tGL, v, lane);
-      mv(S.W2, S.b2, v, v, lane);
+      mv16(S.W2, S.b2, v, v, lane);
       if (DROP && have) {
         const uint32_t kk = opaque(k2);
 #pragma unroll
