@@ -120,6 +120,8 @@ class TorchAdamWUpdater(Updater):
         self._bkey = None      # identity key of the last validated batch (_batch)
         self._bval = None
         self._arrays = None    # (identity key, ctypes arrays) of the last launch (update)
+        self._fast = None      # steady-state plan of the cached batch (_fast_plan)
+        self._arrays_bkey = None   # the batch key the launch arrays were last checked for
 
     def _batch(self):
         """(params, grads, states) of the tensors torch would update now, or None if
@@ -168,11 +170,71 @@ class TorchAdamWUpdater(Updater):
             self._pending = self._batch()
         return self._pending is not None
 
+    def _fast_plan(self, batch):
+        """Steady state (the cached batch again, every state created, one step count per
+        parameter group, the cached launch arrays built for it): the per-parameter step
+        tensors become views of ONE host tensor, so a batch's host bookkeeping is one add and
+        one read instead of a loop over the parameters.  None when not in that state."""
+        f = self._fast
+        st_of = self.opt.state
+        if f is not None and f["key"] == self._bkey and f["akey"] == self._arrays[0]:
+            if all(st_of[p]["step"] is t for (_, p, _), t in zip(batch, f["steps"])):
+                return f
+        sts = [st_of.get(p) for _, p, _ in batch]
+        # the cached launch arrays must be this batch's (built by the general path for it)
+        if self._bkey is None or self._arrays_bkey != self._bkey or any(not st for st in sts):
+            return None
+        gis = [gi for gi, _, _ in batch]
+        vals = [float(st["step"]) for st in sts]
+        per_group = {}
+        for gi, v in zip(gis, vals):
+            if per_group.setdefault(gi, v) != v:
+                return None
+        order = list(per_group)                         # first appearance: the general path's
+        if tuple(order.index(gi) for gi in gis) != self._arrays[0][5]:   # set numbering
+            return None
+        base = torch.tensor(vals, dtype=torch.float32)
+        steps = []
+        for k, st in enumerate(sts):
+            st["step"] = base[k]          # a view: torch's own step() updates it in place too
+            steps.append(st["step"])
+        self._fast = {"key": self._bkey, "akey": self._arrays[0], "base": base, "steps": steps,
+                      "order": order, "first": [gis.index(gi) for gi in order],
+                      "stepped": [(p, False) for _, p, _ in batch]}
+        return self._fast
+
+    def _fast_update(self, f, skip):
+        base = f["base"]
+        base.add_(1.0)
+        try:
+            vals = base.tolist()
+            groups = self.opt.param_groups
+            coefs = []
+            for gi, k in zip(f["order"], f["first"]):
+                step = vals[k]
+                grp = groups[gi]
+                lr, wd, eps = grp["lr"], grp["weight_decay"], grp["eps"]
+                b1, b2 = grp["betas"]
+                bc1 = 1 - b1 ** step
+                bc2 = 1 - b2 ** step
+                coefs += [1 - lr * wd, 1 - b1, b2, 1 - b2, bc2 ** 0.5, eps, (lr / bc1) * -1, 0.0]
+            pa, ga, ma, va, na, sa = self._arrays[1]
+            _lib.lib.adamw_list(pa, ga, ma, va, na, sa, (C.c_float * len(coefs))(*coefs),
+                                len(f["steps"]), skip, TORCH_FMA, _lib.stream())
+        except BaseException:
+            base.sub_(1.0)                # the step counts never run ahead of launched updates
+            raise
+        self.hist.append(f["stepped"])
+
     def update(self, skip=None, flat=None):
         batch = self._pending
         self._pending = None
         if not batch:
             self.hist.append([])
+            return
+        f = self._fast_plan(batch) if self._arrays is not None else None
+        if f is not None:
+            self._fast_update(f, skip)
             return
         groups = self.opt.param_groups
         ps, gs, ms, vs, ns, sets = [], [], [], [], [], []
@@ -219,6 +281,7 @@ class TorchAdamWUpdater(Updater):
             if self._arrays is None or self._arrays[0] != akey:
                 self._arrays = (akey, (_lib.ptr_array(ps), _lib.ptr_array(gs), _lib.ptr_array(ms),
                                        _lib.ptr_array(vs), (C.c_int64 * n)(*ns), (C.c_int32 * n)(*sets)))
+            self._arrays_bkey = self._bkey
             pa, ga, ma, va, na, sa = self._arrays[1]
             _lib.lib.adamw_list(pa, ga, ma, va, na, sa, (C.c_float * len(coefs))(*coefs), n,
                                 skip, TORCH_FMA, _lib.stream())
