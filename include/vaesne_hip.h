@@ -130,9 +130,12 @@ int vaesne_reduce_partials(const float* partial, int G, int F, float* out0, floa
  * word layout depends on the kernel family the shape takes (dh 8 with Lq > 16:
  * the split-f16 matrix-core kernels; otherwise the packed-VALU ones),
  * the keep decisions themselves do not.
- * workspace (may be null): vaesne_attn_workspace(..., bwd) bytes.  Shapes whose
- * grid cannot fill the chip (the encoder's 983-token context self-attention,
- * B*H = 64) then run as key / query chunks with a fixed-order combine. */
+ * workspace: vaesne_attn_workspace(..., bwd) bytes (may be null when that is 0).
+ * Shapes whose grid cannot fill the chip (the encoder's 983-token context
+ * self-attention, B*H = 64; small batches) run as key / query chunks whose partials
+ * (forward o / lse; backward dQ per key block and, split-f16, dK / dV per query
+ * chunk) it holds, combined in fixed order; such a shape given a null workspace
+ * returns hipErrorInvalidValue. */
 int vaesne_mask_bias(const uint8_t* mask, int64_t n, float* out, void* stream);
 int64_t vaesne_attn_keep_bits_size(int B, int H, int Lq, int Lk);
 int64_t vaesne_attn_workspace(int B, int H, int Lq, int Lk, int dh, int bwd);
