@@ -1700,6 +1700,14 @@ int launch_fwd(const Tail& a, int grid, float*, hipStream_t s) {
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
+// the weight-gradient jobs' token chunk of the two-kernel backward: up to 4 data chunks (the
+// data kernel's chunk fills the CUs with one job; the eleven jobs need fewer, longer
+// workgroups: fewer partial rows and loads in flight per wave)
+int wgrad_chunk(int L, int chunk) { return std::min((L + 127) / 128 * 128, 4 * chunk); }
+int wgrad_grid(int M, int L, int chunk) {
+  const int wc = wgrad_chunk(L, chunk);
+  return (M / L) * ((L + wc - 1) / wc);
+}
 template <int LC, bool NEXT, bool DROP>
 int launch_bwd(const Tail& a, int grid, float* scr, hipStream_t s) {
   if (DROP && !a.masks)
@@ -1709,7 +1717,10 @@ int launch_bwd(const Tail& a, int grid, float* scr, hipStream_t s) {
     hipLaunchKernelGGL((dec_tail_bwd_data<LC, NEXT, DROP, true>), dim3(grid), dim3(NT), 0, s, a,
                        scr);
   VAESNE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(dec_tail_wgrad, dim3(grid, NJOB), dim3(NT), 0, s, a, (const float*)scr, 0);
+  Tail b = a;
+  b.chunk = wgrad_chunk(a.L, a.chunk);
+  const int gw = wgrad_grid(a.M, a.L, a.chunk);
+  hipLaunchKernelGGL(dec_tail_wgrad, dim3(gw, NJOB), dim3(NT), 0, s, b, (const float*)scr, 0);
   VAESNE_CHECK_LAUNCH();
   return 0;
 }
@@ -1878,7 +1889,7 @@ VAESNE_API int vaesne_dec_tail_bwd(const float* x, const float* O, const float* 
   int rc = dispatch<false>(a, grid, scr, s);
   if (rc) return rc;
   if (grid > 1) {
-    rc = sum_tail(MODE_FULL, workspace, grid, gflat, defer, s);
+    rc = sum_tail(MODE_FULL, workspace, wgrad_grid(M, L, a.chunk), gflat, defer, s);
     if (rc) return rc;
   }
   // the context k | v projection backward over the Nseq * Lc context tokens
