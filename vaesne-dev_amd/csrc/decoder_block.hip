@@ -1457,8 +1457,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     {
       f16v acc = {};
       mvt(S.W2, t, acc, lane);
+      // GELU'(x) = 0.5 (1 + erf(x / sqrt2)) + x phi(x) = gelu(x) / x + x phi(x): the
+      // recompute's gelu(x), parked in tGL, instead of a second erf (~28 VALU ops each);
+      // the ratio is well conditioned (0.5 (1 + erf) up to the two roundings), x = 0 -> 1/2
+      const int tl = lane & 31;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) t[r] = acc[r] * gelu_erf_grad(f1[r]);   // df1
+      for (int r = 0; r < 16; ++r) {
+        const float x = f1[r];
+        const float gx = tGL[tl * LT + F(r, h)];
+        const float ratio = x != 0.f ? gx / x : 0.5f;
+        t[r] = acc[r] * fmaf(x * 0.39894228040143268f, __expf(-0.5f * x * x), ratio);   // df1
+      }
     }
     put_fl(tT, t, lane);
     get_op(tT, go, lane);
